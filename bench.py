@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Routing-filter benchmark (BASELINE.json metric: routing_filter build Mkeys/s + probe
+Mkeys/s, device-resident, 24 B keys).
+
+Workload = BASELINE config 2 per GPU: 64M x 24 B keys as 8 filters x 8,000,000 keys (the
+per-filter cap at log_index_size 8 is 8,388,607, src/routing_filter.h:120-127), fp_size
+26, seed 42, sequential-id keys in the reference's filter_test format. One STEP = build all
+8 filters from the device-resident keys (hash -> bucket -> encode -> pack pages) AND probe
+all 64M keys against their filters. value = keys / step time (both phases), whole job.
+
+Multi-GPU: one process per GPU (torchrun); each rank owns a contiguous key range and its
+own 8 filters (SplinterDB filters are per key-range, src/trunk.c:4133-4170), so there is
+no data-path collective: scaling is weak, time = max over ranks, value = all ranks' keys
+/ that time.
+
+CPU baseline (rank 0, N=1): the oracle (oracle/rf_oracle.c, a restatement of the
+reference's routing_filter_add / routing_filter_lookup) on a bounded sample of the same
+workload, one filter per thread like SplinterDB's background tasks.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from splinterdb_amd import engine as E  # noqa: E402
+from splinterdb_amd import keys as K  # noqa: E402
+
+METRIC = "routing_filter build Mkeys/s + probe Mkeys/s, device-resident, 24B keys"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--filters", type=int, default=8)
+    p.add_argument("--keys-per-filter", type=int, default=8_000_000)
+    p.add_argument("--log-index-size", type=int, default=8)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-filters", type=int, default=0, help="sample filters (default = threads)")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    return p.parse_args()
+
+
+def stage_bytes(stage, N, P, image_bytes, slot_bytes, unique):
+    """Algorithmic bytes per launch of each stage (DESIGN.md 'Roofline')."""
+    return {
+        "hash_count": N * 24 + N * 4,          # read keys, write entries
+        "scatter": N * 8,                      # read + write entries
+        "cb_sort": N * 4 + unique * 4,         # read bucketed entries, write sorted unique
+        "assemble": unique * 4 + image_bytes,  # read sorted entries, write pages
+        "probe": P * 24 + P * 8 + image_bytes + slot_bytes,  # SURVEY.md §8(d) probe figure
+    }.get(stage)
+
+
+def cpu_baseline(args, cfg_lis):
+    from oracle import oracle as O
+    threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
+    nf = args.cpu_filters or threads
+    n = args.keys_per_filter
+    keys = K.seq_keys(0, nf * n).reshape(-1)
+    ocfg = O.make_config(log_index_size=cfg_lis)
+    import ctypes
+    starts = np.arange(nf, dtype=np.uint64) * n
+    counts = np.full(nf, n, dtype=np.uint32)
+    keep = (O.Filter * nf)()
+    L = O.lib()
+    t_build = L.rfo_bench_build(ctypes.byref(ocfg), keys.ctypes.data, 24, 1, starts.ctypes.data,
+                                counts.ctypes.data, nf, 0, threads, keep)
+    fid = (np.arange(nf * n, dtype=np.uint64) // n).astype(np.uint32)
+    found = np.zeros(nf * n, dtype=np.uint64)
+    t_probe = L.rfo_bench_probe(ctypes.byref(ocfg), keep, keys.ctypes.data, 24, fid.ctypes.data,
+                                nf * n, threads, found.ctypes.data)
+    ok = bool((found & np.uint64(1)).all())
+    for i in range(nf):
+        L.rfo_filter_release(ctypes.byref(keep[i]))
+    total = nf * n
+    return {
+        "value": total / (t_build + t_probe) / 1e6,
+        "unit": "Mkeys/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{nf} filters x {n} keys (24 B seq ids): hash+routing_filter_add one filter per "
+                  f"thread ({t_build:.2f} s), then routing_filter_lookup of all {total} keys "
+                  f"({t_probe:.2f} s); no false negatives: {ok}",
+        "build_mkeys_s": total / t_build / 1e6,
+        "probe_mkeys_s": total / t_probe / 1e6,
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    F, n = args.filters, args.keys_per_filter
+    N = F * n
+    cfg = E.routing_config_init(fingerprint_size=26, log_index_size=args.log_index_size, seed=42)
+    eng = E.Engine(local)
+    stream = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(stream):
+        # key-range shard of this rank: ids [rank*N, (rank+1)*N)
+        keys = K.seq_keys_torch(rank * N, N, 24, dev)
+        fid = (torch.arange(N, device=dev, dtype=torch.int64) // n).to(torch.int32)
+        found = torch.empty(N, dtype=torch.int64, device=dev)
+    stream.synchronize()
+    batch = E.FilterBatch(cfg, [n] * F, engine=eng)
+    batch.set_timing(True)
+
+    def step():
+        batch.build_keys(keys, 24, stream=stream.cuda_stream)
+        batch.probe_keys(keys, 24, fid, N, found, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    stages = {k: [] for k in E.FilterBatch.STAGES}
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+        for k, v in batch.timings().items():  # waits for this step's events
+            stages[k].append(v)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # ---- verification (outside the timed region) -------------------------------------
+    ok = bool(((found & 1) == 1).all().item())
+    infos = [batch.info(f) for f in range(F)]
+    image_bytes = sum(i.num_pages for i in infos) * cfg.page_size
+    slot_bytes = sum(i.num_indices for i in infos) * 8
+    unique = sum(i.num_unique for i in infos)
+    verified = ok and all(i.error == 0 for i in infos)
+    if rank == 0 and n == 8_000_000 and args.log_index_size == 8:
+        with open(os.path.join(ROOT, "tests", "golden", "sha256.json")) as fh:
+            want = json.load(fh)["seq_n8000000_lis8"]["pages_sha256"]
+        img = batch.image(0)
+        verified = verified and hashlib.sha256(img.pages.tobytes()).hexdigest() == want
+
+    # ---- end-to-end (PCIe-inclusive) rate, reported beside `value` (never as it) ------
+    # keys H2D from pinned host memory -> build -> probe -> found_values + page images +
+    # index slots D2H into pinned host buffers (the clockcache page buffers' stand-in).
+    e2e = None
+    if not args.no_e2e:
+        hk = torch.from_numpy(K.seq_keys(rank * N, N).reshape(-1)).pin_memory()
+        hfound = torch.empty(N, dtype=torch.int64).pin_memory()
+        hpages = [torch.empty(i.num_pages * cfg.page_size, dtype=torch.uint8).pin_memory() for i in infos]
+        hslots = [torch.empty(i.num_indices, dtype=torch.int64).pin_memory() for i in infos]
+        reps = 3
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(reps):
+            with torch.cuda.stream(stream):
+                keys.view(-1).copy_(hk, non_blocking=True)
+            step()
+            with torch.cuda.stream(stream):
+                hfound.copy_(found, non_blocking=True)
+            for f in range(F):
+                batch.read_image_async(f, hpages[f], hslots[f], stream.cuda_stream)
+        stream.synchronize()
+        e2e = N * reps / (time.perf_counter() - te) / 1e6
+        ok_e2e = bool(((hfound & 1) == 1).all().item())
+        verified = verified and ok_e2e
+
+    ms = {k: float(np.mean(v)) for k, v in stages.items()}
+    kern = {}
+    for k in ("hash_count", "scatter", "cb_sort", "cb_sort_big", "layout", "assemble", "cb_scan", "probe"):
+        b = stage_bytes(k, N, N, image_bytes, slot_bytes, unique)
+        kern[k] = {"ms": round(ms[k], 4)}
+        if b:
+            kern[k]["alg_bytes"] = int(b)
+            kern[k]["gbs"] = round(b / (ms[k] * 1e-3) / 1e9, 1) if ms[k] > 0 else None
+    dom = max(("hash_count", "scatter", "cb_sort", "assemble", "probe"), key=lambda k: ms[k])
+    achieved = kern[dom]["gbs"]
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            with open(args.pmc) as fh:
+                pm = json.load(fh)
+            traffic = pm.get("per_launch_hbm_bytes", {}).get(dom)
+        except Exception:
+            traffic = None
+    build_ms, probe_ms = ms["build_total"], ms["probe"]
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * N / (elapsed / args.steps) / 1e6
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Mkeys/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: sequential-id 24 B keys (filter_test format), generated in HBM",
+        "config": {"workload": "C2: 64M x 24B keys per GPU = 8 filters x 8,000,000, build + full probe",
+                   "filters_per_gpu": F, "keys_per_filter": n, "key_len": 24,
+                   "fingerprint_size": 26, "log_index_size": args.log_index_size, "seed": 42,
+                   "parallelism": f"key-range shards, {world} rank(s), no data-path collective"},
+        "build_mkeys_s": round(world * N / (build_ms * 1e-3) / 1e6, 1),
+        "probe_mkeys_s": round(world * N / (probe_ms * 1e-3) / 1e6, 1),
+        "e2e_pcie_mkeys_s": round(e2e, 1) if e2e else None,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic},
+        "kernels": kern,
+        "verified": verified,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(args, args.log_index_size)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = round(value / cb["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    batch.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+/*
+ * rf_amd.h -- C ABI of the MI355X routing-filter engine.
+ *
+ * Drop-in boundary for SplinterDB's routing filter (reference: vmware/splinterdb,
+ * src/routing_filter.h). Plain C types only: device pointers are `void *` / typed
+ * pointers into HIP device memory, streams are `hipStream_t` passed as `void *`.
+ * Errors follow platform_status (src/platform_linux/platform_status.h): 0 = STATUS_OK,
+ * ENOMEM = STATUS_NO_MEMORY, EINVAL = STATUS_BAD_PARAM, ENODEV = no HIP device.
+ *
+ * Filter images are bit-exact with the reference's page bytes (src/routing_filter.c
+ * :599-633 layout, src/PackedArray.c packing). Index slots are RELOCATABLE:
+ * slot = data_page_no * page_size + byte_offset; the integration shim
+ * adds the mini_alloc'd page address, restoring the reference's absolute slot
+ * (src/routing_filter.c:620).
+ */
+#ifndef RF_AMD_H
+#define RF_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RF_AMD_OK        0
+#define RF_AMD_ENOMEM    12
+#define RF_AMD_ENODEV    19
+#define RF_AMD_EINVAL    22
+
+/* per-filter error bits reported in rf_amd_filter_info.error */
+#define RF_AMD_ERR_INDEX_OVERFLOW 1u /* > 4096 entries in one index (ref: fp_buffer overflow, :596) */
+#define RF_AMD_ERR_BLOCK_TOO_BIG  2u /* one index block > page (ref: writes past page, :603-610) */
+#define RF_AMD_ERR_PAGE_CAP       4u /* internal page bound exceeded (never expected)           */
+#define RF_AMD_ERR_GEOMETRY       8u /* invalid geometry                                         */
+
+/* mirrors routing_config (src/routing_filter.h:32-40); key_hash is always XXH32 */
+typedef struct rf_amd_config {
+   uint32_t fingerprint_size; /* 26 (splinterdb.c:147-152, tests/config.c:29) */
+   uint32_t log_index_size;   /* 9 library default, 8 tests                   */
+   uint32_t seed;             /* 42                                           */
+   uint32_t page_size;        /* 4096                                         */
+   uint32_t pages_per_extent; /* 32                                           */
+} rf_amd_config;
+
+/* mirrors the routing_filter descriptor (src/routing_filter.h:66-72) + image geometry */
+typedef struct rf_amd_filter_info {
+   uint32_t num_fingerprints;
+   uint32_t num_unique;
+   uint32_t value_size;
+   uint32_t num_indices;
+   uint32_t num_pages; /* data pages in the image */
+   uint32_t error;     /* RF_AMD_ERR_* bits, 0 on success */
+} rf_amd_filter_info;
+
+typedef struct rf_amd_engine rf_amd_engine;
+typedef struct rf_amd_batch  rf_amd_batch;
+
+/* ---- engine ------------------------------------------------------------------------ */
+int         rf_amd_engine_create(int device, rf_amd_engine **out);
+void        rf_amd_engine_destroy(rf_amd_engine *e);
+const char *rf_amd_last_error(void);
+
+/* ---- batched device-resident build (the throughput path) ----------------------------
+ * A batch = F independent filters, filter f built from the f-th run of `num_new[f]`
+ * inputs (runs concatenated in filter order), tagged with value[f]. This coalesces the
+ * concurrent routing_filter_add calls SplinterDB issues from its TASK_TYPE_NORMAL
+ * workers (src/trunk.c:3821-3835) into one launch sequence. `old` (may be NULL) gives,
+ * per filter, a previously built filter (batch, index) whose entries are merged in
+ * (routing_filter_add's old_filter, src/routing_filter.c:355-368, 496-544); pass
+ * old_batch[f] = NULL for a fresh filter.
+ */
+int rf_amd_batch_create(rf_amd_engine *e, const rf_amd_config *cfg, uint32_t num_filters,
+                        const uint32_t *num_new, const uint16_t *value,
+                        rf_amd_batch *const *old_batch, const uint32_t *old_index,
+                        rf_amd_batch **out);
+void rf_amd_batch_destroy(rf_amd_batch *b);
+
+/* inputs are DEVICE pointers; all calls are asynchronous on `stream` (NULL = engine's) */
+int rf_amd_batch_build_keys(rf_amd_batch *b, const void *d_keys, uint32_t key_len,
+                            void *stream);
+int rf_amd_batch_build_var_keys(rf_amd_batch *b, const uint8_t *d_bytes,
+                                const uint64_t *d_offsets, void *stream);
+int rf_amd_batch_build_hashes(rf_amd_batch *b, const uint32_t *d_hashes, void *stream);
+
+/* probes: probe i looks up key i in filter d_filter_id[i]; result = routing_filter_lookup's
+ * found_values bit-vector (src/routing_filter.c:985-1073) */
+int rf_amd_batch_probe_keys(rf_amd_batch *b, const void *d_keys, uint32_t key_len,
+                            const uint32_t *d_filter_id, uint64_t n, uint64_t *d_found,
+                            void *stream);
+int rf_amd_batch_probe_var_keys(rf_amd_batch *b, const uint8_t *d_bytes,
+                                const uint64_t *d_offsets, const uint32_t *d_filter_id,
+                                uint64_t n, uint64_t *d_found, void *stream);
+int rf_amd_batch_probe_hashes(rf_amd_batch *b, const uint32_t *d_hashes,
+                              const uint32_t *d_filter_id, uint64_t n, uint64_t *d_found,
+                              void *stream);
+
+/* synchronising accessors */
+int rf_amd_batch_info(rf_amd_batch *b, uint32_t f, rf_amd_filter_info *out);
+/* copy filter f's image to host: num_pages*page_size bytes and num_indices slots */
+int rf_amd_batch_read_image(rf_amd_batch *b, uint32_t f, uint8_t *h_pages,
+                            uint64_t pages_bytes, uint64_t *h_slots, uint32_t num_slots);
+/* asynchronous D2H of filter f's first pages_bytes of pages and num_slots slots on
+ * `stream` (e.g. into hipHostRegister'ed clockcache page buffers); the caller knows the
+ * sizes from a previous rf_amd_batch_info or sizes by the reservation */
+int rf_amd_batch_read_image_async(rf_amd_batch *b, uint32_t f, void *h_pages, uint64_t pages_bytes,
+                                  void *h_slots, uint32_t num_slots, void *stream);
+/* device pointers of filter f's image (pages, slots) for zero-copy consumers */
+int rf_amd_batch_image_ptrs(rf_amd_batch *b, uint32_t f, void **d_pages, void **d_slots);
+uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
+
+/* per-stage timing with HIP events recorded on the launch stream. Stages of the last
+ * build: 0 hash+histogram, 1 bucket scan, 2 scatter, 3 bucket sort, 4 big-bucket sort,
+ * 5 layout, 6 page assembly, 7 whole build; 8 = last probe kernel. Milliseconds, -1 if a
+ * stage did not run. */
+#define RF_AMD_NUM_TIMINGS 9
+int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
+int rf_amd_batch_timings(rf_amd_batch *b, float *ms, uint32_t n);
+
+/* ---- drop-in single-filter calls on HOST buffers ------------------------------------
+ * rf_amd_filter_add replaces routing_filter_add (src/routing_filter.h:78-85): hashes
+ * (32-bit XXH32 of the keys, as btree_pack produces them, src/btree.c:4020-4024) in,
+ * relocatable image out. `old_pages/old_slots/old_info` describe old_filter (NULL for
+ * NULL_ROUTING_FILTER). Unlike the reference, new_fp_arr is not modified.
+ * The image buffers are allocated with malloc and freed with rf_amd_image_free.
+ */
+typedef struct rf_amd_image {
+   rf_amd_filter_info info;
+   uint8_t           *pages; /* info.num_pages * page_size bytes */
+   uint64_t          *slots; /* info.num_indices slots           */
+} rf_amd_image;
+
+int  rf_amd_filter_add(rf_amd_engine *e, const rf_amd_config *cfg, const rf_amd_image *old_filter,
+                       rf_amd_image *filter, const uint32_t *new_fp_arr, uint64_t num_new_fp,
+                       uint16_t value);
+/* replaces routing_filter_lookup (src/routing_filter.h:87-92) for a batch of hashed keys */
+int  rf_amd_filter_lookup_hashes(rf_amd_engine *e, const rf_amd_config *cfg,
+                                 const rf_amd_image *filter, const uint32_t *hashes, uint64_t n,
+                                 uint64_t *found_values);
+/* keys-in form: hashes each fixed-length key (XXH32, cfg->seed) on the GPU, as
+ * routing_filter_lookup does with data_key_hash (src/routing_filter.c:1011) */
+int  rf_amd_filter_lookup_keys(rf_amd_engine *e, const rf_amd_config *cfg,
+                               const rf_amd_image *filter, const void *keys, uint32_t key_len,
+                               uint64_t n, uint64_t *found_values);
+void rf_amd_image_free(rf_amd_image *img);
+
+/* host-side helpers mirroring routing_filter.h (no GPU work) */
+uint64_t rf_amd_max_fingerprints(const rf_amd_config *cfg);              /* .h:120-127  */
+uint32_t rf_amd_estimate_unique_keys_from_count(const rf_amd_config *cfg,
+                                                uint64_t num_unique);     /* .c:1119-1139 */
+uint64_t rf_amd_space_use_bytes(const rf_amd_config *cfg, uint32_t num_pages); /* .c:1149 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,140 @@
+// rf_device.h -- device-side helpers shared by the routing-filter kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rf {
+
+constexpr int WAVE = 64;
+
+// ---- XXH32 (published xxHash algorithm; the reference's platform_hash32,
+//      src/platform_linux/platform_hash.h:23) ----------------------------------------
+constexpr uint32_t XP1 = 2654435761U, XP2 = 2246822519U, XP3 = 3266489917U,
+                   XP4 = 668265263U, XP5 = 374761393U;
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) {
+  return __builtin_rotateleft32(x, r);
+}
+__device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t in) {
+  return rotl32(acc + in * XP2, 13) * XP1;
+}
+__device__ __forceinline__ uint32_t xavalanche(uint32_t h) {
+  h ^= h >> 15; h *= XP2; h ^= h >> 13; h *= XP3; h ^= h >> 16;
+  return h;
+}
+
+// 24-byte key held as 6 little-endian words (the filter_test / BASELINE key format)
+__device__ __forceinline__ uint32_t xxh32_24(const uint32_t w[6], uint32_t seed) {
+  uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+  v1 = xround(v1, w[0]); v2 = xround(v2, w[1]); v3 = xround(v3, w[2]); v4 = xround(v4, w[3]);
+  uint32_t h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+  h += 24u;
+  h = rotl32(h + w[4] * XP3, 17) * XP4;
+  h = rotl32(h + w[5] * XP3, 17) * XP4;
+  return xavalanche(h);
+}
+
+// Generic length, 4-byte aligned base: word loads.
+__device__ __forceinline__ uint32_t xxh32_words(const uint32_t* p, uint32_t len, uint32_t seed) {
+  uint32_t h, i = 0;
+  if (len >= 16) {
+    uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+    uint32_t nstripe = len / 16;
+    for (uint32_t s = 0; s < nstripe; s++) {
+      v1 = xround(v1, p[4 * s]); v2 = xround(v2, p[4 * s + 1]);
+      v3 = xround(v3, p[4 * s + 2]); v4 = xround(v4, p[4 * s + 3]);
+    }
+    i = nstripe * 16;
+    h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+  } else {
+    h = seed + XP5;
+  }
+  h += len;
+  for (; i + 4 <= len; i += 4) h = rotl32(h + p[i / 4] * XP3, 17) * XP4;
+  if (i < len) {
+    uint32_t w = p[i / 4];
+    for (; i < len; i++) {
+      h = rotl32(h + (w & 0xffu) * XP5, 11) * XP1;
+      w >>= 8;
+    }
+  }
+  return xavalanche(h);
+}
+
+// Arbitrary alignment (variable-length keys): byte loads, assembled little-endian.
+__device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint32_t xxh32_bytes(const uint8_t* p, uint32_t len, uint32_t seed) {
+  uint32_t h, i = 0;
+  if (len >= 16) {
+    uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+    for (; i + 16 <= len; i += 16) {
+      v1 = xround(v1, ld_u32_bytes(p + i)); v2 = xround(v2, ld_u32_bytes(p + i + 4));
+      v3 = xround(v3, ld_u32_bytes(p + i + 8)); v4 = xround(v4, ld_u32_bytes(p + i + 12));
+    }
+    h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+  } else {
+    h = seed + XP5;
+  }
+  h += len;
+  for (; i + 4 <= len; i += 4) h = rotl32(h + ld_u32_bytes(p + i) * XP3, 17) * XP4;
+  for (; i < len; i++) h = rotl32(h + (uint32_t)p[i] * XP5, 11) * XP1;
+  return xavalanche(h);
+}
+
+// ---- scans ------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  const int lane = threadIdx.x & (WAVE - 1);
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, WAVE);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// Block-wide exclusive scan. s_tmp needs NT/64 + 1 words. Returns the exclusive prefix,
+// writes the block total to *total. Contains barriers: call from every thread.
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_tmp, uint32_t* total) {
+  constexpr int NW = NT / WAVE;
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  uint32_t inc = wave_incl_scan(x);
+  if (lane == WAVE - 1) s_tmp[w] = inc;
+  __syncthreads();
+  if (threadIdx.x < WAVE) {
+    uint32_t v = (int)threadIdx.x < NW ? s_tmp[threadIdx.x] : 0u;
+    uint32_t vi = wave_incl_scan(v);
+    if ((int)threadIdx.x < NW) s_tmp[threadIdx.x] = vi - v;
+    if ((int)threadIdx.x == NW - 1) s_tmp[NW] = vi;
+  }
+  __syncthreads();
+  uint32_t r = s_tmp[w] + inc - x;
+  *total = s_tmp[NW];
+  __syncthreads();
+  return r;
+}
+
+// ---- unaligned little-endian reads from filter page bytes (4-byte aligned buffer) -------
+__device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* base, uint64_t byte_off) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base) + (byte_off >> 2);
+  uint32_t sh = (uint32_t)(byte_off & 3) * 8;
+  uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  if (sh == 0) return lo;
+  uint64_t hi = w[2];
+  return (lo >> sh) | (hi << (64 - sh));
+}
+__device__ __forceinline__ uint32_t ld_bits(const uint8_t* base, uint64_t bitpos, uint32_t nbits) {
+  if (nbits == 0) return 0;
+  uint64_t v = ld_u64_unaligned(base, bitpos >> 3) >> (bitpos & 7);
+  return (uint32_t)(v & ((nbits >= 32) ? 0xffffffffull : ((1ull << nbits) - 1)));
+}
+
+// position of the k-th (0-based) set bit of x (requires popcount(x) > k)
+__device__ __forceinline__ uint32_t select64(uint64_t x, uint32_t k) {
+  for (uint32_t i = 0; i < k; i++) x &= x - 1;
+  return (uint32_t)__builtin_ctzll(x);
+}
+
+}  // namespace rf

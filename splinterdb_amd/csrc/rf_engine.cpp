@@ -1,0 +1,656 @@
+// rf_engine.cpp -- host runtime of the MI355X routing-filter engine (C ABI: include/rf_amd.h).
+//
+// Owns device workspaces, builds the per-batch plan (geometry of src/routing_filter.c:
+// 357-389 per filter, plus the coarse-bucket / page-bound bookkeeping of this engine) and
+// issues the kernel sequence of rf_kernels.hip on one HIP stream. No compute happens on
+// the host: there is no CPU fallback, and every entry point fails with ENODEV when no HIP
+// device is present.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rf_amd.h"
+#include "rf_plan.h"
+
+using namespace rf;
+
+extern "C" int rf_launch_build(const LaunchArgs* a);
+extern "C" int rf_launch_old_decode(const LaunchArgs* a, uint32_t f, uint32_t old_num_indices,
+                                    uint32_t* d_cnt, uint32_t* d_pos);
+extern "C" int rf_launch_probe(const LaunchArgs* a, int kind, const void* in0, const uint64_t* offs,
+                               uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found);
+
+static thread_local std::string g_err;
+static int fail(int rc, const std::string& msg) {
+  g_err = msg;
+  return rc;
+}
+#define HIPCHK(x)                                                                     \
+  do {                                                                                \
+    hipError_t _e = (x);                                                              \
+    if (_e != hipSuccess)                                                             \
+      return fail(_e == hipErrorOutOfMemory ? RF_AMD_ENOMEM : RF_AMD_EINVAL,          \
+                  std::string(#x) + ": " + hipGetErrorString(_e));                    \
+  } while (0)
+
+struct rf_amd_engine {
+  int device;
+  hipStream_t stream;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  int alloc(size_t bytes) {
+    n = bytes ? bytes : 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return fail(RF_AMD_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    return 0;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct rf_amd_batch {
+  rf_amd_engine* eng = nullptr;
+  rf_amd_config cfg{};
+  uint32_t F = 0;
+  bool wide = false;
+  std::vector<FilterPlan> plans;
+  std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter;
+  uint64_t E = 0, keys_total = 0;
+  uint32_t CB = 0, I = 0, PS = 0, PF = 0;
+  DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
+      d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
+      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos;
+  std::vector<uint32_t> old_num_indices;
+  bool built = false;
+  std::vector<hipEvent_t> events;  // per-stage timing (rf_amd_batch_set_timing)
+  ~rf_amd_batch() {
+    for (auto ev : events) (void)hipEventDestroy(ev);
+  }
+};
+
+extern "C" const char* rf_amd_last_error(void) { return g_err.c_str(); }
+
+extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return fail(RF_AMD_ENODEV, "no HIP device: the routing-filter engine has no CPU fallback");
+  if (device < 0 || device >= n) return fail(RF_AMD_EINVAL, "bad device ordinal");
+  HIPCHK(hipSetDevice(device));
+  auto* e = new rf_amd_engine{device, nullptr};
+  // a BLOCKING stream: ordered with the legacy null stream that torch and most callers use
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess) {
+    delete e;
+    return fail(RF_AMD_EINVAL, "hipStreamCreate failed");
+  }
+  *out = e;
+  return 0;
+}
+
+extern "C" void rf_amd_engine_destroy(rf_amd_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipStreamSynchronize(e->stream);
+  (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+static int check_cfg(const rf_amd_config* cfg) {
+  if (!cfg) return fail(RF_AMD_EINVAL, "null config");
+  if (cfg->page_size != MAX_PAGE || cfg->pages_per_extent != 32)
+    return fail(RF_AMD_EINVAL, "engine supports 4 KiB pages in 32-page extents");
+  if (cfg->fingerprint_size == 0 || cfg->fingerprint_size > 32 || cfg->log_index_size > MAX_LIS ||
+      cfg->log_index_size < 3)
+    return fail(RF_AMD_EINVAL, "unsupported fingerprint_size / log_index_size");
+  return 0;
+}
+
+static uint32_t vsize_of(uint32_t value) { return value == 0 ? 0 : 32 - __builtin_clz(value); }
+
+extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t num_filters,
+                                   const uint32_t* num_new, const uint16_t* value,
+                                   rf_amd_batch* const* old_batch, const uint32_t* old_index,
+                                   rf_amd_batch** out) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (int rc = check_cfg(cfg)) return rc;
+  if (num_filters == 0 || !num_new || !out) return fail(RF_AMD_EINVAL, "empty batch");
+  HIPCHK(hipSetDevice(e->device));
+  auto* b = new rf_amd_batch();
+  b->eng = e;
+  b->cfg = *cfg;
+  b->F = num_filters;
+  b->plans.resize(num_filters);
+  b->old_num_indices.assign(num_filters, 0);
+  const uint32_t lis = cfg->log_index_size, fps = cfg->fingerprint_size, P = cfg->page_size;
+  const uint32_t IS = 1u << lis;
+  uint64_t e_first = 0, key_first = 0;
+  uint32_t cb_base = 0, idx_base = 0, page_base = 0, pf_base = 0;
+  for (uint32_t f = 0; f < num_filters; f++) {
+    FilterPlan& p = b->plans[f];
+    memset(&p, 0, sizeof(p));
+    const rf_amd_batch* ob = (old_batch && old_batch[f]) ? old_batch[f] : nullptr;
+    const FilterPlan* op = nullptr;
+    if (ob) {
+      const uint32_t oi = old_index ? old_index[f] : 0;
+      if (oi >= ob->F || !ob->built || ob->eng->device != e->device) {
+        delete b;
+        return fail(RF_AMD_EINVAL, "bad old filter reference");
+      }
+      op = &ob->plans[oi];
+      b->wide = true;
+    }
+    const uint32_t v = value ? value[f] : 0;
+    p.num_new = num_new[f];
+    p.old_region = op ? op->num_fp : 0;
+    const uint64_t nfp = (uint64_t)p.num_new + p.old_region;
+    p.num_fp = (uint32_t)nfp;
+    if (p.num_fp == 0) {
+      delete b;
+      return fail(RF_AMD_EINVAL, "routing_filter_add with zero fingerprints (reference: UB)");
+    }
+    uint32_t lnb = 31 - __builtin_clz(p.num_fp);
+    if (lnb < lis) lnb = lis;
+    p.vs = vsize_of(v);
+    if (lnb > fps || (1u << (lnb - lis)) > MAX_INDICES || fps + p.vs > 32 || (op && p.vs < op->vs)) {
+      delete b;
+      return fail(RF_AMD_EINVAL, "filter geometry out of range (over routing_filter_max_fingerprints, "
+                                 "fp_size + value_size > 32, or value narrower than old filter)");
+    }
+    p.lnb = lnb;
+    p.value = v;
+    p.rem = fps - lnb;
+    p.rvs = p.rem + p.vs;
+    p.num_indices = 1u << (lnb - lis);
+    int cb = (int)lnb - (int)CB_LOG_MEAN;
+    if (cb < 0) cb = 0;
+    if (cb > (int)(lnb - lis)) cb = (int)(lnb - lis);
+    p.cbits = (uint32_t)cb;
+    p.bbits = lnb - p.cbits;
+    p.e_first = e_first;
+    p.key_first = key_first;
+    p.cb_base = cb_base;
+    p.idx_base = idx_base;
+    // page bound: sum of block sizes <= NI*(12 + IS/8) + E*(1+rvs)/8; next-fit <= 2x + 1
+    const uint64_t bound = (uint64_t)p.num_indices * (12 + IS / 8) + (nfp * (1 + p.rvs) + 7) / 8;
+    uint64_t cap = 2 * ((bound + P - 1) / P) + 2;
+    if (cap > p.num_indices) cap = p.num_indices;
+    p.page_cap = (uint32_t)cap;
+    p.page_base = page_base;
+    p.pf_base = pf_base;
+    if (op) {
+      p.old_num_indices = op->num_indices;
+      p.old_vs = op->vs;
+      p.old_rvs = op->rvs;
+      p.old_pages = ob->d_pages.as<uint8_t>() + (uint64_t)op->page_base * P;
+      p.old_slots = ob->d_slots.as<uint64_t>() + op->idx_base;
+      b->old_num_indices[f] = op->num_indices;
+    }
+    for (uint32_t s = 0; s < p.num_new; s += TILE_KEYS) {
+      b->tile_filter.push_back(f);
+      b->tile_start.push_back(s);
+    }
+    for (uint32_t s = 0; s < p.old_region; s += TILE_KEYS) {
+      b->old_tile_filter.push_back(f);
+      b->old_tile_start.push_back(s);
+    }
+    for (uint32_t i = 0; i < (1u << p.cbits); i++) b->cb_filter.push_back(f);
+    for (uint32_t i = 0; i < p.page_cap; i++) b->pg_filter.push_back(f);
+    e_first += nfp;
+    key_first += p.num_new;
+    cb_base += 1u << p.cbits;
+    idx_base += p.num_indices;
+    page_base += p.page_cap;
+    pf_base += p.page_cap + 1;
+  }
+  b->E = e_first;
+  b->keys_total = key_first;
+  b->CB = cb_base;
+  b->I = idx_base;
+  b->PS = page_base;
+  b->PF = pf_base;
+  const size_t esz = b->wide ? 8 : 4;
+  int rc = 0;
+  rc |= b->d_plans.alloc(sizeof(FilterPlan) * num_filters);
+  rc |= b->d_outs.alloc(sizeof(FilterOut) * num_filters);
+  rc |= b->d_ent.alloc(esz * b->E + 64);
+  rc |= b->d_part.alloc(esz * b->E + 64);
+  if (b->wide) rc |= b->d_sorted.alloc(4 * b->E + 64);
+  rc |= b->d_cb_count.alloc(4 * b->CB);
+  rc |= b->d_cb_start.alloc(4 * b->CB);
+  rc |= b->d_cb_cursor.alloc(4 * b->CB);
+  rc |= b->d_cb_filter.alloc(4 * b->CB);
+  rc |= b->d_overflow.alloc(4 * (b->CB + 1));
+  rc |= b->d_idx_cnt.alloc(4 * b->I);
+  rc |= b->d_idx_start.alloc(4 * b->I);
+  rc |= b->d_slots.alloc(8 * b->I);
+  rc |= b->d_page_first.alloc(4 * b->PF);
+  rc |= b->d_pg_filter.alloc(4 * b->PS);
+  rc |= b->d_pages.alloc((size_t)b->PS * P + 256);
+  rc |= b->d_tile_filter.alloc(4 * b->tile_filter.size());
+  rc |= b->d_tile_start.alloc(4 * b->tile_start.size());
+  rc |= b->d_old_tile_filter.alloc(4 * b->old_tile_filter.size());
+  rc |= b->d_old_tile_start.alloc(4 * b->old_tile_start.size());
+  if (b->wide) {
+    rc |= b->d_old_cnt.alloc(4 * MAX_INDICES);
+    rc |= b->d_old_pos.alloc(4 * MAX_INDICES);
+  }
+  if (rc) {
+    delete b;
+    return fail(RF_AMD_ENOMEM, "device allocation failed");
+  }
+  hipStream_t st = e->stream;
+#define UP(buf, vec) \
+  if (!(vec).empty()) HIPCHK(hipMemcpyAsync(buf.p, (vec).data(), sizeof((vec)[0]) * (vec).size(), hipMemcpyHostToDevice, st))
+  UP(b->d_plans, b->plans);
+  UP(b->d_tile_filter, b->tile_filter);
+  UP(b->d_tile_start, b->tile_start);
+  UP(b->d_old_tile_filter, b->old_tile_filter);
+  UP(b->d_old_tile_start, b->old_tile_start);
+  UP(b->d_cb_filter, b->cb_filter);
+  UP(b->d_pg_filter, b->pg_filter);
+#undef UP
+  HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
+  HIPCHK(hipStreamSynchronize(st));
+  *out = b;
+  return 0;
+}
+
+extern "C" void rf_amd_batch_destroy(rf_amd_batch* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->eng->device);
+  (void)hipStreamSynchronize(b->eng->stream);
+  delete b;
+}
+
+extern "C" uint32_t rf_amd_batch_num_filters(const rf_amd_batch* b) { return b ? b->F : 0; }
+
+static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
+  LaunchArgs a;
+  memset(&a, 0, sizeof(a));
+  a.stream = st;
+  a.wide = b->wide;
+  a.plans = b->d_plans.as<FilterPlan>();
+  a.num_filters = b->F;
+  a.tile_filter = b->d_tile_filter.as<uint32_t>();
+  a.tile_start = b->d_tile_start.as<uint32_t>();
+  a.num_tiles = (uint32_t)b->tile_filter.size();
+  a.old_tile_filter = b->d_old_tile_filter.as<uint32_t>();
+  a.old_tile_start = b->d_old_tile_start.as<uint32_t>();
+  a.num_old_tiles = (uint32_t)b->old_tile_filter.size();
+  a.fp_size = b->cfg.fingerprint_size;
+  a.seed = b->cfg.seed;
+  a.lis = b->cfg.log_index_size;
+  a.page_size = b->cfg.page_size;
+  a.ent = b->d_ent.p;
+  a.part = b->d_part.p;
+  a.sorted32 = b->wide ? b->d_sorted.as<uint32_t>() : b->d_part.as<uint32_t>();
+  a.cb_count = b->d_cb_count.as<uint32_t>();
+  a.cb_start = b->d_cb_start.as<uint32_t>();
+  a.cb_cursor = b->d_cb_cursor.as<uint32_t>();
+  a.cb_filter = b->d_cb_filter.as<uint32_t>();
+  a.num_cb = b->CB;
+  a.overflow = b->d_overflow.as<uint32_t>();
+  a.idx_cnt = b->d_idx_cnt.as<uint32_t>();
+  a.idx_start = b->d_idx_start.as<uint32_t>();
+  a.slots = b->d_slots.as<uint64_t>();
+  a.page_first = b->d_page_first.as<uint32_t>();
+  a.pg_filter = b->d_pg_filter.as<uint32_t>();
+  a.num_page_slots = b->PS;
+  a.pages = b->d_pages.as<uint8_t>();
+  a.outs = b->d_outs.p ? b->d_outs.as<FilterOut>() : nullptr;
+  a.events = b->events.empty() ? nullptr : reinterpret_cast<void**>(b->events.data());
+  return a;
+}
+
+static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
+                    void* stream) {
+  if (!b) return fail(RF_AMD_EINVAL, "null batch");
+  if (b->keys_total && !in0) return fail(RF_AMD_EINVAL, "null input");
+  HIPCHK(hipSetDevice(b->eng->device));
+  hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  LaunchArgs a = make_args(b, st);
+  a.kind = kind;
+  a.in0 = in0;
+  a.offs = offs;
+  a.key_len = key_len;
+  if (a.events) HIPCHK(hipEventRecord(b->events[EV_B_START], st));
+  HIPCHK(hipMemsetAsync(b->d_cb_count.p, 0, 4 * (size_t)b->CB, st));
+  HIPCHK(hipMemsetAsync(b->d_outs.p, 0, sizeof(FilterOut) * b->F, st));
+  HIPCHK(hipMemsetAsync(b->d_overflow.p, 0, 4, st));
+  if (b->wide) {
+    HIPCHK(hipMemsetAsync(b->d_ent.p, 0xff, b->d_ent.n, st));
+    for (uint32_t f = 0; f < b->F; f++) {
+      if (!b->old_num_indices[f]) continue;
+      int rc = rf_launch_old_decode(&a, f, b->old_num_indices[f], b->d_old_cnt.as<uint32_t>(),
+                                    b->d_old_pos.as<uint32_t>());
+      if (rc) return fail(RF_AMD_EINVAL, std::string("old decode launch: ") + hipGetErrorString((hipError_t)rc));
+    }
+  }
+  int rc = rf_launch_build(&a);
+  if (rc) return fail(RF_AMD_EINVAL, std::string("build launch: ") + hipGetErrorString((hipError_t)rc));
+  b->built = true;
+  return 0;
+}
+
+static int fixed_kind(const void* p, uint32_t key_len) {
+  const uintptr_t u = (uintptr_t)p;
+  if (key_len == 24 && (u & 7) == 0) return IN_KEYS24;
+  if ((key_len & 3) == 0 && (u & 3) == 0) return IN_KEYS_W;
+  return IN_KEYS_B;
+}
+
+extern "C" int rf_amd_batch_build_keys(rf_amd_batch* b, const void* d_keys, uint32_t key_len, void* stream) {
+  if (key_len == 0) return fail(RF_AMD_EINVAL, "key_len 0");
+  return do_build(b, fixed_kind(d_keys, key_len), d_keys, nullptr, key_len, stream);
+}
+extern "C" int rf_amd_batch_build_var_keys(rf_amd_batch* b, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                                           void* stream) {
+  if (!d_offsets) return fail(RF_AMD_EINVAL, "null offsets");
+  return do_build(b, IN_VAR, d_bytes, d_offsets, 0, stream);
+}
+extern "C" int rf_amd_batch_build_hashes(rf_amd_batch* b, const uint32_t* d_hashes, void* stream) {
+  return do_build(b, IN_HASH, d_hashes, nullptr, 4, stream);
+}
+
+static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
+                    const uint32_t* fid, uint64_t n, uint64_t* found, void* stream) {
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "probe on an unbuilt batch");
+  if (n && (!in0 || !fid || !found)) return fail(RF_AMD_EINVAL, "null probe buffer");
+  HIPCHK(hipSetDevice(b->eng->device));
+  hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  LaunchArgs a = make_args(b, st);
+  int rc = rf_launch_probe(&a, kind, in0, offs, key_len, fid, n, found);
+  if (rc) return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
+  return 0;
+}
+
+extern "C" int rf_amd_batch_probe_keys(rf_amd_batch* b, const void* d_keys, uint32_t key_len,
+                                       const uint32_t* d_filter_id, uint64_t n, uint64_t* d_found, void* stream) {
+  if (key_len == 0) return fail(RF_AMD_EINVAL, "key_len 0");
+  return do_probe(b, fixed_kind(d_keys, key_len), d_keys, nullptr, key_len, d_filter_id, n, d_found, stream);
+}
+extern "C" int rf_amd_batch_probe_var_keys(rf_amd_batch* b, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                                           const uint32_t* d_filter_id, uint64_t n, uint64_t* d_found,
+                                           void* stream) {
+  return do_probe(b, IN_VAR, d_bytes, d_offsets, 0, d_filter_id, n, d_found, stream);
+}
+extern "C" int rf_amd_batch_probe_hashes(rf_amd_batch* b, const uint32_t* d_hashes, const uint32_t* d_filter_id,
+                                         uint64_t n, uint64_t* d_found, void* stream) {
+  return do_probe(b, IN_HASH, d_hashes, nullptr, 4, d_filter_id, n, d_found, stream);
+}
+
+extern "C" int rf_amd_batch_set_timing(rf_amd_batch* b, int enable) {
+  if (!b) return fail(RF_AMD_EINVAL, "null batch");
+  HIPCHK(hipSetDevice(b->eng->device));
+  if (enable && b->events.empty()) {
+    b->events.resize(NUM_EVENTS);
+    for (auto& ev : b->events) HIPCHK(hipEventCreate(&ev));
+  } else if (!enable) {
+    for (auto ev : b->events) (void)hipEventDestroy(ev);
+    b->events.clear();
+  }
+  return 0;
+}
+
+extern "C" int rf_amd_batch_timings(rf_amd_batch* b, float* ms, uint32_t n) {
+  if (!b || b->events.empty() || !ms || n < RF_AMD_NUM_TIMINGS) return fail(RF_AMD_EINVAL, "timing not enabled");
+  HIPCHK(hipSetDevice(b->eng->device));
+  static const int pairs[RF_AMD_NUM_TIMINGS][2] = {
+      {EV_B_START, EV_B_HASH},    {EV_B_HASH, EV_B_SCAN},     {EV_B_SCAN, EV_B_SCATTER},
+      {EV_B_SCATTER, EV_B_SORT},  {EV_B_SORT, EV_B_SORT_BIG}, {EV_B_SORT_BIG, EV_B_LAYOUT},
+      {EV_B_LAYOUT, EV_B_ASSEMBLE}, {EV_B_START, EV_B_ASSEMBLE}, {EV_P_START, EV_P_END}};
+  for (uint32_t i = 0; i < RF_AMD_NUM_TIMINGS; i++) {
+    ms[i] = -1.f;
+    if (hipEventSynchronize(b->events[pairs[i][1]]) != hipSuccess) continue;
+    float t = 0;
+    if (hipEventElapsedTime(&t, b->events[pairs[i][0]], b->events[pairs[i][1]]) == hipSuccess) ms[i] = t;
+  }
+  return 0;
+}
+
+extern "C" int rf_amd_batch_info(rf_amd_batch* b, uint32_t f, rf_amd_filter_info* out) {
+  if (!b || f >= b->F || !out) return fail(RF_AMD_EINVAL, "bad batch/filter");
+  HIPCHK(hipSetDevice(b->eng->device));
+  FilterOut o;
+  HIPCHK(hipStreamSynchronize(b->eng->stream));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(&o, b->d_outs.as<FilterOut>() + f, sizeof(o), hipMemcpyDeviceToHost));
+  const FilterPlan& p = b->plans[f];
+  out->num_fingerprints = p.num_fp;
+  out->num_unique = o.num_unique;
+  out->value_size = p.vs;
+  out->num_indices = p.num_indices;
+  out->num_pages = o.num_pages;
+  out->error = o.error;
+  return 0;
+}
+
+extern "C" int rf_amd_batch_read_image(rf_amd_batch* b, uint32_t f, uint8_t* h_pages, uint64_t pages_bytes,
+                                       uint64_t* h_slots, uint32_t num_slots) {
+  rf_amd_filter_info info;
+  if (int rc = rf_amd_batch_info(b, f, &info)) return rc;
+  if (info.error) return fail(RF_AMD_EINVAL, "filter build reported error bits");
+  const FilterPlan& p = b->plans[f];
+  const uint64_t need = (uint64_t)info.num_pages * b->cfg.page_size;
+  if (h_pages) {
+    if (pages_bytes < need) return fail(RF_AMD_EINVAL, "pages buffer too small");
+    HIPCHK(hipMemcpy(h_pages, b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size, need,
+                     hipMemcpyDeviceToHost));
+  }
+  if (h_slots) {
+    if (num_slots < p.num_indices) return fail(RF_AMD_EINVAL, "slots buffer too small");
+    HIPCHK(hipMemcpy(h_slots, b->d_slots.as<uint64_t>() + p.idx_base, 8ull * p.num_indices,
+                     hipMemcpyDeviceToHost));
+  }
+  return 0;
+}
+
+extern "C" int rf_amd_batch_read_image_async(rf_amd_batch* b, uint32_t f, void* h_pages, uint64_t pages_bytes,
+                                             void* h_slots, uint32_t num_slots, void* stream) {
+  if (!b || f >= b->F) return fail(RF_AMD_EINVAL, "bad batch/filter");
+  const FilterPlan& p = b->plans[f];
+  if (pages_bytes > (uint64_t)p.page_cap * b->cfg.page_size || num_slots > p.num_indices)
+    return fail(RF_AMD_EINVAL, "copy larger than the filter's reservation");
+  HIPCHK(hipSetDevice(b->eng->device));
+  hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  if (h_pages && pages_bytes)
+    HIPCHK(hipMemcpyAsync(h_pages, b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size,
+                          pages_bytes, hipMemcpyDeviceToHost, st));
+  if (h_slots && num_slots)
+    HIPCHK(hipMemcpyAsync(h_slots, b->d_slots.as<uint64_t>() + p.idx_base, 8ull * num_slots,
+                          hipMemcpyDeviceToHost, st));
+  return 0;
+}
+
+extern "C" int rf_amd_batch_image_ptrs(rf_amd_batch* b, uint32_t f, void** d_pages, void** d_slots) {
+  if (!b || f >= b->F) return fail(RF_AMD_EINVAL, "bad batch/filter");
+  const FilterPlan& p = b->plans[f];
+  if (d_pages) *d_pages = b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size;
+  if (d_slots) *d_slots = b->d_slots.as<uint64_t>() + p.idx_base;
+  return 0;
+}
+
+// ---- image batches: a host image uploaded as a built one-filter batch ------------------
+static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* img,
+                            rf_amd_batch** out) {
+  if (int rc = check_cfg(cfg)) return rc;
+  if (!img || !img->pages || !img->slots || img->info.num_fingerprints == 0)
+    return fail(RF_AMD_EINVAL, "bad image");
+  HIPCHK(hipSetDevice(e->device));
+  auto* b = new rf_amd_batch();
+  b->eng = e;
+  b->cfg = *cfg;
+  b->F = 1;
+  b->plans.resize(1);
+  FilterPlan& p = b->plans[0];
+  memset(&p, 0, sizeof(p));
+  const uint32_t lis = cfg->log_index_size;
+  uint32_t lnb = 31 - __builtin_clz(img->info.num_fingerprints);
+  if (lnb < lis) lnb = lis;
+  if (lnb > cfg->fingerprint_size || (1u << (lnb - lis)) > MAX_INDICES) {
+    delete b;
+    return fail(RF_AMD_EINVAL, "image geometry out of range");
+  }
+  p.num_fp = img->info.num_fingerprints;
+  p.lnb = lnb;
+  p.vs = img->info.value_size;
+  p.rem = cfg->fingerprint_size - lnb;
+  p.rvs = p.rem + p.vs;
+  p.num_indices = 1u << (lnb - lis);
+  p.page_cap = img->info.num_pages;
+  b->PS = img->info.num_pages;
+  b->I = p.num_indices;
+  int rc = b->d_plans.alloc(sizeof(FilterPlan));
+  rc |= b->d_pages.alloc((size_t)img->info.num_pages * cfg->page_size + 256);
+  rc |= b->d_slots.alloc(8ull * p.num_indices);
+  if (rc) {
+    delete b;
+    return fail(RF_AMD_ENOMEM, "device allocation failed");
+  }
+  hipStream_t st = e->stream;
+  HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
+  HIPCHK(hipMemcpyAsync(b->d_pages.p, img->pages, (size_t)img->info.num_pages * cfg->page_size,
+                        hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(b->d_slots.p, img->slots, 8ull * p.num_indices, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(b->d_plans.p, &p, sizeof(p), hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  b->built = true;
+  *out = b;
+  return 0;
+}
+
+extern "C" int rf_amd_filter_add(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* old_filter,
+                                 rf_amd_image* filter, const uint32_t* new_fp_arr, uint64_t num_new_fp,
+                                 uint16_t value) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (!filter) return fail(RF_AMD_EINVAL, "null filter out-param");
+  memset(filter, 0, sizeof(*filter));
+  if (num_new_fp && !new_fp_arr) return fail(RF_AMD_EINVAL, "null fingerprint array");
+  if (num_new_fp > 0xffffffffull) return fail(RF_AMD_EINVAL, "too many fingerprints");
+  rf_amd_batch* ob = nullptr;
+  const bool has_old = old_filter && old_filter->pages && old_filter->info.num_fingerprints;
+  if (has_old)
+    if (int rc = batch_from_image(e, cfg, old_filter, &ob)) return rc;
+  rf_amd_batch* b = nullptr;
+  const uint32_t n32 = (uint32_t)num_new_fp;
+  uint32_t zero = 0;
+  int rc = rf_amd_batch_create(e, cfg, 1, &n32, &value, has_old ? &ob : nullptr, has_old ? &zero : nullptr, &b);
+  if (rc) {
+    rf_amd_batch_destroy(ob);
+    return rc;
+  }
+  DevBuf d_h;
+  if ((rc = d_h.alloc(4ull * num_new_fp + 16)) == 0) {
+    hipError_t he = hipMemcpyAsync(d_h.p, new_fp_arr, 4ull * num_new_fp, hipMemcpyHostToDevice, e->stream);
+    if (he != hipSuccess) rc = fail(RF_AMD_EINVAL, "H2D failed");
+  }
+  if (!rc) rc = rf_amd_batch_build_hashes(b, d_h.as<uint32_t>(), nullptr);
+  rf_amd_filter_info info{};
+  if (!rc) rc = rf_amd_batch_info(b, 0, &info);
+  if (!rc && info.error) rc = fail(RF_AMD_EINVAL, "filter exceeds the on-disk format (error bits set)");
+  if (!rc) {
+    filter->info = info;
+    filter->pages = (uint8_t*)calloc((size_t)info.num_pages * cfg->page_size + 16, 1);
+    filter->slots = (uint64_t*)calloc(info.num_indices, 8);
+    if (!filter->pages || !filter->slots) rc = fail(RF_AMD_ENOMEM, "host allocation failed");
+  }
+  if (!rc) rc = rf_amd_batch_read_image(b, 0, filter->pages, (uint64_t)info.num_pages * cfg->page_size,
+                                        filter->slots, info.num_indices);
+  if (rc) rf_amd_image_free(filter);
+  rf_amd_batch_destroy(b);
+  rf_amd_batch_destroy(ob);
+  return rc;
+}
+
+extern "C" int rf_amd_filter_lookup_hashes(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* filter,
+                                           const uint32_t* hashes, uint64_t n, uint64_t* found_values) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (!filter || !filter->pages) {  // NULL filter finds nothing (src/routing_filter.c:1003-1006)
+    if (found_values) memset(found_values, 0, 8 * n);
+    return 0;
+  }
+  if (n == 0) return 0;
+  rf_amd_batch* b = nullptr;
+  if (int rc = batch_from_image(e, cfg, filter, &b)) return rc;
+  DevBuf d_h, d_f, d_id;
+  int rc = d_h.alloc(4 * n) | d_f.alloc(8 * n) | d_id.alloc(4 * n);
+  if (!rc) {
+    hipStream_t st = e->stream;
+    if (hipMemcpyAsync(d_h.p, hashes, 4 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync(d_id.p, 0, 4 * n, st) != hipSuccess)
+      rc = fail(RF_AMD_EINVAL, "H2D failed");
+    if (!rc) rc = rf_amd_batch_probe_hashes(b, d_h.as<uint32_t>(), d_id.as<uint32_t>(), n, d_f.as<uint64_t>(), st);
+    if (!rc && (hipMemcpyAsync(found_values, d_f.p, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
+      rc = fail(RF_AMD_EINVAL, "D2H failed");
+  }
+  rf_amd_batch_destroy(b);
+  return rc;
+}
+
+extern "C" int rf_amd_filter_lookup_keys(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* filter,
+                                         const void* keys, uint32_t key_len, uint64_t n, uint64_t* found_values) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (!filter || !filter->pages) {
+    if (found_values) memset(found_values, 0, 8 * n);
+    return 0;
+  }
+  if (n == 0) return 0;
+  if (!keys || key_len == 0) return fail(RF_AMD_EINVAL, "null keys");
+  rf_amd_batch* b = nullptr;
+  if (int rc = batch_from_image(e, cfg, filter, &b)) return rc;
+  DevBuf d_k, d_f, d_id;
+  int rc = d_k.alloc((size_t)key_len * n + 16) | d_f.alloc(8 * n) | d_id.alloc(4 * n);
+  if (!rc) {
+    hipStream_t st = e->stream;
+    if (hipMemcpyAsync(d_k.p, keys, (size_t)key_len * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync(d_id.p, 0, 4 * n, st) != hipSuccess)
+      rc = fail(RF_AMD_EINVAL, "H2D failed");
+    if (!rc) rc = rf_amd_batch_probe_keys(b, d_k.p, key_len, d_id.as<uint32_t>(), n, d_f.as<uint64_t>(), st);
+    if (!rc && (hipMemcpyAsync(found_values, d_f.p, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
+      rc = fail(RF_AMD_EINVAL, "D2H failed");
+  }
+  rf_amd_batch_destroy(b);
+  return rc;
+}
+
+extern "C" void rf_amd_image_free(rf_amd_image* img) {
+  if (!img) return;
+  free(img->pages);
+  free(img->slots);
+  img->pages = nullptr;
+  img->slots = nullptr;
+}
+
+extern "C" uint64_t rf_amd_max_fingerprints(const rf_amd_config* cfg) {
+  const uint64_t addrs_per_extent = (uint64_t)cfg->page_size * cfg->pages_per_extent / 8;
+  return 2ull * addrs_per_extent * (1ull << cfg->log_index_size) - 1;
+}
+
+extern "C" uint32_t rf_amd_estimate_unique_keys_from_count(const rf_amd_config* cfg, uint64_t num_unique) {
+  const double U = (double)(1ull << cfg->fingerprint_size);
+  const double unseen = U - (double)num_unique;
+  const double U2 = U * U, U4 = U2 * U2, s2 = unseen * unseen, s4 = s2 * s2;
+  const double hd = log(U) - log(unseen) + 0.5 * (1 / U - 1 / unseen) - (1 / 12.0) * (1 / U2 - 1 / s2) +
+                    (1 / 120.0) * (1 / U4 - 1 / s4);
+  return (uint32_t)(U * hd);
+}
+
+extern "C" uint64_t rf_amd_space_use_bytes(const rf_amd_config* cfg, uint32_t num_pages) {
+  const uint64_t extent = (uint64_t)cfg->page_size * cfg->pages_per_extent;
+  return cfg->page_size + extent * (1 + (num_pages + cfg->pages_per_extent - 1) / cfg->pages_per_extent);
+}

@@ -1,0 +1,981 @@
+// rf_kernels.hip -- MI355X (gfx950) kernels of the routing-filter engine.
+//
+// Build pipeline for a batch of F filters (each a SplinterDB routing_filter_add,
+// reference src/routing_filter.c:337-656), one launch each, all on one stream:
+//
+//   K1 k_hash_count   keys/hashes -> entry e = (fp << value_size) | value  (+ coarse-bucket
+//                     histogram in LDS, one global atomic per non-empty bin per tile)
+//   K2 k_cb_scan      per filter: exclusive scan of coarse-bucket counts
+//   K3 k_scatter      entries -> coarse buckets (LDS ranks + per-tile range reservation)
+//   K4 k_cb_sort      one workgroup per coarse bucket (~4-8K entries, held in LDS):
+//                     counting sort by filter bucket, per-bucket insertion sort, dedupe
+//                     (src/routing_filter.c:471-482), per-index counts (:484-494),
+//                     num_unique (:572-574)
+//   K4b k_cb_sort_big same for coarse buckets over LDS capacity (duplicate-heavy input)
+//   K5 k_layout       per filter: block sizes (:599-602) and the greedy page placement
+//                     (:603-610) as a parallel pointer-jumping scan; index slots (:612-620)
+//   K6 k_assemble     one workgroup per 4 KiB page: header, unary encoding with 0xFF
+//                     padding (:622-626), PackedArray remainders (:627-633) built in LDS,
+//                     written with 16-byte stores
+//   K0 k_old_*        incremental add: decode the old filter (:496-544) into entries
+//
+// Probe: k_probe, one lane per probe (routing_filter_lookup, :985-1073).
+//
+// The coarse bucket of an entry is its top `cbits` bits; K4 sorts the low bits, so the
+// result depends only on the multiset of entries, exactly like the reference's sort.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rf_device.h"
+#include "rf_plan.h"
+
+using namespace rf;
+
+// ======================================================================================
+// K1: hash + coarse-bucket histogram
+// ======================================================================================
+template <int KIND, typename EntT>
+__global__ __launch_bounds__(TILE_NT) void k_hash_count(const FilterPlan* __restrict__ plans,
+                                                        const uint32_t* __restrict__ tile_filter,
+                                                        const uint32_t* __restrict__ tile_start,
+                                                        const void* __restrict__ in0,
+                                                        const uint64_t* __restrict__ offs,
+                                                        uint32_t key_len, uint32_t fp_size,
+                                                        uint32_t seed, EntT* __restrict__ ent,
+                                                        uint32_t* __restrict__ cb_count) {
+  __shared__ uint32_t s_hist[MAX_CB];
+  const uint32_t t = blockIdx.x;
+  const FilterPlan& P = plans[tile_filter[t]];
+  const uint32_t start = tile_start[t];
+  const uint32_t count = min((uint32_t)TILE_KEYS, P.num_new - start);
+  const uint32_t num_cb = 1u << P.cbits;
+  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) s_hist[i] = 0;
+  __syncthreads();
+  const uint32_t esh = fp_size + P.vs - P.cbits;  // entry >> esh = coarse bucket
+  for (uint32_t j = threadIdx.x; j < count; j += TILE_NT) {
+    const uint64_t k = P.key_first + start + j;
+    uint32_t h;
+    if constexpr (KIND == IN_KEYS24) {
+      const uint2* kp = reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(in0) + k * 24);
+      uint2 a = kp[0], b = kp[1], c = kp[2];
+      uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+      h = xxh32_24(w, seed);
+    } else if constexpr (KIND == IN_KEYS_W) {
+      h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + k * key_len),
+                      key_len, seed);
+    } else if constexpr (KIND == IN_KEYS_B) {
+      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + k * key_len, key_len, seed);
+    } else if constexpr (KIND == IN_VAR) {
+      const uint64_t o0 = offs[k], o1 = offs[k + 1];
+      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
+    } else {  // IN_HASH
+      h = static_cast<const uint32_t*>(in0)[k];
+    }
+    const uint32_t e = ((h >> (32 - fp_size)) << P.vs) | P.value;
+    if constexpr (sizeof(EntT) == 8) {
+      ent[P.e_first + start + j] = ((uint64_t)e << 1) | 1ull;  // new entry: flag 1
+    } else {
+      ent[P.e_first + start + j] = e;
+    }
+    const uint32_t cb = P.cbits ? (e >> esh) : 0u;
+    atomicAdd(&s_hist[cb], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) {
+    const uint32_t c = s_hist[i];
+    if (c) atomicAdd(&cb_count[P.cb_base + i], c);
+  }
+}
+
+// Histogram of the old-entry region (K0 output); sentinel (~0) slots are skipped.
+__global__ __launch_bounds__(TILE_NT) void k_old_count(const FilterPlan* __restrict__ plans,
+                                                       const uint32_t* __restrict__ tile_filter,
+                                                       const uint32_t* __restrict__ tile_start,
+                                                       uint32_t fp_size,
+                                                       const uint64_t* __restrict__ ent,
+                                                       uint32_t* __restrict__ cb_count) {
+  __shared__ uint32_t s_hist[MAX_CB];
+  const uint32_t t = blockIdx.x;
+  const FilterPlan& P = plans[tile_filter[t]];
+  const uint32_t start = tile_start[t];
+  const uint32_t count = min((uint32_t)TILE_KEYS, P.old_region - start);
+  const uint32_t num_cb = 1u << P.cbits;
+  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) s_hist[i] = 0;
+  __syncthreads();
+  const uint32_t esh = fp_size + P.vs - P.cbits;
+  for (uint32_t j = threadIdx.x; j < count; j += TILE_NT) {
+    const uint64_t x = ent[P.e_first + P.num_new + start + j];
+    if (x == ~0ull) continue;
+    const uint32_t e = (uint32_t)(x >> 1);
+    atomicAdd(&s_hist[P.cbits ? (e >> esh) : 0u], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) {
+    const uint32_t c = s_hist[i];
+    if (c) atomicAdd(&cb_count[P.cb_base + i], c);
+  }
+}
+
+// ======================================================================================
+// K2: per-filter exclusive scan of coarse-bucket counts
+// ======================================================================================
+__global__ __launch_bounds__(256) void k_cb_scan(const FilterPlan* __restrict__ plans,
+                                                 const uint32_t* __restrict__ cb_count,
+                                                 uint32_t* __restrict__ cb_start,
+                                                 uint32_t* __restrict__ cb_cursor) {
+  __shared__ uint32_t s_tmp[256 / WAVE + 1];
+  const FilterPlan& P = plans[blockIdx.x];
+  const uint32_t num_cb = 1u << P.cbits;
+  constexpr uint32_t PER = MAX_CB / 256;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x * PER + k;
+    v[k] = i < num_cb ? cb_count[P.cb_base + i] : 0u;
+    sum += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan<256>(sum, s_tmp, &total);
+#pragma unroll
+  for (uint32_t k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x * PER + k;
+    if (i < num_cb) {
+      cb_start[P.cb_base + i] = run;
+      cb_cursor[P.cb_base + i] = run;
+    }
+    run += v[k];
+  }
+}
+
+// ======================================================================================
+// K3: scatter entries into coarse buckets
+// ======================================================================================
+template <typename EntT>
+__global__ __launch_bounds__(TILE_NT) void k_scatter(const FilterPlan* __restrict__ plans,
+                                                     const uint32_t* __restrict__ tile_filter,
+                                                     const uint32_t* __restrict__ tile_start,
+                                                     uint32_t region_is_old, uint32_t fp_size,
+                                                     const EntT* __restrict__ ent,
+                                                     EntT* __restrict__ part,
+                                                     uint32_t* __restrict__ cb_cursor) {
+  __shared__ uint32_t s_hist[MAX_CB];
+  constexpr int PER = TILE_KEYS / TILE_NT;
+  const uint32_t t = blockIdx.x;
+  const FilterPlan& P = plans[tile_filter[t]];
+  const uint32_t start = tile_start[t];
+  const uint32_t region = region_is_old ? P.old_region : P.num_new;
+  const uint64_t base = P.e_first + (region_is_old ? P.num_new : 0u) + start;
+  const uint32_t count = min((uint32_t)TILE_KEYS, region - start);
+  const uint32_t num_cb = 1u << P.cbits;
+  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) s_hist[i] = 0;
+  __syncthreads();
+  const uint32_t esh = fp_size + P.vs - P.cbits;
+  EntT v[PER];
+  uint32_t cbv[PER], rank[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x + k * TILE_NT;
+    cbv[k] = ~0u;
+    if (j < count) {
+      v[k] = ent[base + j];
+      uint32_t e;
+      bool valid = true;
+      if constexpr (sizeof(EntT) == 8) {
+        valid = v[k] != ~0ull;
+        e = (uint32_t)(v[k] >> 1);
+      } else {
+        e = v[k];
+      }
+      if (valid) {
+        cbv[k] = P.cbits ? (e >> esh) : 0u;
+        rank[k] = atomicAdd(&s_hist[cbv[k]], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) {
+    const uint32_t c = s_hist[i];
+    if (c) s_hist[i] = atomicAdd(&cb_cursor[P.cb_base + i], c);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    if (cbv[k] != ~0u) part[P.e_first + s_hist[cbv[k]] + rank[k]] = v[k];
+  }
+}
+
+// ======================================================================================
+// K4: per coarse bucket sort / dedupe / index counts
+// ======================================================================================
+template <typename EntT>
+__device__ __forceinline__ uint32_t ent_e(EntT x) {
+  if constexpr (sizeof(EntT) == 8) return (uint32_t)(x >> 1);
+  else return x;
+}
+// dedupe rule (src/routing_filter.c:471-482 for new entries; old entries are never
+// deduplicated, :559-597): drop x if it equals its predecessor and is a new entry.
+template <typename EntT>
+__device__ __forceinline__ bool ent_drop(EntT x, EntT prev) {
+  if constexpr (sizeof(EntT) == 8) return x == prev && (x & 1ull);
+  else return x == prev;
+}
+
+// Finish a sorted coarse bucket held in `B` (LDS or global): write per-index counts and
+// starts, the compacted entries, and the num_unique contribution. Shared by K4 and K4b.
+struct CbCtx {
+  uint32_t rvs, vs, lis, bbits, idx0;  // idx0 = global index id of the cb's first index
+  uint32_t cb_rel;                     // cb start relative to the filter's e_first
+  uint64_t e_first;
+};
+
+__device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_t* sorted, uint32_t kept,
+                                                   uint32_t* idx_cnt, uint32_t* idx_start,
+                                                   uint32_t* uniq_out) {
+  // sorted: compacted e values (u32). Index-in-cb of e = (e >> (lis + rvs)) & (ipc - 1)
+  const uint32_t ipc = 1u << (c.bbits - c.lis);
+  const uint32_t ish = c.lis + c.rvs;
+  for (uint32_t li = threadIdx.x; li < ipc; li += blockDim.x) {
+    auto lb = [&](uint32_t key) {
+      uint32_t lo = 0, hi = kept;
+      while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        uint32_t m = ish >= 32 ? 0u : ((sorted[mid] >> ish) & (ipc - 1));
+        if (m < key) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    const uint32_t lo = lb(li);
+    const uint32_t hi = (li + 1 < ipc) ? lb(li + 1) : kept;
+    idx_cnt[c.idx0 + li] = hi - lo;
+    idx_start[c.idx0 + li] = c.cb_rel + lo;
+  }
+  // num_unique (:558, :572-574): per index, count entries whose fingerprint differs from the
+  // previous entry's; the first entry of an index compares against UINT32_MAX >> value_size.
+  // Equal fingerprints share an index, so "previous entry in the coarse bucket" suffices
+  // except at an index's first entry.
+  uint32_t uniq = 0;
+  for (uint32_t i = threadIdx.x; i < kept; i += blockDim.x) {
+    const uint32_t fp = sorted[i] >> c.vs;
+    const bool first = (i == 0) || (ish < 32 && ((sorted[i] >> ish) != (sorted[i - 1] >> ish)));
+    const uint32_t prev = first ? (0xffffffffu >> c.vs) : (sorted[i - 1] >> c.vs);
+    uniq += (fp != prev) ? 1u : 0u;
+  }
+  *uniq_out = uniq;
+}
+
+template <typename EntT>
+__global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restrict__ plans,
+                                                     const uint32_t* __restrict__ cb_filter,
+                                                     const uint32_t* __restrict__ cb_count,
+                                                     const uint32_t* __restrict__ cb_start,
+                                                     const EntT* __restrict__ part,
+                                                     uint32_t* __restrict__ sorted32,
+                                                     uint32_t* __restrict__ idx_cnt,
+                                                     uint32_t* __restrict__ idx_start,
+                                                     FilterOut* __restrict__ outs,
+                                                     uint32_t* __restrict__ overflow,
+                                                     uint32_t lis) {
+  constexpr int PER = SORT_CAP / SORT_NT;
+  __shared__ EntT s_b[SORT_CAP];
+  __shared__ uint32_t s_bin[MAX_BINS + 1];
+  __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
+  const uint32_t cb = blockIdx.x;
+  const uint32_t f = cb_filter[cb];
+  const FilterPlan& P = plans[f];
+  const uint32_t n = cb_count[cb];
+  const uint32_t cbl = cb - P.cb_base;
+  CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_start[cb], P.e_first};
+  if (n > SORT_CAP) {  // handled by k_cb_sort_big
+    if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
+    return;
+  }
+  const uint32_t nbins = 1u << P.bbits;
+  const uint32_t bmask = nbins - 1;
+  for (uint32_t i = threadIdx.x; i <= nbins; i += SORT_NT) s_bin[i] = 0;
+  __syncthreads();
+  // load + per-bin rank (bin = filter bucket within the coarse bucket)
+  EntT v[PER];
+  uint32_t r[PER];
+  const EntT* src = part + P.e_first + c.cb_rel;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x + k * SORT_NT;
+    if (i < n) {
+      v[k] = src[i];
+      const uint32_t e = ent_e(v[k]);
+      const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
+      r[k] = atomicAdd(&s_bin[b], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of bin counts (nbins <= MAX_BINS = 8 * SORT_NT)
+  {
+    constexpr int BPT = MAX_BINS / SORT_NT;
+    uint32_t bv[BPT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < BPT; k++) {
+      const uint32_t i = threadIdx.x * BPT + k;
+      bv[k] = i < nbins ? s_bin[i] : 0u;
+      sum += bv[k];
+    }
+    uint32_t total;
+    uint32_t run = block_excl_scan<SORT_NT>(sum, s_tmp, &total);
+#pragma unroll
+    for (int k = 0; k < BPT; k++) {
+      const uint32_t i = threadIdx.x * BPT + k;
+      if (i < nbins) s_bin[i] = run;
+      run += bv[k];
+    }
+    if (threadIdx.x == 0) s_bin[nbins] = n;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x + k * SORT_NT;
+    if (i < n) {
+      const uint32_t e = ent_e(v[k]);
+      const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
+      s_b[s_bin[b] + r[k]] = v[k];
+    }
+  }
+  __syncthreads();
+  // insertion sort inside each bin (bins hold ~1-2 entries for random keys)
+  for (uint32_t b = threadIdx.x; b < nbins; b += SORT_NT) {
+    const uint32_t s = s_bin[b], e = s_bin[b + 1];
+    for (uint32_t i = s + 1; i < e; i++) {
+      const EntT x = s_b[i];
+      uint32_t j = i;
+      while (j > s && s_b[j - 1] > x) {
+        s_b[j] = s_b[j - 1];
+        j--;
+      }
+      s_b[j] = x;
+    }
+  }
+  __syncthreads();
+  // dedupe + compaction: thread t owns the contiguous run [t*PER, t*PER + PER)
+  uint32_t keep_mask = 0, cnt = 0;
+  EntT w[PER];
+  {
+    const uint32_t i0 = threadIdx.x * PER;
+    EntT prev = (i0 > 0 && i0 <= n) ? s_b[i0 - 1] : EntT(0);
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t i = i0 + k;
+      if (i < n) {
+        w[k] = s_b[i];
+        const bool drop = (i > 0) && ent_drop(w[k], prev);
+        if (!drop) { keep_mask |= 1u << k; cnt++; }
+        prev = w[k];
+      }
+    }
+  }
+  uint32_t kept;
+  uint32_t pos = block_excl_scan<SORT_NT>(cnt, s_tmp, &kept);  // has barriers: reads done
+  uint32_t* s_sorted = reinterpret_cast<uint32_t*>(s_b);        // compacted e values (u32)
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    if (keep_mask & (1u << k)) s_sorted[pos++] = ent_e(w[k]);
+  }
+  __syncthreads();
+  uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
+  for (uint32_t i = threadIdx.x; i < kept; i += SORT_NT) dst[i] = s_sorted[i];
+  uint32_t uniq, tot_uniq;
+  write_index_bounds(c, s_sorted, kept, idx_cnt, idx_start, &uniq);
+  block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
+  if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
+}
+
+// K4b: coarse buckets larger than LDS (duplicate-heavy inputs). One workgroup per listed
+// bucket, working in global memory: `scratch` is the K1 entry array (free after K3).
+template <typename EntT>
+__global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __restrict__ plans,
+                                                        const uint32_t* __restrict__ cb_filter,
+                                                        const uint32_t* __restrict__ cb_count,
+                                                        const uint32_t* __restrict__ cb_start,
+                                                        const EntT* __restrict__ part,
+                                                        EntT* __restrict__ scratch,
+                                                        uint32_t* __restrict__ sorted32,
+                                                        uint32_t* __restrict__ idx_cnt,
+                                                        uint32_t* __restrict__ idx_start,
+                                                        FilterOut* __restrict__ outs,
+                                                        const uint32_t* __restrict__ overflow,
+                                                        uint32_t lis) {
+  __shared__ uint32_t s_bin[MAX_BINS + 1];
+  __shared__ uint32_t s_cur[MAX_BINS];
+  __shared__ uint32_t s_tmp[BIG_NT / WAVE + 1];
+  __shared__ uint32_t s_run;
+  const uint32_t nover = overflow[0];
+  for (uint32_t it = blockIdx.x; it < nover; it += gridDim.x) {
+    const uint32_t cb = overflow[1 + it];
+    const uint32_t f = cb_filter[cb];
+    const FilterPlan& P = plans[f];
+    const uint32_t n = cb_count[cb];
+    const uint32_t cbl = cb - P.cb_base;
+    CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_start[cb], P.e_first};
+    const uint32_t nbins = 1u << P.bbits, bmask = nbins - 1;
+    const EntT* src = part + P.e_first + c.cb_rel;
+    EntT* tmp = scratch + P.e_first + c.cb_rel;
+    uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
+    for (uint32_t i = threadIdx.x; i <= nbins; i += BIG_NT) s_bin[i] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += BIG_NT) {
+      const uint32_t e = ent_e(src[i]);
+      atomicAdd(&s_bin[P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t run = 0;
+      for (uint32_t b = 0; b < nbins; b++) {
+        const uint32_t x = s_bin[b];
+        s_bin[b] = run;
+        s_cur[b] = run;
+        run += x;
+      }
+      s_bin[nbins] = run;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += BIG_NT) {
+      const EntT x = src[i];
+      const uint32_t e = ent_e(x);
+      tmp[atomicAdd(&s_cur[P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask)], 1u)] = x;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += BIG_NT) {
+      const uint32_t s = s_bin[b], e = s_bin[b + 1];
+      for (uint32_t i = s + 1; i < e; i++) {
+        const EntT x = tmp[i];
+        uint32_t j = i;
+        while (j > s && tmp[j - 1] > x) {
+          tmp[j] = tmp[j - 1];
+          j--;
+        }
+        tmp[j] = x;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_run = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += BIG_NT) {
+      const uint32_t i = base + threadIdx.x;
+      uint32_t keep = 0;
+      EntT x = 0;
+      if (i < n) {
+        x = tmp[i];
+        keep = (i == 0 || !ent_drop(x, tmp[i - 1])) ? 1u : 0u;
+      }
+      uint32_t tot;
+      const uint32_t p = block_excl_scan<BIG_NT>(keep, s_tmp, &tot);
+      const uint32_t run = s_run;
+      if (keep) dst[run + p] = ent_e(x);
+      __syncthreads();
+      if (threadIdx.x == 0) s_run = run + tot;
+      __syncthreads();
+    }
+    const uint32_t kept = s_run;
+    uint32_t uniq, tot_uniq;
+    write_index_bounds(c, dst, kept, idx_cnt, idx_start, &uniq);
+    block_excl_scan<BIG_NT>(uniq, s_tmp, &tot_uniq);
+    if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
+    __syncthreads();
+  }
+}
+
+// ======================================================================================
+// K5: block sizes + greedy page placement (src/routing_filter.c:599-620)
+//
+// next(j) = the block that starts the page after a page starting at block j
+// (first q with excl[q+1] - excl[j] > page_size). Page starts are the orbit of block 0
+// under next(); it is marked in ceil(log2(n+1)) pointer-doubling rounds.
+// ======================================================================================
+__device__ __forceinline__ uint32_t block_size(uint32_t c, uint32_t index_size, uint32_t rvs) {
+  const uint32_t enc = (c + index_size - 1) / 8 + 4;
+  const uint64_t bits = (uint64_t)c * rvs;
+  const uint32_t rbs = bits == 0 ? 3u : (uint32_t)((bits - 1) / 8 + 4);  // u32 wrap quirk
+  return enc + 2 + rbs;
+}
+
+__global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restrict__ plans,
+                                                      const uint32_t* __restrict__ idx_cnt,
+                                                      uint64_t* __restrict__ slots,
+                                                      uint32_t* __restrict__ page_first,
+                                                      FilterOut* __restrict__ outs,
+                                                      uint32_t lis, uint32_t page_size) {
+  __shared__ uint32_t s_excl[MAX_INDICES + 1];
+  __shared__ uint16_t s_jA[MAX_INDICES + 1];
+  __shared__ uint16_t s_jB[MAX_INDICES + 1];
+  __shared__ uint8_t s_mark[MAX_INDICES + 1];
+  __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
+  __shared__ uint32_t s_err;
+  const uint32_t f = blockIdx.x;
+  const FilterPlan& P = plans[f];
+  const uint32_t n = P.num_indices;
+  const uint32_t index_size = 1u << lis;
+  constexpr int PER = MAX_INDICES / LAYOUT_NT;
+  if (threadIdx.x == 0) s_err = 0;
+  __syncthreads();
+  // sizes -> exclusive prefix (contiguous ownership: thread t owns [t*PER, t*PER+PER))
+  uint32_t sz[PER], sum = 0, err = 0;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x * PER + k;
+    sz[k] = 0;
+    if (j < n) {
+      const uint32_t c = idx_cnt[P.idx_base + j];
+      if (c > 4096) err |= ERR_INDEX_OVERFLOW;
+      sz[k] = block_size(c, index_size, P.rvs);
+      if (sz[k] > page_size) err |= ERR_BLOCK_TOO_BIG;
+    }
+    sum += sz[k];
+  }
+  if (err) atomicOr(&s_err, err);
+  uint32_t total;
+  uint32_t run = block_excl_scan<LAYOUT_NT>(sum, s_tmp, &total);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x * PER + k;
+    if (j <= n) s_excl[j] = run;  // j == n writes the total
+    run += sz[k];
+  }
+  __syncthreads();
+  if (s_err) {
+    if (threadIdx.x == 0) outs[f].error |= s_err;
+    return;
+  }
+  // next(j) by binary search on the prefix sums
+  for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT) {
+    uint32_t q = n;
+    if (j < n) {
+      const uint32_t lim = s_excl[j] + page_size;
+      uint32_t lo = j + 1, hi = n + 1;  // first q in [j+1, n] with excl[q] > lim, else n+1
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_excl[mid] > lim) hi = mid; else lo = mid + 1;
+      }
+      q = lo - 1;  // block q is the first that does not fit (q == n: none)
+    }
+    s_jA[j] = (uint16_t)q;
+    s_mark[j] = (j == 0) ? 1 : 0;
+  }
+  __syncthreads();
+  uint16_t* cur = s_jA;
+  uint16_t* nxt = s_jB;
+  for (uint32_t span = 1; span <= n; span <<= 1) {
+    for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT)
+      if (s_mark[j]) s_mark[cur[j]] = 1;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT) nxt[j] = cur[cur[j]];
+    __syncthreads();
+    uint16_t* t = cur; cur = nxt; nxt = t;
+  }
+  // page numbers: inclusive scan of marks over [0, n)
+  uint32_t mk[PER], msum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x * PER + k;
+    mk[k] = j < n ? s_mark[j] : 0u;
+    msum += mk[k];
+  }
+  uint32_t npages;
+  uint32_t mrun = block_excl_scan<LAYOUT_NT>(msum, s_tmp, &npages);
+  uint16_t* s_pstart = nxt;  // reuse: page -> first block
+  uint32_t pg[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x * PER + k;
+    mrun += mk[k];
+    pg[k] = mrun - 1;
+    if (j < n && mk[k]) s_pstart[pg[k]] = (uint16_t)j;
+  }
+  __syncthreads();
+  uint32_t* pf = page_first + P.pf_base;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x * PER + k;
+    if (j < n) {
+      const uint32_t ps = s_pstart[pg[k]];
+      slots[P.idx_base + j] = (uint64_t)pg[k] * page_size + (s_excl[j] - s_excl[ps]);
+      if (mk[k] && pg[k] < P.page_cap) pf[pg[k]] = j;
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (npages <= P.page_cap) pf[npages] = n;
+    outs[f].num_pages = npages;
+    if (npages > P.page_cap) outs[f].error |= ERR_PAGE_CAP;
+  }
+}
+
+// ======================================================================================
+// K6: page assembly in LDS, 16-byte stores (src/routing_filter.c:612-633)
+// ======================================================================================
+__device__ __forceinline__ void lds_or_bits(uint32_t* s, uint64_t bitpos, uint32_t val, uint32_t nbits) {
+  if (nbits == 0) return;
+  const uint32_t w = (uint32_t)(bitpos >> 5), sh = (uint32_t)(bitpos & 31);
+  const uint64_t v = (uint64_t)(nbits >= 32 ? val : (val & ((1u << nbits) - 1))) << sh;
+  if ((uint32_t)v) atomicOr(&s[w], (uint32_t)v);
+  if ((uint32_t)(v >> 32)) atomicOr(&s[w + 1], (uint32_t)(v >> 32));
+}
+
+__global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restrict__ plans,
+                                                     const uint32_t* __restrict__ pg_filter,
+                                                     const uint32_t* __restrict__ idx_cnt,
+                                                     const uint32_t* __restrict__ idx_start,
+                                                     const uint32_t* __restrict__ sorted32,
+                                                     const uint64_t* __restrict__ slots,
+                                                     const uint32_t* __restrict__ page_first,
+                                                     const FilterOut* __restrict__ outs,
+                                                     uint8_t* __restrict__ pages, uint32_t lis,
+                                                     uint32_t page_size) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_pg[MAX_PAGE / 4 + 4];
+  const uint32_t slot = blockIdx.x;
+  const uint32_t f = pg_filter[slot];
+  const FilterPlan& P = plans[f];
+  const uint32_t p = slot - P.page_base;
+  if (outs[f].error || p >= outs[f].num_pages) return;
+  const uint32_t nwords = page_size / 4;
+  for (uint32_t i = threadIdx.x; i < nwords + 4; i += ASM_NT) s_pg[i] = 0;
+  const uint32_t* pf = page_first + P.pf_base;
+  const uint32_t b0 = pf[p], b1 = pf[p + 1];
+  const uint32_t index_size = 1u << lis;
+  __syncthreads();
+  // phase 1: header count + 0xFF encoding fill
+  for (uint32_t b = b0; b < b1; b++) {
+    const uint32_t g = P.idx_base + b;
+    const uint32_t off = (uint32_t)(slots[g] - (uint64_t)p * page_size);
+    const uint32_t c = idx_cnt[g];
+    const uint32_t enc = (c + index_size - 1) / 8 + 4;
+    if (threadIdx.x == 0) lds_or_bits(s_pg, (uint64_t)off * 8, c & 0xffffu, 16);
+    // encoding bytes [off+2, off+2+enc) set to 0xFF, word-wise
+    const uint32_t e0 = off + 2, e1 = off + 2 + enc;
+    for (uint32_t w = (e0 >> 2) + threadIdx.x; w <= ((e1 - 1) >> 2); w += ASM_NT) {
+      const uint32_t lo = max(e0, w * 4), hi = min(e1, w * 4 + 4);
+      const uint32_t m = (hi - lo == 4) ? 0xffffffffu : (((1u << ((hi - lo) * 8)) - 1) << ((lo & 3) * 8));
+      atomicOr(&s_pg[w], m);
+    }
+  }
+  __syncthreads();
+  // phase 2: clear encoding bits of entries, OR packed remainders
+  const uint32_t remmask = P.rem >= 32 ? 0xffffffffu : ((1u << P.rem) - 1);
+  for (uint32_t b = b0; b < b1; b++) {
+    const uint32_t g = P.idx_base + b;
+    const uint32_t off = (uint32_t)(slots[g] - (uint64_t)p * page_size);
+    const uint32_t c = idx_cnt[g];
+    const uint32_t enc = (c + index_size - 1) / 8 + 4;
+    const uint32_t* ent = sorted32 + P.e_first + idx_start[g];
+    const uint64_t ebit = (uint64_t)(off + 2) * 8;
+    const uint64_t rbit = (uint64_t)(off + 2 + enc) * 8;
+    for (uint32_t k = threadIdx.x; k < c; k += ASM_NT) {
+      const uint32_t e = ent[k];
+      const uint32_t fp = e >> P.vs;
+      const uint32_t bucket_off = (P.rem >= 32 ? 0u : (fp >> P.rem)) & (index_size - 1);
+      const uint64_t hb = ebit + k + bucket_off;
+      atomicAnd(&s_pg[hb >> 5], ~(1u << (hb & 31)));
+      const uint32_t rv = ((fp & remmask) << P.vs) | (e & ((1u << P.vs) - 1));
+      lds_or_bits(s_pg, rbit + (uint64_t)k * P.rvs, rv, P.rvs);
+    }
+  }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(pages + (uint64_t)slot * page_size);
+  const uint4* src = reinterpret_cast<const uint4*>(s_pg);
+  for (uint32_t i = threadIdx.x; i < page_size / 16; i += ASM_NT) dst[i] = src[i];
+}
+
+// ======================================================================================
+// K0: incremental add -- decode an old filter into entries (src/routing_filter.c:496-544)
+// ======================================================================================
+// exclusive scan of n <= MAX_INDICES counts in one workgroup
+__global__ __launch_bounds__(LAYOUT_NT) void k_scan_small(const uint32_t* __restrict__ in,
+                                                          uint32_t* __restrict__ out, uint32_t n) {
+  __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
+  constexpr int PER = MAX_INDICES / LAYOUT_NT;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x * PER + k;
+    v[k] = i < n ? in[i] : 0u;
+    sum += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan<LAYOUT_NT>(sum, s_tmp, &total);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x * PER + k;
+    if (i < n) out[i] = run;
+    run += v[k];
+  }
+}
+
+// k_old_counts: per old index, num_remainders from its header -> cnt
+__global__ void k_old_counts(const FilterPlan* __restrict__ plans, uint32_t f,
+                             uint32_t* __restrict__ cnt) {
+  const FilterPlan& P = plans[f];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.old_num_indices) return;
+  const uint64_t s = P.old_slots[i];
+  cnt[i] = (uint32_t)P.old_pages[s] | ((uint32_t)P.old_pages[s + 1] << 8);
+}
+
+// k_old_decode: one wave per old index. Entry k of the block: bucket offset = number of
+// 1-bits before its 0-bit in the encoding (routing_get_bucket_counts, :281-306); value
+// bits re-widened to the new value_size (:536-543). Written as (e << 1) | 0 (old flag).
+__global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict__ plans, uint32_t f,
+                                                    const uint32_t* __restrict__ pos,
+                                                    uint64_t* __restrict__ ent, uint32_t lis,
+                                                    uint32_t fp_size) {
+  const FilterPlan& P = plans[f];
+  const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  if (wid >= P.old_num_indices) return;
+  const uint32_t index_size = 1u << lis;
+  const uint64_t hdr = P.old_slots[wid];
+  const uint8_t* pg = P.old_pages;
+  const uint32_t c = (uint32_t)pg[hdr] | ((uint32_t)pg[hdr + 1] << 8);
+  const uint32_t enc = (c + index_size - 1) / 8 + 4;
+  const uint64_t ebit = (hdr + 2) * 8;
+  const uint64_t rbit = (hdr + 2 + enc) * 8;
+  const uint32_t total_bits = c + index_size;
+  uint64_t* out = ent + P.e_first + P.num_new + pos[wid];
+  const uint32_t old_vmask = (uint32_t)((1ull << P.old_vs) - 1);
+  // walk the encoding 64 bits per lane-step: each lane takes one 64-bit chunk per round
+  uint32_t zeros_before = 0, ones_before = 0;
+  for (uint32_t base = 0; base < total_bits; base += 64 * WAVE) {
+    const uint32_t bit0 = base + lane * 64;
+    uint64_t x = 0;
+    uint32_t nb = 0;
+    if (bit0 < total_bits) {
+      nb = min(64u, total_bits - bit0);
+      const uint64_t bp = ebit + bit0;
+      const uint32_t sh = (uint32_t)(bp & 7);
+      x = ld_u64_unaligned(pg, bp >> 3) >> sh;
+      if (sh) x |= (uint64_t)pg[(bp >> 3) + 8] << (64 - sh);  // the chunk's top bits
+      if (nb < 64) x &= (1ull << nb) - 1;
+    }
+    const uint32_t ones = __popcll(x);
+    const uint32_t zer = nb - ones;
+    const uint32_t ones_ex = wave_incl_scan(ones) - ones + ones_before;
+    const uint32_t zer_ex = wave_incl_scan(zer) - zer + zeros_before;
+    // every zero bit of this chunk is an entry
+    uint64_t z = ~x & (nb == 64 ? ~0ull : ((1ull << nb) - 1));
+    uint32_t k = zer_ex;
+    while (z) {
+      const uint32_t b = __builtin_ctzll(z);
+      z &= z - 1;
+      // bucket offset = 1-bits before this 0-bit = chunk-prefix ones + (b - zeros before b in chunk)
+      const uint32_t bo = ones_ex + (b - (k - zer_ex));
+      const uint32_t rv = ld_bits(pg, rbit + (uint64_t)k * P.old_rvs, P.old_rvs);
+      const uint32_t bucket = wid * index_size + bo;
+      const uint32_t e_old = (P.old_rvs >= 32 ? 0u : (bucket << P.old_rvs)) | rv;
+      const uint32_t old_value = e_old & old_vmask;
+      const uint32_t fpv = e_old >> P.old_vs;
+      const uint32_t e = (fpv << P.vs) | old_value;
+      out[k] = (uint64_t)e << 1;
+      k++;
+    }
+    ones_before = __shfl(ones_ex + ones, WAVE - 1, WAVE);
+    zeros_before = __shfl(zer_ex + zer, WAVE - 1, WAVE);
+  }
+}
+
+// ======================================================================================
+// Probe: routing_filter_lookup (src/routing_filter.c:985-1073), one lane per probe
+// ======================================================================================
+__device__ __forceinline__ uint64_t probe_one(const FilterPlan& P, const uint8_t* pages,
+                                              const uint64_t* slots, uint32_t h, uint32_t fp_size,
+                                              uint32_t lis, uint32_t page_size) {
+  const uint32_t index_size = 1u << lis;
+  const uint32_t fp = h >> (32 - fp_size);
+  const uint32_t x = fp << P.vs;
+  const uint32_t bucket = P.rvs >= 32 ? 0u : x >> P.rvs;
+  const uint32_t bo = bucket & (index_size - 1);
+  const uint32_t irvs = P.rvs + lis;
+  const uint32_t index = irvs >= 32 ? 0u : x >> irvs;
+  const uint32_t remmask = P.rem >= 32 ? 0xffffffffu : ((1u << P.rem) - 1);
+  const uint32_t remainder = fp & remmask;
+  const uint8_t* pg = pages + (uint64_t)P.page_base * page_size;
+  const uint64_t hdr = slots[P.idx_base + index];
+  const uint32_t c = (uint32_t)pg[hdr] | ((uint32_t)pg[hdr + 1] << 8);
+  const uint32_t enc = (c + index_size - 1) / 8 + 4;
+  const uint64_t ebit = (hdr + 2) * 8;
+  // select: position of 1-bit #(bo-1) and #bo (0-based) in the encoding
+  uint32_t start = 0, end = 0, cum = 0;
+  bool have_start = (bo == 0);
+  const uint32_t wmax = (c + index_size) / 56 + 2;  // bound: a corrupt image cannot hang the wave
+  for (uint32_t w = 0;; w++) {
+    if (w > wmax) return 0;
+    const uint64_t bp = ebit + (uint64_t)w * 56;  // 56-bit steps keep the byte shift in range
+    const uint64_t xw = (ld_u64_unaligned(pg, bp >> 3) >> (bp & 7)) & ((1ull << 56) - 1);
+    const uint32_t pc = __popcll(xw);
+    if (!have_start && cum + pc > bo - 1) {
+      start = w * 56 + select64(xw, bo - 1 - cum) + 1 - bo;
+      have_start = true;
+    }
+    if (cum + pc > bo) {
+      end = w * 56 + select64(xw, bo - cum) - bo;
+      break;
+    }
+    cum += pc;
+  }
+  if (start == end) return 0;
+  const uint64_t rbit = (hdr + 2 + enc) * 8;
+  const uint32_t vmask = (uint32_t)((1ull << P.vs) - 1);
+  uint64_t found = 0;
+  for (uint32_t pos = start; pos < end; pos++) {
+    const uint32_t rv = ld_bits(pg, rbit + (uint64_t)pos * P.rvs, P.rvs);
+    if ((rv >> P.vs) == remainder) {
+      const uint32_t v = rv & vmask;
+      if (v < 64) found |= 1ull << v;
+    }
+  }
+  return found;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_probe(const FilterPlan* __restrict__ plans,
+                                               const uint8_t* __restrict__ pages,
+                                               const uint64_t* __restrict__ slots,
+                                               const void* __restrict__ in0,
+                                               const uint64_t* __restrict__ offs, uint32_t key_len,
+                                               const uint32_t* __restrict__ filter_id, uint64_t n,
+                                               uint64_t* __restrict__ found, uint32_t fp_size,
+                                               uint32_t seed, uint32_t lis, uint32_t page_size,
+                                               uint32_t num_filters, const FilterOut* __restrict__ outs) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t fid = filter_id[i];
+  if (fid >= num_filters || (outs && outs[fid].error)) {  // unknown / failed filter finds nothing
+    found[i] = 0;
+    return;
+  }
+  uint32_t h;
+  if constexpr (KIND == IN_KEYS24) {
+    const uint2* kp = reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(in0) + i * 24);
+    uint2 a = kp[0], b = kp[1], c = kp[2];
+    uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    h = xxh32_24(w, seed);
+  } else if constexpr (KIND == IN_KEYS_W) {
+    h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + i * key_len),
+                    key_len, seed);
+  } else if constexpr (KIND == IN_KEYS_B) {
+    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + i * key_len, key_len, seed);
+  } else if constexpr (KIND == IN_VAR) {
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
+  } else {
+    h = static_cast<const uint32_t*>(in0)[i];
+  }
+  const FilterPlan& P = plans[fid];
+  found[i] = probe_one(P, pages, slots, h, fp_size, lis, page_size);
+}
+
+// ======================================================================================
+// launch wrappers (called from rf_engine.cpp)
+// ======================================================================================
+#define CHECK_LAUNCH() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
+#define REC(slot) do { if (a.events) (void)hipEventRecord((hipEvent_t)a.events[slot], (hipStream_t)a.stream); } while (0)
+
+template <typename EntT>
+static int launch_hash_count_t(int kind, const LaunchArgs& a, EntT* ent) {
+  dim3 g(a.num_tiles), b(TILE_NT);
+  switch (kind) {
+    case IN_KEYS24: hipLaunchKernelGGL((k_hash_count<IN_KEYS24, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
+    case IN_KEYS_W: hipLaunchKernelGGL((k_hash_count<IN_KEYS_W, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
+    case IN_KEYS_B: hipLaunchKernelGGL((k_hash_count<IN_KEYS_B, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
+    case IN_VAR:    hipLaunchKernelGGL((k_hash_count<IN_VAR, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
+    default:        hipLaunchKernelGGL((k_hash_count<IN_HASH, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
+  }
+  CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename EntT>
+static int launch_rest_t(const LaunchArgs& a, EntT* ent, EntT* part) {
+  if (a.num_tiles) {
+    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_tiles), dim3(TILE_NT), 0, (hipStream_t)a.stream, a.plans,
+                       a.tile_filter, a.tile_start, 0u, a.fp_size, ent, part, a.cb_cursor);
+    CHECK_LAUNCH();
+  }
+  if (a.num_old_tiles) {
+    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_old_tiles), dim3(TILE_NT), 0, (hipStream_t)a.stream, a.plans,
+                       a.old_tile_filter, a.old_tile_start, 1u, a.fp_size, ent, part, a.cb_cursor);
+    CHECK_LAUNCH();
+  }
+  REC(EV_B_SCATTER);
+  hipLaunchKernelGGL((k_cb_sort<EntT>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
+                     a.cb_count, a.cb_start, part, a.sorted32, a.idx_cnt, a.idx_start, a.outs, a.overflow,
+                     a.lis);
+  CHECK_LAUNCH();
+  REC(EV_B_SORT);
+  hipLaunchKernelGGL((k_cb_sort_big<EntT>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
+                     a.cb_count, a.cb_start, part, ent, a.sorted32, a.idx_cnt, a.idx_start, a.outs,
+                     a.overflow, a.lis);
+  CHECK_LAUNCH();
+  REC(EV_B_SORT_BIG);
+  return 0;
+}
+
+extern "C" int rf_launch_build(const LaunchArgs* pa) {
+  const LaunchArgs& a = *pa;
+  if (a.wide) {
+    uint64_t* ent = (uint64_t*)a.ent;
+    // old entries first (they were decoded into the old region by rf_launch_old_decode)
+    if (a.num_old_tiles) {
+      hipLaunchKernelGGL(k_old_count, dim3(a.num_old_tiles), dim3(TILE_NT), 0, (hipStream_t)a.stream, a.plans,
+                         a.old_tile_filter, a.old_tile_start, a.fp_size, ent, a.cb_count);
+      CHECK_LAUNCH();
+    }
+    if (a.num_tiles) { int rc = launch_hash_count_t<uint64_t>(a.kind, a, ent); if (rc) return rc; }
+  } else {
+    if (a.num_tiles) { int rc = launch_hash_count_t<uint32_t>(a.kind, a, (uint32_t*)a.ent); if (rc) return rc; }
+  }
+  REC(EV_B_HASH);
+  hipLaunchKernelGGL(k_cb_scan, dim3(a.num_filters), dim3(256), 0, (hipStream_t)a.stream, a.plans, a.cb_count,
+                     a.cb_start, a.cb_cursor);
+  CHECK_LAUNCH();
+  REC(EV_B_SCAN);
+  int rc = a.wide ? launch_rest_t<uint64_t>(a, (uint64_t*)a.ent, (uint64_t*)a.part)
+                  : launch_rest_t<uint32_t>(a, (uint32_t*)a.ent, (uint32_t*)a.part);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_layout, dim3(a.num_filters), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, a.plans, a.idx_cnt,
+                     a.slots, a.page_first, a.outs, a.lis, a.page_size);
+  CHECK_LAUNCH();
+  REC(EV_B_LAYOUT);
+  hipLaunchKernelGGL(k_assemble, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans, a.pg_filter,
+                     a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages, a.lis,
+                     a.page_size);
+  CHECK_LAUNCH();
+  REC(EV_B_ASSEMBLE);
+  return 0;
+}
+
+extern "C" int rf_launch_old_decode(const LaunchArgs* pa, uint32_t f, uint32_t old_num_indices,
+                                    uint32_t* d_cnt, uint32_t* d_pos) {
+  const LaunchArgs& a = *pa;
+  hipLaunchKernelGGL(k_old_counts, dim3((old_num_indices + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a.plans, f,
+                     d_cnt);
+  CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, d_cnt, d_pos, old_num_indices);
+  CHECK_LAUNCH();
+  const uint32_t waves_per_block = 256 / WAVE;
+  hipLaunchKernelGGL(k_old_decode, dim3((old_num_indices + waves_per_block - 1) / waves_per_block), dim3(256),
+                     0, (hipStream_t)a.stream, a.plans, f, d_pos, (uint64_t*)a.ent, a.lis, a.fp_size);
+  CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, const uint64_t* offs,
+                               uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found) {
+  const LaunchArgs& a = *pa;
+  if (n == 0) return 0;
+  dim3 g((uint32_t)((n + 255) / 256)), b(256);
+  REC(EV_P_START);
+  switch (kind) {
+    case IN_KEYS24: hipLaunchKernelGGL(k_probe<IN_KEYS24>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_KEYS_W: hipLaunchKernelGGL(k_probe<IN_KEYS_W>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_KEYS_B: hipLaunchKernelGGL(k_probe<IN_KEYS_B>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_VAR:    hipLaunchKernelGGL(k_probe<IN_VAR>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    default:        hipLaunchKernelGGL(k_probe<IN_HASH>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+  }
+  CHECK_LAUNCH();
+  REC(EV_P_END);
+  return 0;
+}

@@ -1,0 +1,93 @@
+// rf_plan.h -- host/device shared batch plan of the routing-filter engine.
+#pragma once
+#include <stdint.h>
+
+namespace rf {
+
+// geometry limits (page 4096 B, 32-page extents: 16384 index slots, src/routing_filter.h:120-127)
+constexpr uint32_t MAX_PAGE = 4096;
+constexpr uint32_t MAX_INDICES = 16384;
+constexpr uint32_t MAX_LIS = 12;
+constexpr uint32_t CB_LOG_MEAN = 12;  // coarse bucket ~ 2^12..2^13 entries
+constexpr uint32_t MAX_CB = 2048;     // coarse buckets per filter (lnb <= 23)
+constexpr uint32_t MAX_BINS = 4096;   // filter buckets per coarse bucket
+
+// kernel shapes
+constexpr int TILE_NT = 256;
+constexpr int TILE_KEYS = 4096;  // keys per K1/K3 tile
+constexpr int SORT_NT = 512;
+constexpr int SORT_CAP = 12288;  // entries per coarse bucket held in LDS
+constexpr int BIG_NT = 1024;
+constexpr int BIG_GRID = 64;
+constexpr int LAYOUT_NT = 1024;
+constexpr int ASM_NT = 256;
+
+enum InputKind { IN_KEYS24 = 0, IN_KEYS_W = 1, IN_KEYS_B = 2, IN_VAR = 3, IN_HASH = 4 };
+
+constexpr uint32_t ERR_INDEX_OVERFLOW = 1u, ERR_BLOCK_TOO_BIG = 2u, ERR_PAGE_CAP = 4u,
+                   ERR_GEOMETRY = 8u;
+
+struct FilterPlan {
+  uint64_t e_first;    // first entry slot of this filter in the entry arrays
+  uint64_t key_first;  // first input (key / hash) of this filter's new fingerprints
+  uint32_t num_new;    // new fingerprints
+  uint32_t old_region; // entry slots reserved for decoded old entries (old num_fingerprints)
+  uint32_t num_fp;     // routing_filter.num_fingerprints (new + old)
+  uint32_t value;
+  uint32_t vs, rem, rvs, lnb;
+  uint32_t num_indices;
+  uint32_t cbits, bbits;  // coarse-bucket bits, bucket-in-coarse-bucket bits (sum = lnb)
+  uint32_t cb_base, idx_base, page_base, page_cap, pf_base;
+  // old filter (incremental add)
+  uint32_t old_num_indices, old_vs, old_rvs, pad0;
+  const uint8_t* old_pages;
+  const uint64_t* old_slots;
+};
+
+struct FilterOut {
+  uint32_t num_unique;
+  uint32_t num_pages;
+  uint32_t error;
+  uint32_t pad;
+};
+
+struct LaunchArgs {
+  void* stream;
+  int kind;
+  int wide;  // 64-bit entries (old/new flag) -- only for incremental adds
+  const FilterPlan* plans;
+  uint32_t num_filters;
+  const uint32_t* tile_filter;
+  const uint32_t* tile_start;
+  uint32_t num_tiles;
+  const uint32_t* old_tile_filter;
+  const uint32_t* old_tile_start;
+  uint32_t num_old_tiles;
+  const void* in0;
+  const uint64_t* offs;
+  uint32_t key_len, fp_size, seed, lis, page_size;
+  void* ent;
+  void* part;
+  uint32_t* sorted32;
+  uint32_t* cb_count;
+  uint32_t* cb_start;
+  uint32_t* cb_cursor;
+  const uint32_t* cb_filter;
+  uint32_t num_cb;
+  uint32_t* overflow;
+  uint32_t* idx_cnt;
+  uint32_t* idx_start;
+  uint64_t* slots;
+  uint32_t* page_first;
+  const uint32_t* pg_filter;
+  uint32_t num_page_slots;
+  uint8_t* pages;
+  FilterOut* outs;
+  void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)
+};
+
+// per-stage timing events: build = [B_START .. B_ASSEMBLE], probe = [P_START, P_END]
+enum EventSlot { EV_B_START = 0, EV_B_HASH, EV_B_SCAN, EV_B_SCATTER, EV_B_SORT, EV_B_SORT_BIG,
+                 EV_B_LAYOUT, EV_B_ASSEMBLE, EV_P_START, EV_P_END, NUM_EVENTS };
+
+}  // namespace rf

@@ -1,0 +1,419 @@
+"""Python host mirror of SplinterDB's routing_filter.h API over the MI355X engine's C ABI.
+
+Names, argument meaning and errors follow the reference interface
+(src/routing_filter.h:32-192): `routing_config_init`, `routing_filter_add`,
+`routing_filter_lookup`, `routing_filter_get_next_value`, `routing_filter_is_value_found`,
+`routing_filter_max_fingerprints`, `routing_filter_estimate_unique_keys_from_count`,
+`routing_filter_space_use_bytes`. Errors raise `PlatformStatusError` carrying the
+platform_status code (ENOMEM / EINVAL / ENODEV).
+
+The compute runs only in librf_amd.so (hand-written HIP kernels for gfx950). There is
+no CPU fallback: without the library or a HIP device every call raises.
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librf_amd.so")
+
+STATUS_OK = 0
+STATUS_NO_MEMORY = 12
+STATUS_NO_DEVICE = 19
+STATUS_BAD_PARAM = 22
+MAX_FILTERS = 32  # src/routing_filter.h:25
+ROUTING_NOT_FOUND = 0xFFFF  # src/routing_filter.h:26
+
+# symbols the C ABI (include/rf_amd.h) exports
+EXPORTED = [
+    "rf_amd_engine_create", "rf_amd_engine_destroy", "rf_amd_last_error",
+    "rf_amd_batch_create", "rf_amd_batch_destroy", "rf_amd_batch_build_keys",
+    "rf_amd_batch_build_var_keys", "rf_amd_batch_build_hashes", "rf_amd_batch_probe_keys",
+    "rf_amd_batch_probe_var_keys", "rf_amd_batch_probe_hashes", "rf_amd_batch_info",
+    "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
+    "rf_amd_batch_set_timing", "rf_amd_batch_timings",
+    "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",
+    "rf_amd_image_free",
+    "rf_amd_max_fingerprints", "rf_amd_estimate_unique_keys_from_count",
+    "rf_amd_space_use_bytes",
+]
+
+
+class PlatformStatusError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"platform_status {code}: {msg}")
+        self.code = code
+
+
+class RfConfig(ctypes.Structure):
+    _fields_ = [("fingerprint_size", ctypes.c_uint32), ("log_index_size", ctypes.c_uint32),
+                ("seed", ctypes.c_uint32), ("page_size", ctypes.c_uint32),
+                ("pages_per_extent", ctypes.c_uint32)]
+
+
+class RfFilterInfo(ctypes.Structure):
+    _fields_ = [("num_fingerprints", ctypes.c_uint32), ("num_unique", ctypes.c_uint32),
+                ("value_size", ctypes.c_uint32), ("num_indices", ctypes.c_uint32),
+                ("num_pages", ctypes.c_uint32), ("error", ctypes.c_uint32)]
+
+
+class RfImage(ctypes.Structure):
+    _fields_ = [("info", RfFilterInfo), ("pages", ctypes.POINTER(ctypes.c_uint8)),
+                ("slots", ctypes.POINTER(ctypes.c_uint64))]
+
+
+_lib = None
+
+
+def load_library(build_if_missing=True):
+    """Load librf_amd.so (building it in-tree with hipcc if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if not build_if_missing:
+            raise PlatformStatusError(STATUS_NO_DEVICE, f"{LIB_PATH} missing (run build)")
+        from . import build as _b
+        _b.build()
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    L.rf_amd_last_error.restype = ctypes.c_char_p
+    L.rf_amd_engine_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.rf_amd_engine_destroy.argtypes = [vp]
+    L.rf_amd_engine_destroy.restype = None
+    L.rf_amd_batch_create.argtypes = [vp, ctypes.POINTER(RfConfig), u32, vp, vp, vp, vp,
+                                      ctypes.POINTER(vp)]
+    L.rf_amd_batch_destroy.argtypes = [vp]
+    L.rf_amd_batch_destroy.restype = None
+    L.rf_amd_batch_build_keys.argtypes = [vp, vp, u32, vp]
+    L.rf_amd_batch_build_var_keys.argtypes = [vp, vp, vp, vp]
+    L.rf_amd_batch_build_hashes.argtypes = [vp, vp, vp]
+    L.rf_amd_batch_probe_keys.argtypes = [vp, vp, u32, vp, u64, vp, vp]
+    L.rf_amd_batch_probe_var_keys.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+    L.rf_amd_batch_probe_hashes.argtypes = [vp, vp, vp, u64, vp, vp]
+    L.rf_amd_batch_info.argtypes = [vp, u32, ctypes.POINTER(RfFilterInfo)]
+    L.rf_amd_batch_read_image.argtypes = [vp, u32, vp, u64, vp, u32]
+    L.rf_amd_batch_read_image_async.argtypes = [vp, u32, vp, u64, vp, u32, vp]
+    L.rf_amd_batch_image_ptrs.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    L.rf_amd_batch_set_timing.argtypes = [vp, i32]
+    L.rf_amd_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), u32]
+    L.rf_amd_batch_num_filters.argtypes = [vp]
+    L.rf_amd_batch_num_filters.restype = u32
+    L.rf_amd_filter_add.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),
+                                    ctypes.POINTER(RfImage), vp, u64, ctypes.c_uint16]
+    L.rf_amd_filter_lookup_hashes.argtypes = [vp, ctypes.POINTER(RfConfig),
+                                              ctypes.POINTER(RfImage), vp, u64, vp]
+    L.rf_amd_filter_lookup_keys.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),
+                                            vp, u32, u64, vp]
+    L.rf_amd_image_free.argtypes = [ctypes.POINTER(RfImage)]
+    L.rf_amd_image_free.restype = None
+    L.rf_amd_max_fingerprints.argtypes = [ctypes.POINTER(RfConfig)]
+    L.rf_amd_max_fingerprints.restype = u64
+    L.rf_amd_estimate_unique_keys_from_count.argtypes = [ctypes.POINTER(RfConfig), u64]
+    L.rf_amd_estimate_unique_keys_from_count.restype = u32
+    L.rf_amd_space_use_bytes.argtypes = [ctypes.POINTER(RfConfig), u32]
+    L.rf_amd_space_use_bytes.restype = u64
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise PlatformStatusError(rc, load_library().rf_amd_last_error().decode())
+
+
+# ---- routing_config (src/routing_filter.h:32-58) --------------------------------------
+@dataclass
+class RoutingConfig:
+    fingerprint_size: int = 26
+    log_index_size: int = 8
+    seed: int = 42
+    page_size: int = 4096
+    pages_per_extent: int = 32
+
+    @property
+    def index_size(self):
+        return 1 << self.log_index_size
+
+    def c(self):
+        return RfConfig(self.fingerprint_size, self.log_index_size, self.seed, self.page_size,
+                        self.pages_per_extent)
+
+
+def routing_config_init(fingerprint_size=26, log_index_size=8, seed=42, page_size=4096,
+                        pages_per_extent=32):
+    """routing_config_init (src/routing_filter.h:42-58); the key_hash argument of the
+    reference is ignored there too -- hashing is XXH32 with `seed`."""
+    return RoutingConfig(fingerprint_size, log_index_size, seed, page_size, pages_per_extent)
+
+
+class Engine:
+    """One HIP device + stream. Raises PlatformStatusError(ENODEV) without a GPU."""
+
+    def __init__(self, device=0):
+        L = load_library()
+        h = ctypes.c_void_p()
+        _check(L.rf_amd_engine_create(device, ctypes.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            load_library().rf_amd_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_engine = None
+
+
+def default_engine():
+    global _default_engine
+    if _default_engine is None:
+        _default_engine = Engine(0)
+    return _default_engine
+
+
+# ---- routing_filter descriptor + image -----------------------------------------------
+@dataclass
+class RoutingFilter:
+    """routing_filter (src/routing_filter.h:66-72) plus its relocatable page image:
+    pages = num_pages * page_size bytes, slots[i] = data_page_no * page_size + offset."""
+    num_fingerprints: int
+    num_unique: int
+    value_size: int
+    num_indices: int
+    num_pages: int
+    pages: np.ndarray
+    slots: np.ndarray
+
+    def _c(self):
+        img = RfImage()
+        img.info = RfFilterInfo(self.num_fingerprints, self.num_unique, self.value_size,
+                                self.num_indices, self.num_pages, 0)
+        self._pages_c = np.ascontiguousarray(self.pages, dtype=np.uint8)
+        self._slots_c = np.ascontiguousarray(self.slots, dtype=np.uint64)
+        img.pages = self._pages_c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        img.slots = self._slots_c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        return img
+
+
+NULL_ROUTING_FILTER = None
+
+
+def routing_filter_add(cfg: RoutingConfig, old_filter, new_fp_arr, value=0, engine=None):
+    """routing_filter_add (src/routing_filter.h:78-85): 32-bit key hashes in, new filter
+    out. new_fp_arr is not modified (the reference shifts/sorts it in place)."""
+    eng = engine or default_engine()
+    L = load_library()
+    fps = np.ascontiguousarray(new_fp_arr, dtype=np.uint32)
+    out = RfImage()
+    old_c = old_filter._c() if old_filter is not None else None
+    _check(L.rf_amd_filter_add(eng.h, ctypes.byref(cfg.c()),
+                               ctypes.byref(old_c) if old_c is not None else None,
+                               ctypes.byref(out), fps.ctypes.data if fps.size else None,
+                               fps.size, value))
+    try:
+        info = out.info
+        npg = info.num_pages * cfg.page_size
+        pages = np.ctypeslib.as_array(out.pages, shape=(npg,)).copy()
+        slots = np.ctypeslib.as_array(out.slots, shape=(info.num_indices,)).copy()
+    finally:
+        L.rf_amd_image_free(ctypes.byref(out))
+    return RoutingFilter(info.num_fingerprints, info.num_unique, info.value_size,
+                         info.num_indices, info.num_pages, pages, slots)
+
+
+def routing_filter_lookup_hashes(cfg: RoutingConfig, filt, hashes, engine=None):
+    eng = engine or default_engine()
+    L = load_library()
+    h = np.ascontiguousarray(hashes, dtype=np.uint32)
+    out = np.zeros(h.size, dtype=np.uint64)
+    fc = filt._c() if filt is not None else None
+    _check(L.rf_amd_filter_lookup_hashes(eng.h, ctypes.byref(cfg.c()),
+                                         ctypes.byref(fc) if fc is not None else None,
+                                         h.ctypes.data, h.size, out.ctypes.data))
+    return out
+
+
+def routing_filter_lookup_keys(cfg: RoutingConfig, filt, keys: np.ndarray, engine=None):
+    """Fixed-length keys (n x key_len uint8) hashed and probed on the GPU."""
+    eng = engine or default_engine()
+    L = load_library()
+    k = np.ascontiguousarray(keys, dtype=np.uint8)
+    if k.ndim == 1:
+        k = k.reshape(1, -1)
+    out = np.zeros(k.shape[0], dtype=np.uint64)
+    fc = filt._c() if filt is not None else None
+    _check(L.rf_amd_filter_lookup_keys(eng.h, ctypes.byref(cfg.c()),
+                                       ctypes.byref(fc) if fc is not None else None,
+                                       k.ctypes.data, k.shape[1], k.shape[0], out.ctypes.data))
+    return out
+
+
+def routing_filter_lookup(cfg: RoutingConfig, filt, key: bytes, engine=None):
+    """routing_filter_lookup (src/routing_filter.h:87-92) for one key; returns found_values."""
+    arr = np.frombuffer(bytes(key), dtype=np.uint8)
+    return int(routing_filter_lookup_keys(cfg, filt, arr, engine)[0])
+
+
+def routing_filter_get_next_value(found_values: int, last_value: int) -> int:
+    """src/routing_filter.h:94-105 (the reference builds its mask with an int shift)."""
+    if last_value != ROUTING_NOT_FOUND:
+        mask = ((1 << last_value) - 1) & 0xFFFFFFFFFFFFFFFF
+        found_values &= mask
+    if found_values == 0:
+        return ROUTING_NOT_FOUND
+    return found_values.bit_length() - 1
+
+
+def routing_filter_is_value_found(found_values: int, value: int) -> bool:
+    return (found_values & (1 << value)) != 0
+
+
+def routing_filter_max_fingerprints(cfg: RoutingConfig) -> int:
+    return load_library().rf_amd_max_fingerprints(ctypes.byref(cfg.c()))
+
+
+def routing_filter_estimate_unique_keys_from_count(cfg: RoutingConfig, num_unique: int) -> int:
+    return load_library().rf_amd_estimate_unique_keys_from_count(ctypes.byref(cfg.c()), num_unique)
+
+
+def routing_filter_estimate_unique_keys(filt: RoutingFilter, cfg: RoutingConfig) -> int:
+    return routing_filter_estimate_unique_keys_from_count(cfg, filt.num_unique)
+
+
+def routing_filter_space_use_bytes(cfg: RoutingConfig, filt: RoutingFilter) -> int:
+    if filt is None:
+        return 0
+    return load_library().rf_amd_space_use_bytes(ctypes.byref(cfg.c()), filt.num_pages)
+
+
+# ---- batched device-resident engine -----------------------------------------------------
+def _stream(stream):
+    """The caller's stream: explicit handle, else torch's current stream when torch has a
+    live HIP context and uses a non-default stream, else None (the engine's blocking
+    stream, which is ordered with the legacy null stream)."""
+    if stream is not None:
+        return stream
+    import sys
+    t = sys.modules.get("torch")
+    if t is not None and t.cuda.is_initialized():
+        h = t.cuda.current_stream().cuda_stream
+        return h or None
+    return None
+
+
+def _dptr(x):
+    """Device pointer of a torch tensor (or an int address)."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+class FilterBatch:
+    """F independent filters built in one launch sequence on the device.
+
+    num_new[f] inputs feed filter f (runs concatenated in filter order); old=[(batch, i)
+    or None] merges a previously built filter (incremental routing_filter_add)."""
+
+    def __init__(self, cfg: RoutingConfig, num_new, values=None, old=None, engine=None):
+        self.engine = engine or default_engine()
+        self.cfg = cfg
+        L = load_library()
+        nn = np.ascontiguousarray(num_new, dtype=np.uint32)
+        self.F = nn.size
+        vals = np.ascontiguousarray(values if values is not None else np.zeros(self.F),
+                                    dtype=np.uint16)
+        self.num_new = nn
+        self.values = vals
+        self._keep = [nn, vals]
+        ob_arr = oi_arr = None
+        if old is not None:
+            ob_arr = (ctypes.c_void_p * self.F)(*[(o[0].h.value if o else None) for o in old])
+            oi_arr = np.ascontiguousarray([(o[1] if o else 0) for o in old], dtype=np.uint32)
+            self._keep += [ob_arr, oi_arr, [o[0] for o in old if o]]
+        h = ctypes.c_void_p()
+        _check(L.rf_amd_batch_create(self.engine.h, ctypes.byref(cfg.c()), self.F,
+                                     nn.ctypes.data, vals.ctypes.data,
+                                     ctypes.cast(ob_arr, ctypes.c_void_p) if ob_arr is not None else None,
+                                     oi_arr.ctypes.data if oi_arr is not None else None,
+                                     ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rf_amd_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def build_keys(self, d_keys, key_len, stream=None):
+        _check(load_library().rf_amd_batch_build_keys(self.h, _dptr(d_keys), key_len, _stream(stream)))
+
+    def build_var_keys(self, d_bytes, d_offsets, stream=None):
+        _check(load_library().rf_amd_batch_build_var_keys(self.h, _dptr(d_bytes), _dptr(d_offsets),
+                                                          _stream(stream)))
+
+    def build_hashes(self, d_hashes, stream=None):
+        _check(load_library().rf_amd_batch_build_hashes(self.h, _dptr(d_hashes), _stream(stream)))
+
+    def probe_keys(self, d_keys, key_len, d_filter_id, n, d_found, stream=None):
+        _check(load_library().rf_amd_batch_probe_keys(self.h, _dptr(d_keys), key_len,
+                                                      _dptr(d_filter_id), n, _dptr(d_found), _stream(stream)))
+
+    def probe_var_keys(self, d_bytes, d_offsets, d_filter_id, n, d_found, stream=None):
+        _check(load_library().rf_amd_batch_probe_var_keys(self.h, _dptr(d_bytes), _dptr(d_offsets),
+                                                          _dptr(d_filter_id), n, _dptr(d_found),
+                                                          _stream(stream)))
+
+    def probe_hashes(self, d_hashes, d_filter_id, n, d_found, stream=None):
+        _check(load_library().rf_amd_batch_probe_hashes(self.h, _dptr(d_hashes), _dptr(d_filter_id),
+                                                        n, _dptr(d_found), _stream(stream)))
+
+    STAGES = ["hash_count", "cb_scan", "scatter", "cb_sort", "cb_sort_big", "layout",
+              "assemble", "build_total", "probe"]
+
+    def set_timing(self, enable=True):
+        _check(load_library().rf_amd_batch_set_timing(self.h, 1 if enable else 0))
+
+    def timings(self):
+        """Per-stage milliseconds of the last build / probe (HIP events on the launch stream)."""
+        arr = (ctypes.c_float * len(self.STAGES))()
+        _check(load_library().rf_amd_batch_timings(self.h, arr, len(self.STAGES)))
+        return dict(zip(self.STAGES, [float(x) for x in arr]))
+
+    def info(self, f):
+        out = RfFilterInfo()
+        _check(load_library().rf_amd_batch_info(self.h, f, ctypes.byref(out)))
+        return out
+
+    def read_image_async(self, f, h_pages, h_slots, stream=None):
+        """D2H of filter f's pages/slots into (pinned) host tensors sized by the caller."""
+        _check(load_library().rf_amd_batch_read_image_async(
+            self.h, f, h_pages.data_ptr(), h_pages.numel(), h_slots.data_ptr(), h_slots.numel(),
+            _stream(stream)))
+
+    def image(self, f) -> RoutingFilter:
+        inf = self.info(f)
+        if inf.error:
+            raise PlatformStatusError(STATUS_BAD_PARAM, f"filter {f} error bits {inf.error:#x}")
+        pages = np.zeros(inf.num_pages * self.cfg.page_size, dtype=np.uint8)
+        slots = np.zeros(inf.num_indices, dtype=np.uint64)
+        _check(load_library().rf_amd_batch_read_image(self.h, f, pages.ctypes.data, pages.size,
+                                                      slots.ctypes.data, slots.size))
+        return RoutingFilter(inf.num_fingerprints, inf.num_unique, inf.value_size,
+                             inf.num_indices, inf.num_pages, pages, slots)
