@@ -73,7 +73,7 @@ struct rf_amd_batch {
   uint32_t CB = 0, I = 0, PS = 0, PF = 0;
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
-      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos;
+      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old;
   std::vector<uint32_t> old_num_indices;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing (rf_amd_batch_set_timing)
@@ -194,6 +194,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       p.old_num_indices = op->num_indices;
       p.old_vs = op->vs;
       p.old_rvs = op->rvs;
+      p.npo = p.num_indices / op->num_indices;
       p.old_pages = ob->d_pages.as<uint8_t>() + (uint64_t)op->page_base * P;
       p.old_slots = ob->d_slots.as<uint64_t>() + op->idx_base;
       b->old_num_indices[f] = op->num_indices;
@@ -246,6 +247,8 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   if (b->wide) {
     rc |= b->d_old_cnt.alloc(4 * MAX_INDICES);
     rc |= b->d_old_pos.alloc(4 * MAX_INDICES);
+    rc |= b->d_first_old.alloc(4 * b->I);
+    rc |= b->d_has_old.alloc(4 * b->I);
   }
   if (rc) {
     delete b;
@@ -305,6 +308,8 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.overflow = b->d_overflow.as<uint32_t>();
   a.idx_cnt = b->d_idx_cnt.as<uint32_t>();
   a.idx_start = b->d_idx_start.as<uint32_t>();
+  a.first_old = b->d_first_old.as<uint32_t>();
+  a.has_old = b->d_has_old.as<uint32_t>();
   a.slots = b->d_slots.as<uint64_t>();
   a.page_first = b->d_page_first.as<uint32_t>();
   a.pg_filter = b->d_pg_filter.as<uint32_t>();

@@ -274,11 +274,14 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
                                                      uint32_t* __restrict__ idx_start,
                                                      FilterOut* __restrict__ outs,
                                                      uint32_t* __restrict__ overflow,
-                                                     uint32_t lis) {
+                                                     uint32_t lis, uint32_t* __restrict__ first_old,
+                                                     uint32_t* __restrict__ has_old) {
   constexpr int PER = SORT_CAP / SORT_NT;
   __shared__ EntT s_b[SORT_CAP];
   __shared__ uint32_t s_bin[MAX_BINS + 1];
   __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
+  __shared__ uint32_t s_fo[sizeof(EntT) == 8 ? MAX_IPC : 1];
+  __shared__ uint32_t s_ho[sizeof(EntT) == 8 ? MAX_IPC : 1];
   const uint32_t cb = blockIdx.x;
   const uint32_t f = cb_filter[cb];
   const FilterPlan& P = plans[f];
@@ -291,7 +294,11 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
   }
   const uint32_t nbins = 1u << P.bbits;
   const uint32_t bmask = nbins - 1;
+  const uint32_t ipc = 1u << (P.bbits - lis), ish = lis + P.rvs;
   for (uint32_t i = threadIdx.x; i <= nbins; i += SORT_NT) s_bin[i] = 0;
+  if constexpr (sizeof(EntT) == 8) {
+    for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
+  }
   __syncthreads();
   // load + per-bin rank (bin = filter bucket within the coarse bucket)
   EntT v[PER];
@@ -375,9 +382,25 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
   uint32_t* s_sorted = reinterpret_cast<uint32_t*>(s_b);        // compacted e values (u32)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    if (keep_mask & (1u << k)) s_sorted[pos++] = ent_e(w[k]);
+    if (keep_mask & (1u << k)) {
+      const uint32_t e = ent_e(w[k]);
+      s_sorted[pos++] = e;
+      if constexpr (sizeof(EntT) == 8) {
+        if (!(w[k] & 1ull)) {  // old entry: remember each index's smallest (num_unique quirk)
+          const uint32_t li = ish >= 32 ? 0u : ((e >> ish) & (ipc - 1));
+          atomicMin(&s_fo[li], e);
+          s_ho[li] = 1;
+        }
+      }
+    }
   }
   __syncthreads();
+  if constexpr (sizeof(EntT) == 8) {
+    for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) {
+      first_old[c.idx0 + i] = s_fo[i];
+      has_old[c.idx0 + i] = s_ho[i];
+    }
+  }
   uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
   for (uint32_t i = threadIdx.x; i < kept; i += SORT_NT) dst[i] = s_sorted[i];
   uint32_t uniq, tot_uniq;
@@ -400,8 +423,11 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
                                                         uint32_t* __restrict__ idx_start,
                                                         FilterOut* __restrict__ outs,
                                                         const uint32_t* __restrict__ overflow,
-                                                        uint32_t lis) {
+                                                        uint32_t lis, uint32_t* __restrict__ first_old,
+                                                        uint32_t* __restrict__ has_old) {
   __shared__ uint32_t s_bin[MAX_BINS + 1];
+  __shared__ uint32_t s_fo[MAX_IPC];
+  __shared__ uint32_t s_ho[MAX_IPC];
   __shared__ uint32_t s_cur[MAX_BINS];
   __shared__ uint32_t s_tmp[BIG_NT / WAVE + 1];
   __shared__ uint32_t s_run;
@@ -417,7 +443,9 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     const EntT* src = part + P.e_first + c.cb_rel;
     EntT* tmp = scratch + P.e_first + c.cb_rel;
     uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
+    const uint32_t ipc = 1u << (P.bbits - lis), ish = lis + P.rvs;
     for (uint32_t i = threadIdx.x; i <= nbins; i += BIG_NT) s_bin[i] = 0;
+    for (uint32_t i = threadIdx.x; i < ipc; i += BIG_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += BIG_NT) {
       const uint32_t e = ent_e(src[i]);
@@ -467,12 +495,28 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
       uint32_t tot;
       const uint32_t p = block_excl_scan<BIG_NT>(keep, s_tmp, &tot);
       const uint32_t run = s_run;
-      if (keep) dst[run + p] = ent_e(x);
+      if (keep) {
+        dst[run + p] = ent_e(x);
+        if constexpr (sizeof(EntT) == 8) {
+          if (!(x & 1ull)) {
+            const uint32_t e = ent_e(x);
+            const uint32_t li = ish >= 32 ? 0u : ((e >> ish) & (ipc - 1));
+            atomicMin(&s_fo[li], e);
+            s_ho[li] = 1;
+          }
+        }
+      }
       __syncthreads();
       if (threadIdx.x == 0) s_run = run + tot;
       __syncthreads();
     }
     const uint32_t kept = s_run;
+    if constexpr (sizeof(EntT) == 8) {
+      for (uint32_t i = threadIdx.x; i < ipc; i += BIG_NT) {
+        first_old[c.idx0 + i] = s_fo[i];
+        has_old[c.idx0 + i] = s_ho[i];
+      }
+    }
     uint32_t uniq, tot_uniq;
     write_index_bounds(c, dst, kept, idx_cnt, idx_start, &uniq);
     block_excl_scan<BIG_NT>(uniq, s_tmp, &tot_uniq);
@@ -497,6 +541,10 @@ __device__ __forceinline__ uint32_t block_size(uint32_t c, uint32_t index_size, 
 
 __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restrict__ plans,
                                                       const uint32_t* __restrict__ idx_cnt,
+                                                      const uint32_t* __restrict__ idx_start,
+                                                      const uint32_t* __restrict__ sorted32,
+                                                      const uint32_t* __restrict__ first_old,
+                                                      const uint32_t* __restrict__ has_old,
                                                       uint64_t* __restrict__ slots,
                                                       uint32_t* __restrict__ page_first,
                                                       FilterOut* __restrict__ outs,
@@ -597,6 +645,51 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
       slots[P.idx_base + j] = (uint64_t)pg[k] * page_size + (s_excl[j] - s_excl[ps]);
       if (mk[k] && pg[k] < P.page_cap) pf[pg[k]] = j;
     }
+  }
+  // num_unique quirk of the old/new merge (src/routing_filter.c:572-590): when index j runs
+  // out of entries while its old index still holds entries of a later new index, the first
+  // of those is counted before the bucket check puts it back, and counted again later.
+  if (P.npo > 1) {
+    __syncthreads();
+    uint32_t* s_next = s_excl;  // reuse: next index with an old entry (suffix min)
+    uint32_t loc[PER], m = 0xffffffffu;
+#pragma unroll
+    for (int k = PER - 1; k >= 0; k--) {
+      const uint32_t j = threadIdx.x * PER + k;
+      loc[k] = m;  // exclusive suffix min within this thread's chunk
+      if (j < n && has_old[P.idx_base + j]) m = j;
+    }
+    // exclusive suffix-min across threads: thread t needs min over threads > t
+    uint32_t x = m;
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const uint32_t y = __shfl_down(x, d, WAVE);
+      if (lane + d < WAVE) x = min(x, y);
+    }
+    if (lane == 0) s_tmp[wv] = x;  // wave-inclusive suffix min at lane 0
+    __syncthreads();
+    uint32_t after_wave = 0xffffffffu;
+    for (int w2 = wv + 1; w2 < LAYOUT_NT / WAVE; w2++) after_wave = min(after_wave, s_tmp[w2]);
+    uint32_t xn = __shfl_down(x, 1, WAVE);
+    if (lane == WAVE - 1) xn = 0xffffffffu;
+    const uint32_t beyond = min(xn, after_wave);  // min over threads > t
+    uint32_t extra = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t j = threadIdx.x * PER + k;
+      const uint32_t nx = min(loc[k], beyond);
+      if (j < n && (j + 1) % P.npo != 0 && nx < (j / P.npo + 1) * P.npo) {
+        const uint32_t c = idx_cnt[P.idx_base + j];
+        const uint32_t last = c ? sorted32[P.e_first + idx_start[P.idx_base + j] + c - 1] : 0xffffffffu;
+        const uint32_t peek = first_old[P.idx_base + nx];
+        if ((peek >> P.vs) != (last >> P.vs)) extra++;
+      }
+    }
+    (void)s_next;
+    uint32_t tot_extra;
+    block_excl_scan<LAYOUT_NT>(extra, s_tmp, &tot_extra);
+    if (threadIdx.x == 0 && tot_extra) atomicAdd(&outs[f].num_unique, tot_extra);
   }
   if (threadIdx.x == 0) {
     if (npages <= P.page_cap) pf[npages] = n;
@@ -902,12 +995,12 @@ static int launch_rest_t(const LaunchArgs& a, EntT* ent, EntT* part) {
   REC(EV_B_SCATTER);
   hipLaunchKernelGGL((k_cb_sort<EntT>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
                      a.cb_count, a.cb_start, part, a.sorted32, a.idx_cnt, a.idx_start, a.outs, a.overflow,
-                     a.lis);
+                     a.lis, a.first_old, a.has_old);
   CHECK_LAUNCH();
   REC(EV_B_SORT);
   hipLaunchKernelGGL((k_cb_sort_big<EntT>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
                      a.cb_count, a.cb_start, part, ent, a.sorted32, a.idx_cnt, a.idx_start, a.outs,
-                     a.overflow, a.lis);
+                     a.overflow, a.lis, a.first_old, a.has_old);
   CHECK_LAUNCH();
   REC(EV_B_SORT_BIG);
   return 0;
@@ -936,7 +1029,7 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
                   : launch_rest_t<uint32_t>(a, (uint32_t*)a.ent, (uint32_t*)a.part);
   if (rc) return rc;
   hipLaunchKernelGGL(k_layout, dim3(a.num_filters), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, a.plans, a.idx_cnt,
-                     a.slots, a.page_first, a.outs, a.lis, a.page_size);
+                     a.idx_start, a.sorted32, a.first_old, a.has_old, a.slots, a.page_first, a.outs, a.lis, a.page_size);
   CHECK_LAUNCH();
   REC(EV_B_LAYOUT);
   hipLaunchKernelGGL(k_assemble, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans, a.pg_filter,

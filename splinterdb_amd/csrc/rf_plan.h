@@ -11,6 +11,7 @@ constexpr uint32_t MAX_LIS = 12;
 constexpr uint32_t CB_LOG_MEAN = 12;  // coarse bucket ~ 2^12..2^13 entries
 constexpr uint32_t MAX_CB = 2048;     // coarse buckets per filter (lnb <= 23)
 constexpr uint32_t MAX_BINS = 4096;   // filter buckets per coarse bucket
+constexpr uint32_t MAX_IPC = 512;     // indices per coarse bucket (2^(12-3))
 
 // kernel shapes
 constexpr int TILE_NT = 256;
@@ -39,7 +40,7 @@ struct FilterPlan {
   uint32_t cbits, bbits;  // coarse-bucket bits, bucket-in-coarse-bucket bits (sum = lnb)
   uint32_t cb_base, idx_base, page_base, page_cap, pf_base;
   // old filter (incremental add)
-  uint32_t old_num_indices, old_vs, old_rvs, pad0;
+  uint32_t old_num_indices, old_vs, old_rvs, npo;  // npo = new indices per old index
   const uint8_t* old_pages;
   const uint64_t* old_slots;
 };
@@ -77,6 +78,8 @@ struct LaunchArgs {
   uint32_t* overflow;
   uint32_t* idx_cnt;
   uint32_t* idx_start;
+  uint32_t* first_old;  // wide mode: per index, smallest old entry (valid if has_old)
+  uint32_t* has_old;
   uint64_t* slots;
   uint32_t* page_first;
   const uint32_t* pg_filter;
