@@ -73,7 +73,7 @@ struct rf_amd_batch {
   uint32_t CB = 0, I = 0, PS = 0, PF = 0;
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
-      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old;
+      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans;
   std::vector<uint32_t> old_num_indices;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing (rf_amd_batch_set_timing)
@@ -225,6 +225,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   const size_t esz = b->wide ? 8 : 4;
   int rc = 0;
   rc |= b->d_plans.alloc(sizeof(FilterPlan) * num_filters);
+  rc |= b->d_pplans.alloc(16ull * num_filters);
   rc |= b->d_outs.alloc(sizeof(FilterOut) * num_filters);
   rc |= b->d_ent.alloc(esz * b->E + 64);
   rc |= b->d_part.alloc(esz * b->E + 64);
@@ -258,6 +259,12 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
 #define UP(buf, vec) \
   if (!(vec).empty()) HIPCHK(hipMemcpyAsync(buf.p, (vec).data(), sizeof((vec)[0]) * (vec).size(), hipMemcpyHostToDevice, st))
   UP(b->d_plans, b->plans);
+  std::vector<uint4> pp(num_filters);
+  for (uint32_t f = 0; f < num_filters; f++) {
+    const FilterPlan& q = b->plans[f];
+    pp[f] = make_uint4(q.vs | (q.rem << 8) | (q.rvs << 16), q.page_base, q.idx_base, 0);
+  }
+  UP(b->d_pplans, pp);
   UP(b->d_tile_filter, b->tile_filter);
   UP(b->d_tile_start, b->tile_start);
   UP(b->d_old_tile_filter, b->old_tile_filter);
@@ -286,6 +293,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.stream = st;
   a.wide = b->wide;
   a.plans = b->d_plans.as<FilterPlan>();
+  a.pplans = b->d_pplans.as<uint4>();
   a.num_filters = b->F;
   a.tile_filter = b->d_tile_filter.as<uint32_t>();
   a.tile_start = b->d_tile_start.as<uint32_t>();
@@ -519,6 +527,7 @@ static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf
   b->PS = img->info.num_pages;
   b->I = p.num_indices;
   int rc = b->d_plans.alloc(sizeof(FilterPlan));
+  rc |= b->d_pplans.alloc(16);
   rc |= b->d_pages.alloc((size_t)img->info.num_pages * cfg->page_size + 256);
   rc |= b->d_slots.alloc(8ull * p.num_indices);
   if (rc) {
@@ -531,6 +540,8 @@ static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf
                         hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(b->d_slots.p, img->slots, 8ull * p.num_indices, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(b->d_plans.p, &p, sizeof(p), hipMemcpyHostToDevice, st));
+  const uint4 pp1 = make_uint4(p.vs | (p.rem << 8) | (p.rvs << 16), 0, 0, 0);
+  HIPCHK(hipMemcpyAsync(b->d_pplans.p, &pp1, sizeof(pp1), hipMemcpyHostToDevice, st));
   HIPCHK(hipStreamSynchronize(st));
   b->built = true;
   *out = b;

@@ -872,49 +872,110 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
 // ======================================================================================
 // Probe: routing_filter_lookup (src/routing_filter.c:985-1073), one lane per probe
 // ======================================================================================
-__device__ __forceinline__ uint64_t probe_one(const FilterPlan& P, const uint8_t* pages,
-                                              const uint64_t* slots, uint32_t h, uint32_t fp_size,
-                                              uint32_t lis, uint32_t page_size) {
+// select: position of the r-th (0-based) set bit of x, by popcount bisection
+__device__ __forceinline__ uint32_t select64_fast(uint64_t x, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = __popcll(x & ((1ull << w) - 1));
+    if (r >= c) { r -= c; x >>= w; pos += w; }
+  }
+  return pos;
+}
+__device__ __forceinline__ uint32_t select128(uint64_t lo, uint64_t hi, uint32_t r) {
+  const uint32_t c = __popcll(lo);
+  return r < c ? select64_fast(lo, r) : 64 + select64_fast(hi, r - c);
+}
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+// one 16-byte aligned window of the page bytes as two little-endian u64
+__device__ __forceinline__ void ld_win(const uint8_t* pg, uint64_t a16, uint64_t& lo, uint64_t& hi) {
+  const v4u v = *reinterpret_cast<const v4u*>(pg + a16);
+  lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+}
+__device__ __forceinline__ uint64_t pick4(uint32_t j, uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+  return j == 0 ? a : (j == 1 ? b : (j == 2 ? c : d));
+}
+
+// routing_filter_lookup on a built image, given the key's 32-bit hash. `pp` = packed probe
+// plan {vs | rem << 8 | rvs << 16, page_base, idx_base, -}.
+__device__ __forceinline__ uint64_t probe_one(const uint4 pp, const uint8_t* pages, const uint64_t* slots,
+                                              uint32_t h, uint32_t fp_size, uint32_t lis,
+                                              uint32_t page_size) {
+  const uint32_t vs = pp.x & 0xff, rem = (pp.x >> 8) & 0xff, rvs = (pp.x >> 16) & 0xff;
   const uint32_t index_size = 1u << lis;
   const uint32_t fp = h >> (32 - fp_size);
-  const uint32_t x = fp << P.vs;
-  const uint32_t bucket = P.rvs >= 32 ? 0u : x >> P.rvs;
-  const uint32_t bo = bucket & (index_size - 1);
-  const uint32_t irvs = P.rvs + lis;
+  const uint32_t x = fp << vs;
+  const uint32_t bo = (rvs >= 32 ? 0u : x >> rvs) & (index_size - 1);
+  const uint32_t irvs = rvs + lis;
   const uint32_t index = irvs >= 32 ? 0u : x >> irvs;
-  const uint32_t remmask = P.rem >= 32 ? 0xffffffffu : ((1u << P.rem) - 1);
-  const uint32_t remainder = fp & remmask;
-  const uint8_t* pg = pages + (uint64_t)P.page_base * page_size;
-  const uint64_t hdr = slots[P.idx_base + index];
-  const uint32_t c = (uint32_t)pg[hdr] | ((uint32_t)pg[hdr + 1] << 8);
+  const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+  const uint8_t* pg = pages + (uint64_t)pp.y * page_size;
+  const uint64_t hdr = slots[pp.z + index];
+  // window 0 holds the 2-byte header (unless it straddles) and the first encoding bits
+  const uint64_t a0 = hdr & ~15ull;
+  uint64_t lo, hi;
+  ld_win(pg, a0, lo, hi);
+  const uint32_t hs = (uint32_t)(hdr - a0) * 8;  // header bit offset in window 0
+  uint32_t c;
+  if (hs <= 112) {
+    c = (uint32_t)((hs < 64 ? (lo >> hs) | (hs ? hi << (64 - hs) : 0) : hi >> (hs - 64)) & 0xffff);
+  } else {  // header bytes at window offsets 15 and 16
+    c = (uint32_t)(hi >> 56) | ((uint32_t)pg[hdr + 1] << 8);
+  }
   const uint32_t enc = (c + index_size - 1) / 8 + 4;
-  const uint64_t ebit = (hdr + 2) * 8;
-  // select: position of 1-bit #(bo-1) and #bo (0-based) in the encoding
+  // select over 128-bit windows; encoding bit 0 is window-0 bit (hs + 16)
+  const uint32_t target_lo = bo ? bo - 1 : 0;
   uint32_t start = 0, end = 0, cum = 0;
   bool have_start = (bo == 0);
-  const uint32_t wmax = (c + index_size) / 56 + 2;  // bound: a corrupt image cannot hang the wave
-  for (uint32_t w = 0;; w++) {
-    if (w > wmax) return 0;
-    const uint64_t bp = ebit + (uint64_t)w * 56;  // 56-bit steps keep the byte shift in range
-    const uint64_t xw = (ld_u64_unaligned(pg, bp >> 3) >> (bp & 7)) & ((1ull << 56) - 1);
-    const uint32_t pc = __popcll(xw);
-    if (!have_start && cum + pc > bo - 1) {
-      start = w * 56 + select64(xw, bo - 1 - cum) + 1 - bo;
+  const uint32_t e0 = hs + 16;          // may be >= 128: then window 0 has no encoding bits
+  const uint32_t nwin = (e0 + c + index_size + 127) / 128 + 1;
+  for (uint32_t k = 0;; k++) {
+    if (k > nwin) return 0;  // corrupt image: never hang
+    if (k) ld_win(pg, a0 + 16ull * k, lo, hi);
+    if (k == 0 || (k == 1 && e0 > 128)) {  // drop the bits before the encoding
+      const uint32_t cut = k == 0 ? min(e0, 128u) : e0 - 128;
+      if (cut >= 64) { lo = 0; hi = cut >= 128 ? 0 : (hi >> (cut - 64)) << (cut - 64); }
+      else if (cut) { lo = (lo >> cut) << cut; }
+    }
+    const uint32_t pc = __popcll(lo) + __popcll(hi);
+    const uint32_t base = 128 * k - e0;  // encoding-relative bit of window bit 0 (mod 2^32)
+    if (!have_start && cum + pc > target_lo) {
+      start = base + select128(lo, hi, target_lo - cum) + 1 - bo;
       have_start = true;
     }
     if (cum + pc > bo) {
-      end = w * 56 + select64(xw, bo - cum) - bo;
+      end = base + select128(lo, hi, bo - cum) - bo;
       break;
     }
     cum += pc;
   }
-  if (start == end) return 0;
-  const uint64_t rbit = (hdr + 2 + enc) * 8;
-  const uint32_t vmask = (uint32_t)((1ull << P.vs) - 1);
+  if (start >= end) return 0;
+  // remainders [start, end): one 32-byte aligned span covers the bucket in practice
+  const uint64_t rbit0 = (hdr + 2 + enc) * 8;
+  const uint64_t bs = rbit0 + (uint64_t)start * rvs;
+  const uint64_t ra = (bs >> 3) & ~15ull;
+  uint64_t w0, w1, w2, w3;
+  ld_win(pg, ra, w0, w1);
+  ld_win(pg, ra + 16, w2, w3);
+  const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
+  const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
   uint64_t found = 0;
   for (uint32_t pos = start; pos < end; pos++) {
-    const uint32_t rv = ld_bits(pg, rbit + (uint64_t)pos * P.rvs, P.rvs);
-    if ((rv >> P.vs) == remainder) {
+    const uint64_t b = rbit0 + (uint64_t)pos * rvs - ra * 8;
+    uint32_t rv;
+    if (b + rvs <= 256) {
+      const uint32_t j = (uint32_t)(b >> 6), sh = (uint32_t)(b & 63);
+      uint64_t v = pick4(j, w0, w1, w2, w3) >> sh;
+      if (sh + rvs > 64) v |= pick4(j + 1, w0, w1, w2, w3) << (64 - sh);
+      rv = (uint32_t)v & rvmask;
+    } else {
+      rv = ld_bits(pg, rbit0 + (uint64_t)pos * rvs, rvs);
+    }
+    if ((rv >> vs) == remainder) {
       const uint32_t v = rv & vmask;
       if (v < 64) found |= 1ull << v;
     }
@@ -922,8 +983,16 @@ __device__ __forceinline__ uint64_t probe_one(const FilterPlan& P, const uint8_t
   return found;
 }
 
+// XCD-aware block -> chunk remap (bijective for any grid): the blocks that share an XCD
+// (b % 8, round-robin dispatch) process one contiguous eighth of the probe array, so an
+// XCD's L2 holds the images of the filters its probes hit (MI355X_MICROARCH.md, XCD L2).
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
+  const uint32_t q = nb / 8, r = nb % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
 template <int KIND>
-__global__ __launch_bounds__(256) void k_probe(const FilterPlan* __restrict__ plans,
+__global__ __launch_bounds__(256) void k_probe(const uint4* __restrict__ pplans,
                                                const uint8_t* __restrict__ pages,
                                                const uint64_t* __restrict__ slots,
                                                const void* __restrict__ in0,
@@ -932,17 +1001,18 @@ __global__ __launch_bounds__(256) void k_probe(const FilterPlan* __restrict__ pl
                                                uint64_t* __restrict__ found, uint32_t fp_size,
                                                uint32_t seed, uint32_t lis, uint32_t page_size,
                                                uint32_t num_filters, const FilterOut* __restrict__ outs) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t fid = filter_id[i];
+  const uint32_t fid = __builtin_nontemporal_load(filter_id + i);
   if (fid >= num_filters || (outs && outs[fid].error)) {  // unknown / failed filter finds nothing
-    found[i] = 0;
+    __builtin_nontemporal_store(0ull, found + i);
     return;
   }
   uint32_t h;
   if constexpr (KIND == IN_KEYS24) {
-    const uint2* kp = reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(in0) + i * 24);
-    uint2 a = kp[0], b = kp[1], c = kp[2];
+    const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) + i * 24);
+    const v2u a = __builtin_nontemporal_load(kp), b = __builtin_nontemporal_load(kp + 1),
+              c = __builtin_nontemporal_load(kp + 2);
     uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
     h = xxh32_24(w, seed);
   } else if constexpr (KIND == IN_KEYS_W) {
@@ -954,10 +1024,10 @@ __global__ __launch_bounds__(256) void k_probe(const FilterPlan* __restrict__ pl
     const uint64_t o0 = offs[i], o1 = offs[i + 1];
     h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
   } else {
-    h = static_cast<const uint32_t*>(in0)[i];
+    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + i);
   }
-  const FilterPlan& P = plans[fid];
-  found[i] = probe_one(P, pages, slots, h, fp_size, lis, page_size);
+  const uint64_t r = probe_one(pplans[fid], pages, slots, h, fp_size, lis, page_size);
+  __builtin_nontemporal_store(r, found + i);
 }
 
 // ======================================================================================
@@ -1062,11 +1132,11 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
   dim3 g((uint32_t)((n + 255) / 256)), b(256);
   REC(EV_P_START);
   switch (kind) {
-    case IN_KEYS24: hipLaunchKernelGGL(k_probe<IN_KEYS24>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    case IN_KEYS_W: hipLaunchKernelGGL(k_probe<IN_KEYS_W>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    case IN_KEYS_B: hipLaunchKernelGGL(k_probe<IN_KEYS_B>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    case IN_VAR:    hipLaunchKernelGGL(k_probe<IN_VAR>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    default:        hipLaunchKernelGGL(k_probe<IN_HASH>, g, b, 0, (hipStream_t)a.stream, a.plans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_KEYS24: hipLaunchKernelGGL(k_probe<IN_KEYS24>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_KEYS_W: hipLaunchKernelGGL(k_probe<IN_KEYS_W>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_KEYS_B: hipLaunchKernelGGL(k_probe<IN_KEYS_B>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_VAR:    hipLaunchKernelGGL(k_probe<IN_VAR>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    default:        hipLaunchKernelGGL(k_probe<IN_HASH>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
   }
   CHECK_LAUNCH();
   REC(EV_P_END);

@@ -1,5 +1,6 @@
 // rf_plan.h -- host/device shared batch plan of the routing-filter engine.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace rf {
@@ -57,6 +58,7 @@ struct LaunchArgs {
   int kind;
   int wide;  // 64-bit entries (old/new flag) -- only for incremental adds
   const FilterPlan* plans;
+  const uint4* pplans;  // packed probe plan per filter {vs|rem<<8|rvs<<16, page_base, idx_base, 0}
   uint32_t num_filters;
   const uint32_t* tile_filter;
   const uint32_t* tile_start;
