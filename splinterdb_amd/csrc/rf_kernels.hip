@@ -151,15 +151,21 @@ __global__ __launch_bounds__(256) void k_cb_scan(const FilterPlan* __restrict__ 
 // K3: scatter entries into coarse buckets
 // ======================================================================================
 template <typename EntT>
-__global__ __launch_bounds__(TILE_NT) void k_scatter(const FilterPlan* __restrict__ plans,
+__global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ tile_filter,
                                                      const uint32_t* __restrict__ tile_start,
                                                      uint32_t region_is_old, uint32_t fp_size,
                                                      const EntT* __restrict__ ent,
                                                      EntT* __restrict__ part,
                                                      uint32_t* __restrict__ cb_cursor) {
-  __shared__ uint32_t s_hist[MAX_CB];
-  constexpr int PER = TILE_KEYS / TILE_NT;
+  // The tile is sorted by coarse bucket in LDS, then each bucket's run is written by
+  // consecutive lanes: whole 64-byte granules instead of scattered 4-byte stores.
+  __shared__ EntT s_stage[TILE_KEYS];
+  __shared__ uint32_t s_off[MAX_CB];
+  __shared__ uint32_t s_base[MAX_CB];
+  __shared__ uint32_t s_tmp[SCAT_NT / WAVE + 1];
+  constexpr int PER = TILE_KEYS / SCAT_NT;
+  constexpr int BPT = MAX_CB / SCAT_NT;
   const uint32_t t = blockIdx.x;
   const FilterPlan& P = plans[tile_filter[t]];
   const uint32_t start = tile_start[t];
@@ -167,40 +173,61 @@ __global__ __launch_bounds__(TILE_NT) void k_scatter(const FilterPlan* __restric
   const uint64_t base = P.e_first + (region_is_old ? P.num_new : 0u) + start;
   const uint32_t count = min((uint32_t)TILE_KEYS, region - start);
   const uint32_t num_cb = 1u << P.cbits;
-  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) s_hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < num_cb; i += SCAT_NT) s_off[i] = 0;
   __syncthreads();
   const uint32_t esh = fp_size + P.vs - P.cbits;
+  auto cb_of = [&](EntT x) -> uint32_t {
+    uint32_t e;
+    if constexpr (sizeof(EntT) == 8) e = (uint32_t)(x >> 1);
+    else e = x;
+    return P.cbits ? (e >> esh) : 0u;
+  };
   EntT v[PER];
   uint32_t cbv[PER], rank[PER];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x + k * TILE_NT;
+    const uint32_t j = threadIdx.x + k * SCAT_NT;
     cbv[k] = ~0u;
     if (j < count) {
       v[k] = ent[base + j];
-      uint32_t e;
       bool valid = true;
-      if constexpr (sizeof(EntT) == 8) {
-        valid = v[k] != ~0ull;
-        e = (uint32_t)(v[k] >> 1);
-      } else {
-        e = v[k];
-      }
+      if constexpr (sizeof(EntT) == 8) valid = v[k] != ~0ull;
       if (valid) {
-        cbv[k] = P.cbits ? (e >> esh) : 0u;
-        rank[k] = atomicAdd(&s_hist[cbv[k]], 1u);
+        cbv[k] = cb_of(v[k]);
+        rank[k] = atomicAdd(&s_off[cbv[k]], 1u);
       }
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) {
-    const uint32_t c = s_hist[i];
-    if (c) s_hist[i] = atomicAdd(&cb_cursor[P.cb_base + i], c);
+  // local exclusive offsets + one global reservation per non-empty bucket
+  uint32_t cnt[BPT], sum = 0;
+#pragma unroll
+  for (int k = 0; k < BPT; k++) {
+    const uint32_t b = threadIdx.x * BPT + k;
+    cnt[k] = b < num_cb ? s_off[b] : 0u;
+    sum += cnt[k];
+  }
+  uint32_t valid_total;
+  uint32_t run = block_excl_scan<SCAT_NT>(sum, s_tmp, &valid_total);
+#pragma unroll
+  for (int k = 0; k < BPT; k++) {
+    const uint32_t b = threadIdx.x * BPT + k;
+    if (b < num_cb) {
+      s_off[b] = run;
+      if (cnt[k]) s_base[b] = atomicAdd(&cb_cursor[P.cb_base + b], cnt[k]) - run;
+      run += cnt[k];
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    if (cbv[k] != ~0u) part[P.e_first + s_hist[cbv[k]] + rank[k]] = v[k];
+    if (cbv[k] != ~0u) s_stage[s_off[cbv[k]] + rank[k]] = v[k];
+  }
+  __syncthreads();
+  EntT* dst = part + P.e_first;
+  for (uint32_t j = threadIdx.x; j < valid_total; j += SCAT_NT) {
+    const EntT x = s_stage[j];
+    dst[s_base[cb_of(x)] + j] = x;
   }
 }
 
@@ -900,67 +927,117 @@ __device__ __forceinline__ uint64_t pick4(uint32_t j, uint64_t a, uint64_t b, ui
   return j == 0 ? a : (j == 1 ? b : (j == 2 ? c : d));
 }
 
-// routing_filter_lookup on a built image, given the key's 32-bit hash. `pp` = packed probe
-// plan {vs | rem << 8 | rvs << 16, page_base, idx_base, -}.
-__device__ __forceinline__ uint64_t probe_one(const uint4 pp, const uint8_t* pages, const uint64_t* slots,
-                                              uint32_t h, uint32_t fp_size, uint32_t lis,
-                                              uint32_t page_size) {
-  const uint32_t vs = pp.x & 0xff, rem = (pp.x >> 8) & 0xff, rvs = (pp.x >> 16) & 0xff;
+// Probe = routing_filter_lookup on a built image, given the key's 32-bit hash, in three
+// steps: (A) per lane: fingerprint -> index / bucket / remainder, index slot -> header
+// address; (B) per wave, cooperatively: the 128 bytes from each probe's header window are
+// staged in LDS, 8 lanes per probe (8 probes per 16-byte-per-lane load instruction, so a
+// wave touches ~100 cache lines instead of 512 for per-lane loads); (C) per lane: unary
+// select over the staged bits, then the bucket's packed remainders.
+struct ProbeLane {
+  uint32_t bo, remainder, vs, rvs;
+  const uint8_t* pg;  // the filter's page base
+  uint64_t hdr;       // header byte offset in pg
+};
+
+__device__ __forceinline__ ProbeLane probe_locate(const uint4 pp, const uint8_t* pages, const uint64_t* slots,
+                                                  uint32_t h, uint32_t fp_size, uint32_t lis,
+                                                  uint32_t page_size) {
+  ProbeLane L;
+  L.vs = pp.x & 0xff;
+  const uint32_t rem = (pp.x >> 8) & 0xff;
+  L.rvs = (pp.x >> 16) & 0xff;
   const uint32_t index_size = 1u << lis;
   const uint32_t fp = h >> (32 - fp_size);
-  const uint32_t x = fp << vs;
-  const uint32_t bo = (rvs >= 32 ? 0u : x >> rvs) & (index_size - 1);
-  const uint32_t irvs = rvs + lis;
+  const uint32_t x = fp << L.vs;
+  L.bo = (L.rvs >= 32 ? 0u : x >> L.rvs) & (index_size - 1);
+  const uint32_t irvs = L.rvs + lis;
   const uint32_t index = irvs >= 32 ? 0u : x >> irvs;
-  const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-  const uint8_t* pg = pages + (uint64_t)pp.y * page_size;
-  const uint64_t hdr = slots[pp.z + index];
-  // window 0 holds the 2-byte header (unless it straddles) and the first encoding bits
+  L.remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+  L.pg = pages + (uint64_t)pp.y * page_size;
+  L.hdr = slots[pp.z + index];
+  return L;
+}
+
+// W = the 128 bytes at (hdr & ~15) as 16 little-endian u64
+__device__ __forceinline__ uint64_t probe_finish(const ProbeLane& L, const uint64_t (&W)[16], uint32_t lis) {
+  const uint32_t index_size = 1u << lis;
+  const uint32_t bo = L.bo, vs = L.vs, rvs = L.rvs;
+  const uint8_t* pg = L.pg;
+  const uint64_t hdr = L.hdr;
   const uint64_t a0 = hdr & ~15ull;
-  uint64_t lo, hi;
-  ld_win(pg, a0, lo, hi);
-  const uint32_t hs = (uint32_t)(hdr - a0) * 8;  // header bit offset in window 0
+  const uint32_t hs = (uint32_t)(hdr - a0) * 8;  // header bit offset in the 1024-bit span
   uint32_t c;
-  if (hs <= 112) {
-    c = (uint32_t)((hs < 64 ? (lo >> hs) | (hs ? hi << (64 - hs) : 0) : hi >> (hs - 64)) & 0xffff);
-  } else {  // header bytes at window offsets 15 and 16
-    c = (uint32_t)(hi >> 56) | ((uint32_t)pg[hdr + 1] << 8);
+  {
+    const uint32_t j = hs >> 6, sh = hs & 63;  // hs <= 120: words 0..1 (+2 when straddling)
+    uint64_t v = (j == 0 ? W[0] : W[1]) >> sh;
+    if (sh > 48) v |= (j == 0 ? W[1] : W[2]) << (64 - sh);
+    c = (uint32_t)(v & 0xffff);
   }
   const uint32_t enc = (c + index_size - 1) / 8 + 4;
-  // select over 128-bit windows; encoding bit 0 is window-0 bit (hs + 16)
+  const uint32_t e0 = hs + 16;  // encoding bit 0 in span coordinates
   const uint32_t target_lo = bo ? bo - 1 : 0;
   uint32_t start = 0, end = 0, cum = 0;
-  bool have_start = (bo == 0);
-  const uint32_t e0 = hs + 16;          // may be >= 128: then window 0 has no encoding bits
-  const uint32_t nwin = (e0 + c + index_size + 127) / 128 + 1;
-  for (uint32_t k = 0;; k++) {
-    if (k > nwin) return 0;  // corrupt image: never hang
-    if (k) ld_win(pg, a0 + 16ull * k, lo, hi);
-    if (k == 0 || (k == 1 && e0 > 128)) {  // drop the bits before the encoding
-      const uint32_t cut = k == 0 ? min(e0, 128u) : e0 - 128;
-      if (cut >= 64) { lo = 0; hi = cut >= 128 ? 0 : (hi >> (cut - 64)) << (cut - 64); }
-      else if (cut) { lo = (lo >> cut) << cut; }
+  bool have_start = (bo == 0), done = false;
+  if (e0 + c + index_size <= 1024) {
+    // select over the registers (compile-time indices only)
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      uint64_t x = W[k];
+      const uint32_t wb = 64u * k;
+      if (wb + 64 <= e0) x = 0;
+      else if (wb < e0) x = (x >> (e0 - wb)) << (e0 - wb);
+      const uint32_t pc = __popcll(x);
+      if (!done) {
+        const uint32_t base = wb - e0;
+        if (!have_start && cum + pc > target_lo) {
+          start = base + select64_fast(x, target_lo - cum) + 1 - bo;
+          have_start = true;
+        }
+        if (cum + pc > bo) {
+          end = base + select64_fast(x, bo - cum) - bo;
+          done = true;
+        }
+        cum += pc;
+      }
     }
-    const uint32_t pc = __popcll(lo) + __popcll(hi);
-    const uint32_t base = 128 * k - e0;  // encoding-relative bit of window bit 0 (mod 2^32)
-    if (!have_start && cum + pc > target_lo) {
-      start = base + select128(lo, hi, target_lo - cum) + 1 - bo;
-      have_start = true;
+    if (!done) return 0;  // corrupt image
+  } else {
+    // long encodings (> ~860 entries in the index): stream 128-bit windows
+    const uint32_t nwin = (e0 + c + index_size + 127) / 128 + 1;
+    for (uint32_t k = 0;; k++) {
+      if (k > nwin) return 0;
+      uint64_t lo, hi;
+      ld_win(pg, a0 + 16ull * k, lo, hi);
+      const uint32_t wb = 128u * k;
+      if (wb + 128 <= e0) { lo = 0; hi = 0; }
+      else if (wb < e0) {
+        const uint32_t cut = e0 - wb;
+        if (cut >= 64) { lo = 0; hi = (hi >> (cut - 64)) << (cut - 64); }
+        else { lo = (lo >> cut) << cut; }
+      }
+      const uint32_t pc = __popcll(lo) + __popcll(hi);
+      const uint32_t base = wb - e0;
+      if (!have_start && cum + pc > target_lo) {
+        start = base + select128(lo, hi, target_lo - cum) + 1 - bo;
+        have_start = true;
+      }
+      if (cum + pc > bo) {
+        end = base + select128(lo, hi, bo - cum) - bo;
+        break;
+      }
+      cum += pc;
     }
-    if (cum + pc > bo) {
-      end = base + select128(lo, hi, bo - cum) - bo;
-      break;
-    }
-    cum += pc;
   }
   if (start >= end) return 0;
-  // remainders [start, end): one 32-byte aligned span covers the bucket in practice
+  // remainders [start, end): the 16-byte window holding the first one, plus the next
+  // window only for lanes whose run crosses it
   const uint64_t rbit0 = (hdr + 2 + enc) * 8;
   const uint64_t bs = rbit0 + (uint64_t)start * rvs;
   const uint64_t ra = (bs >> 3) & ~15ull;
-  uint64_t w0, w1, w2, w3;
+  uint64_t w0, w1, w2 = 0, w3 = 0;
   ld_win(pg, ra, w0, w1);
-  ld_win(pg, ra + 16, w2, w3);
+  const uint64_t last_bit = rbit0 + (uint64_t)end * rvs - ra * 8;  // exclusive, span-relative
+  if (last_bit > 128) ld_win(pg, ra + 16, w2, w3);
   const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
   const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
   uint64_t found = 0;
@@ -975,7 +1052,7 @@ __device__ __forceinline__ uint64_t probe_one(const uint4 pp, const uint8_t* pag
     } else {
       rv = ld_bits(pg, rbit0 + (uint64_t)pos * rvs, rvs);
     }
-    if ((rv >> vs) == remainder) {
+    if ((rv >> vs) == L.remainder) {
       const uint32_t v = rv & vmask;
       if (v < 64) found |= 1ull << v;
     }
@@ -991,42 +1068,81 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
-template <int KIND>
-__global__ __launch_bounds__(256) void k_probe(const uint4* __restrict__ pplans,
-                                               const uint8_t* __restrict__ pages,
-                                               const uint64_t* __restrict__ slots,
-                                               const void* __restrict__ in0,
-                                               const uint64_t* __restrict__ offs, uint32_t key_len,
-                                               const uint32_t* __restrict__ filter_id, uint64_t n,
-                                               uint64_t* __restrict__ found, uint32_t fp_size,
-                                               uint32_t seed, uint32_t lis, uint32_t page_size,
-                                               uint32_t num_filters, const FilterOut* __restrict__ outs) {
+constexpr int PROBE_NT = 256;
+
+// STAGE: stage block heads through LDS cooperatively (step B) instead of per-lane loads.
+// Measured on MI355X (C2, 64M probes): per-lane 2.34 ms, staged 3.09 ms -- the kernel is
+// bound by random L2 line fetches (~3.5 per probe), not by load-instruction issue, so the
+// per-lane form (full occupancy, no barrier) is the default.
+template <int KIND, bool STAGE = false>
+__global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
+                                                    const uint8_t* __restrict__ pages,
+                                                    const uint64_t* __restrict__ slots,
+                                                    const void* __restrict__ in0,
+                                                    const uint64_t* __restrict__ offs, uint32_t key_len,
+                                                    const uint32_t* __restrict__ filter_id, uint64_t n,
+                                                    uint64_t* __restrict__ found, uint32_t fp_size,
+                                                    uint32_t seed, uint32_t lis, uint32_t page_size,
+                                                    uint32_t num_filters, const FilterOut* __restrict__ outs) {
+  __shared__ __attribute__((aligned(16))) v4u s_blk[STAGE ? PROBE_NT * 8 : 1];  // 128 B per probe
   const uint64_t i = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  v4u* wbuf = s_blk + (threadIdx.x - lane) * 8;  // this wave's 64 x 128 B
+  bool live = i < n;
+  uint32_t fid = 0;
+  if (live) {
+    fid = __builtin_nontemporal_load(filter_id + i);
+    live = fid < num_filters && !(outs && outs[fid].error);  // unknown / failed filter: 0
+  }
+  ProbeLane L{};
+  if (live) {
+    uint32_t h;
+    if constexpr (KIND == IN_KEYS24) {
+      const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) + i * 24);
+      const v2u a = __builtin_nontemporal_load(kp), b = __builtin_nontemporal_load(kp + 1),
+                c = __builtin_nontemporal_load(kp + 2);
+      uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+      h = xxh32_24(w, seed);
+    } else if constexpr (KIND == IN_KEYS_W) {
+      h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + i * key_len),
+                      key_len, seed);
+    } else if constexpr (KIND == IN_KEYS_B) {
+      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + i * key_len, key_len, seed);
+    } else if constexpr (KIND == IN_VAR) {
+      const uint64_t o0 = offs[i], o1 = offs[i + 1];
+      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
+    } else {
+      h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + i);
+    }
+    L = probe_locate(pplans[fid], pages, slots, h, fp_size, lis, page_size);
+  }
+  // (B) cooperative staging: instruction k moves probes 8k..8k+7, lane -> (probe, 16-B part)
+  if constexpr (STAGE) {
+    // byte offset (from `pages`) of the probe's 16-byte header window; ~0 = no probe
+    const uint64_t my_off = live ? (uint64_t)(L.pg - pages) + (L.hdr & ~15ull) : ~0ull;
+    const uint32_t lo32 = (uint32_t)my_off, hi32 = (uint32_t)(my_off >> 32);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int p = 8 * k + (int)(lane >> 3);
+      const uint64_t off = (uint64_t)__shfl(lo32, p, WAVE) | ((uint64_t)__shfl(hi32, p, WAVE) << 32);
+      if (off != ~0ull) wbuf[p * 8 + (lane & 7)] = *reinterpret_cast<const v4u*>(pages + off + 16 * (lane & 7));
+    }
+    __syncthreads();
+  }
   if (i >= n) return;
-  const uint32_t fid = __builtin_nontemporal_load(filter_id + i);
-  if (fid >= num_filters || (outs && outs[fid].error)) {  // unknown / failed filter finds nothing
-    __builtin_nontemporal_store(0ull, found + i);
+  if (!live) {
+    __builtin_nontemporal_store((uint64_t)0, found + i);
     return;
   }
-  uint32_t h;
-  if constexpr (KIND == IN_KEYS24) {
-    const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) + i * 24);
-    const v2u a = __builtin_nontemporal_load(kp), b = __builtin_nontemporal_load(kp + 1),
-              c = __builtin_nontemporal_load(kp + 2);
-    uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-    h = xxh32_24(w, seed);
-  } else if constexpr (KIND == IN_KEYS_W) {
-    h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + i * key_len),
-                    key_len, seed);
-  } else if constexpr (KIND == IN_KEYS_B) {
-    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + i * key_len, key_len, seed);
-  } else if constexpr (KIND == IN_VAR) {
-    const uint64_t o0 = offs[i], o1 = offs[i + 1];
-    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
-  } else {
-    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + i);
+  uint64_t W[16];
+  const v4u* src = STAGE ? wbuf + lane * 8 : reinterpret_cast<const v4u*>(L.pg + (L.hdr & ~15ull));
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const v4u v = src[k];
+    W[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    W[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
   }
-  const uint64_t r = probe_one(pplans[fid], pages, slots, h, fp_size, lis, page_size);
+  const uint64_t r = probe_finish(L, W, lis);
   __builtin_nontemporal_store(r, found + i);
 }
 
@@ -1053,12 +1169,12 @@ static int launch_hash_count_t(int kind, const LaunchArgs& a, EntT* ent) {
 template <typename EntT>
 static int launch_rest_t(const LaunchArgs& a, EntT* ent, EntT* part) {
   if (a.num_tiles) {
-    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_tiles), dim3(TILE_NT), 0, (hipStream_t)a.stream, a.plans,
+    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
                        a.tile_filter, a.tile_start, 0u, a.fp_size, ent, part, a.cb_cursor);
     CHECK_LAUNCH();
   }
   if (a.num_old_tiles) {
-    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_old_tiles), dim3(TILE_NT), 0, (hipStream_t)a.stream, a.plans,
+    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_old_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
                        a.old_tile_filter, a.old_tile_start, 1u, a.fp_size, ent, part, a.cb_cursor);
     CHECK_LAUNCH();
   }
@@ -1129,7 +1245,7 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found) {
   const LaunchArgs& a = *pa;
   if (n == 0) return 0;
-  dim3 g((uint32_t)((n + 255) / 256)), b(256);
+  dim3 g((uint32_t)((n + PROBE_NT - 1) / PROBE_NT)), b(PROBE_NT);
   REC(EV_P_START);
   switch (kind) {
     case IN_KEYS24: hipLaunchKernelGGL(k_probe<IN_KEYS24>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;

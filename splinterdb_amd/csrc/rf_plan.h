@@ -16,7 +16,8 @@ constexpr uint32_t MAX_IPC = 512;     // indices per coarse bucket (2^(12-3))
 
 // kernel shapes
 constexpr int TILE_NT = 256;
-constexpr int TILE_KEYS = 4096;  // keys per K1/K3 tile
+constexpr int TILE_KEYS = 16384;  // keys per K1/K3 tile
+constexpr int SCAT_NT = 512;
 constexpr int SORT_NT = 512;
 constexpr int SORT_CAP = 12288;  // entries per coarse bucket held in LDS
 constexpr int BIG_NT = 1024;
