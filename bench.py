@@ -32,6 +32,14 @@ sys.path.insert(0, ROOT)
 
 from splinterdb_amd import engine as E  # noqa: E402
 from splinterdb_amd import keys as K  # noqa: E402
+from splinterdb_amd import shard as S  # noqa: E402
+
+WORKLOADS = {
+    # name: (filters, keys per filter, scaling, description)
+    "c2": (8, 8_000_000, "weak", "C2: 64M x 24B keys per GPU = 8 filters x 8,000,000, build + full probe"),
+    "c3": (256, 1 << 20, "weak", "C3: 256M x 24B keys per GPU = 256 filters x 2^20, build + full probe"),
+    "c4": (1024, 1 << 20, "strong", "C4: 2^30 x 24B keys = 1024 filters x 2^20 split by key range, build + full probe"),
+}
 
 METRIC = "routing_filter build Mkeys/s + probe Mkeys/s, device-resident, 24B keys"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -42,8 +50,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--filters", type=int, default=8)
-    p.add_argument("--keys-per-filter", type=int, default=8_000_000)
+    p.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2",
+                   help="c2: 8 x 8,000,000 keys per GPU (weak); c3: 256 x 2^20 per GPU (weak); "
+                        "c4: 1024 x 2^20 keys in total, split over the GPUs (strong)")
+    p.add_argument("--filters", type=int, default=0, help="override filters (per GPU for c2/c3)")
+    p.add_argument("--keys-per-filter", type=int, default=0)
     p.add_argument("--log-index-size", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -64,11 +75,10 @@ def stage_bytes(stage, N, P, image_bytes, slot_bytes, unique):
     }.get(stage)
 
 
-def cpu_baseline(args, cfg_lis):
+def cpu_baseline(args, cfg_lis, n):
     from oracle import oracle as O
     threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
     nf = args.cpu_filters or threads
-    n = args.keys_per_filter
     keys = K.seq_keys(0, nf * n).reshape(-1)
     ocfg = O.make_config(log_index_size=cfg_lis)
     import ctypes
@@ -111,14 +121,21 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    F, n = args.filters, args.keys_per_filter
-    N = F * n
+    wf, wn, scaling, wdesc = WORKLOADS[args.workload]
+    n = args.keys_per_filter or wn
+    if scaling == "weak":
+        F_total = (args.filters or wf) * world
+    else:
+        F_total = args.filters or wf
+    me = S.plan_shards(F_total, n, world)[rank]
+    F = me.num_filters
+    N = me.num_keys
     cfg = E.routing_config_init(fingerprint_size=26, log_index_size=args.log_index_size, seed=42)
     eng = E.Engine(local)
     stream = torch.cuda.Stream(device=dev)
     with torch.cuda.stream(stream):
-        # key-range shard of this rank: ids [rank*N, (rank+1)*N)
-        keys = K.seq_keys_torch(rank * N, N, 24, dev)
+        # key-range shard of this rank: ids [key_begin, key_end), filter f = ids of its range
+        keys = K.seq_keys_torch(me.key_begin, N, 24, dev)
         fid = (torch.arange(N, device=dev, dtype=torch.int64) // n).to(torch.int32)
         found = torch.empty(N, dtype=torch.int64, device=dev)
     stream.synchronize()
@@ -152,10 +169,8 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = S.max_over_ranks(elapsed, dist, dev)
+    keys_all = S.sum_over_ranks(float(N), dist, dev)
 
     # ---- verification (outside the timed region) -------------------------------------
     ok = bool(((found & 1) == 1).all().item())
@@ -164,7 +179,7 @@ def main():
     slot_bytes = sum(i.num_indices for i in infos) * 8
     unique = sum(i.num_unique for i in infos)
     verified = ok and all(i.error == 0 for i in infos)
-    if rank == 0 and n == 8_000_000 and args.log_index_size == 8:
+    if rank == 0 and me.key_begin == 0 and n == 8_000_000 and args.log_index_size == 8:
         with open(os.path.join(ROOT, "tests", "golden", "sha256.json")) as fh:
             want = json.load(fh)["seq_n8000000_lis8"]["pages_sha256"]
         img = batch.image(0)
@@ -175,7 +190,7 @@ def main():
     # index slots D2H into pinned host buffers (the clockcache page buffers' stand-in).
     e2e = None
     if not args.no_e2e:
-        hk = torch.from_numpy(K.seq_keys(rank * N, N).reshape(-1)).pin_memory()
+        hk = torch.from_numpy(K.seq_keys(me.key_begin, N).reshape(-1)).pin_memory()
         hfound = torch.empty(N, dtype=torch.int64).pin_memory()
         hpages = [torch.empty(i.num_pages * cfg.page_size, dtype=torch.uint8).pin_memory() for i in infos]
         hslots = [torch.empty(i.num_indices, dtype=torch.int64).pin_memory() for i in infos]
@@ -191,7 +206,7 @@ def main():
             for f in range(F):
                 batch.read_image_async(f, hpages[f], hslots[f], stream.cuda_stream)
         stream.synchronize()
-        e2e = N * reps / (time.perf_counter() - te) / 1e6
+        e2e = S.sum_over_ranks(N * reps / (time.perf_counter() - te) / 1e6, dist, dev)
         ok_e2e = bool(((hfound & 1) == 1).all().item())
         verified = verified and ok_e2e
 
@@ -215,7 +230,7 @@ def main():
             traffic = None
     build_ms, probe_ms = ms["build_total"], ms["probe"]
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * N / (elapsed / args.steps) / 1e6
+    value = keys_all / (elapsed / args.steps) / 1e6
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -225,16 +240,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic: sequential-id 24 B keys (filter_test format), generated in HBM",
-        "config": {"workload": "C2: 64M x 24B keys per GPU = 8 filters x 8,000,000, build + full probe",
+        "config": {"workload": wdesc, "filters_total": F_total,
                    "filters_per_gpu": F, "keys_per_filter": n, "key_len": 24,
                    "fingerprint_size": 26, "log_index_size": args.log_index_size, "seed": 42,
                    "parallelism": f"key-range shards, {world} rank(s), no data-path collective"},
-        "build_mkeys_s": round(world * N / (build_ms * 1e-3) / 1e6, 1),
-        "probe_mkeys_s": round(world * N / (probe_ms * 1e-3) / 1e6, 1),
+        "build_mkeys_s": round(keys_all / (build_ms * 1e-3) / 1e6, 1),
+        "probe_mkeys_s": round(keys_all / (probe_ms * 1e-3) / 1e6, 1),
         "e2e_pcie_mkeys_s": round(e2e, 1) if e2e else None,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -243,7 +258,7 @@ def main():
         "verified": verified,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args, args.log_index_size)
+        cb = cpu_baseline(args, args.log_index_size, n)
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu"] = round(value / cb["value"], 1)
     if rank == 0:
