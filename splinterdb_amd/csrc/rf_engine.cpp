@@ -22,10 +22,12 @@ using namespace rf;
 extern "C" int rf_launch_build(const LaunchArgs* a);
 extern "C" int rf_launch_old_decode(const LaunchArgs* a, uint32_t f, uint32_t old_num_indices,
                                     uint32_t* d_cnt, uint32_t* d_pos);
+extern "C" int rf_launch_prec(const LaunchArgs* a);
 extern "C" int rf_launch_probe(const LaunchArgs* a, int kind, const void* in0, const uint64_t* offs,
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found);
 
 static thread_local std::string g_err;
+static uint32_t g_probe_ablate = 0;  // diagnostics only (rf_amd_debug_probe_ablate)
 static int fail(int rc, const std::string& msg) {
   g_err = msg;
   return rc;
@@ -68,12 +70,12 @@ struct rf_amd_batch {
   uint32_t F = 0;
   bool wide = false;
   std::vector<FilterPlan> plans;
-  std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter;
+  std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter, idx_filter;
   uint64_t E = 0, keys_total = 0;
   uint32_t CB = 0, I = 0, PS = 0, PF = 0;
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
-      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans;
+      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_precs, d_idx_filter;
   std::vector<uint32_t> old_num_indices;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing (rf_amd_batch_set_timing)
@@ -209,6 +211,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     }
     for (uint32_t i = 0; i < (1u << p.cbits); i++) b->cb_filter.push_back(f);
     for (uint32_t i = 0; i < p.page_cap; i++) b->pg_filter.push_back(f);
+    b->idx_filter.insert(b->idx_filter.end(), p.num_indices, f);
     e_first += nfp;
     key_first += p.num_new;
     cb_base += 1u << p.cbits;
@@ -238,6 +241,8 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   rc |= b->d_idx_cnt.alloc(4 * b->I);
   rc |= b->d_idx_start.alloc(4 * b->I);
   rc |= b->d_slots.alloc(8 * b->I);
+  rc |= b->d_precs.alloc(16ull * b->I);
+  rc |= b->d_idx_filter.alloc(4ull * b->I);
   rc |= b->d_page_first.alloc(4 * b->PF);
   rc |= b->d_pg_filter.alloc(4 * b->PS);
   rc |= b->d_pages.alloc((size_t)b->PS * P + 256);
@@ -271,6 +276,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   UP(b->d_old_tile_start, b->old_tile_start);
   UP(b->d_cb_filter, b->cb_filter);
   UP(b->d_pg_filter, b->pg_filter);
+  UP(b->d_idx_filter, b->idx_filter);
 #undef UP
   HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -319,6 +325,9 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.first_old = b->d_first_old.as<uint32_t>();
   a.has_old = b->d_has_old.as<uint32_t>();
   a.slots = b->d_slots.as<uint64_t>();
+  a.precs = b->d_precs.as<uint4>();
+  a.idx_filter = b->d_idx_filter.as<uint32_t>();
+  a.num_idx = b->I;
   a.page_first = b->d_page_first.as<uint32_t>();
   a.pg_filter = b->d_pg_filter.as<uint32_t>();
   a.num_page_slots = b->PS;
@@ -385,6 +394,7 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   HIPCHK(hipSetDevice(b->eng->device));
   hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
   LaunchArgs a = make_args(b, st);
+  a.ablate = g_probe_ablate;
   int rc = rf_launch_probe(&a, kind, in0, offs, key_len, fid, n, found);
   if (rc) return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
   return 0;
@@ -404,6 +414,9 @@ extern "C" int rf_amd_batch_probe_hashes(rf_amd_batch* b, const uint32_t* d_hash
                                          uint64_t n, uint64_t* d_found, void* stream) {
   return do_probe(b, IN_HASH, d_hashes, nullptr, 4, d_filter_id, n, d_found, stream);
 }
+
+// Diagnostic: 1 = hash only, 2 = + index slot, 3 = + block head; 0 = normal probe.
+extern "C" void rf_amd_debug_probe_ablate(uint32_t mode) { g_probe_ablate = mode; }
 
 extern "C" int rf_amd_batch_set_timing(rf_amd_batch* b, int enable) {
   if (!b) return fail(RF_AMD_EINVAL, "null batch");
@@ -530,18 +543,25 @@ static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf
   rc |= b->d_pplans.alloc(16);
   rc |= b->d_pages.alloc((size_t)img->info.num_pages * cfg->page_size + 256);
   rc |= b->d_slots.alloc(8ull * p.num_indices);
+  rc |= b->d_precs.alloc(16ull * p.num_indices);
+  rc |= b->d_idx_filter.alloc(4ull * p.num_indices);
   if (rc) {
     delete b;
     return fail(RF_AMD_ENOMEM, "device allocation failed");
   }
   hipStream_t st = e->stream;
   HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
+  HIPCHK(hipMemsetAsync(b->d_idx_filter.p, 0, b->d_idx_filter.n, st));
   HIPCHK(hipMemcpyAsync(b->d_pages.p, img->pages, (size_t)img->info.num_pages * cfg->page_size,
                         hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(b->d_slots.p, img->slots, 8ull * p.num_indices, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(b->d_plans.p, &p, sizeof(p), hipMemcpyHostToDevice, st));
   const uint4 pp1 = make_uint4(p.vs | (p.rem << 8) | (p.rvs << 16), 0, 0, 0);
   HIPCHK(hipMemcpyAsync(b->d_pplans.p, &pp1, sizeof(pp1), hipMemcpyHostToDevice, st));
+  {
+    LaunchArgs a = make_args(b, st);
+    if (int lrc = rf_launch_prec(&a)) return fail(RF_AMD_EINVAL, std::string("prec launch: ") + hipGetErrorString((hipError_t)lrc));
+  }
   HIPCHK(hipStreamSynchronize(st));
   b->built = true;
   *out = b;

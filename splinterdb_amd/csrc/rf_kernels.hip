@@ -939,9 +939,9 @@ struct ProbeLane {
   uint64_t hdr;       // header byte offset in pg
 };
 
-__device__ __forceinline__ ProbeLane probe_locate(const uint4 pp, const uint8_t* pages, const uint64_t* slots,
+__device__ __forceinline__ ProbeLane probe_locate(const uint4 pp, const uint8_t* pages, const uint4* precs,
                                                   uint32_t h, uint32_t fp_size, uint32_t lis,
-                                                  uint32_t page_size) {
+                                                  uint32_t page_size, uint4& rec) {
   ProbeLane L;
   L.vs = pp.x & 0xff;
   const uint32_t rem = (pp.x >> 8) & 0xff;
@@ -954,12 +954,13 @@ __device__ __forceinline__ ProbeLane probe_locate(const uint4 pp, const uint8_t*
   const uint32_t index = irvs >= 32 ? 0u : x >> irvs;
   L.remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
   L.pg = pages + (uint64_t)pp.y * page_size;
-  L.hdr = slots[pp.z + index];
+  rec = precs[pp.z + index];
+  L.hdr = rec.x & ((1u << 26) - 1);
   return L;
 }
 
 // W = the 128 bytes at (hdr & ~15) as 16 little-endian u64
-__device__ __forceinline__ uint64_t probe_finish(const ProbeLane& L, const uint64_t (&W)[16], uint32_t lis) {
+__device__ __forceinline__ uint64_t probe_finish(const ProbeLane& L, uint64_t (&W)[16], uint32_t lis) {
   const uint32_t index_size = 1u << lis;
   const uint32_t bo = L.bo, vs = L.vs, rvs = L.rvs;
   const uint8_t* pg = L.pg;
@@ -979,28 +980,48 @@ __device__ __forceinline__ uint64_t probe_finish(const ProbeLane& L, const uint6
   uint32_t start = 0, end = 0, cum = 0;
   bool have_start = (bo == 0), done = false;
   if (e0 + c + index_size <= 1024) {
-    // select over the registers (compile-time indices only)
+    // Select over the registers: per-word popcounts -> the words holding 1-bit #(bo-1) and
+    // #bo (compile-time indices only) -> one bisection select + one ctz. Bits before the
+    // encoding (header, previous block) are masked off.
+    uint32_t j1 = 16, j2 = 16, c1 = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      uint64_t x = W[k];
       const uint32_t wb = 64u * k;
+      uint64_t x = W[k];
       if (wb + 64 <= e0) x = 0;
       else if (wb < e0) x = (x >> (e0 - wb)) << (e0 - wb);
+      W[k] = x;
       const uint32_t pc = __popcll(x);
-      if (!done) {
-        const uint32_t base = wb - e0;
-        if (!have_start && cum + pc > target_lo) {
-          start = base + select64_fast(x, target_lo - cum) + 1 - bo;
-          have_start = true;
-        }
-        if (cum + pc > bo) {
-          end = base + select64_fast(x, bo - cum) - bo;
-          done = true;
-        }
-        cum += pc;
-      }
+      const bool h1 = (j1 == 16) && (cum + pc > target_lo);
+      const bool h2 = (j2 == 16) && (cum + pc > bo);
+      c1 = h1 ? cum : c1;
+      j1 = h1 ? (uint32_t)k : j1;
+      j2 = h2 ? (uint32_t)k : j2;
+      cum += pc;
     }
-    if (!done) return 0;  // corrupt image
+    if (j2 == 16) return 0;  // corrupt image
+    // word j of W without a runtime index (a select chain gets rewritten into an indexed
+    // load, which sends W to scratch): OR of words masked by (j == k)
+    auto pick16 = [&](uint32_t j) {
+      uint64_t r = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) r |= W[k] & (0ull - (uint64_t)(j == (uint32_t)k));
+      return r;
+    };
+    const uint64_t x1 = pick16(j1);
+    const uint32_t p1 = 64u * j1 + select64_fast(x1, target_lo - c1);  // 1-bit #(bo-1) or #0
+    uint32_t p2;
+    if (bo == 0) {
+      p2 = p1;
+    } else if (j2 == j1) {  // 1-bit #bo follows #(bo-1) in the same word
+      const uint32_t b1 = p1 & 63;
+      const uint64_t rest = b1 == 63 ? 0ull : (x1 & (~0ull << (b1 + 1)));
+      p2 = 64u * j1 + (uint32_t)__builtin_ctzll(rest);
+    } else {  // ... or is the first 1-bit of word j2
+      p2 = 64u * j2 + (uint32_t)__builtin_ctzll(pick16(j2));
+    }
+    start = bo ? (p1 - e0) + 1 - bo : 0;
+    end = (p2 - e0) - bo;
   } else {
     // long encodings (> ~860 entries in the index): stream 128-bit windows
     const uint32_t nwin = (e0 + c + index_size + 127) / 128 + 1;
@@ -1060,6 +1081,184 @@ __device__ __forceinline__ uint64_t probe_finish(const ProbeLane& L, const uint6
   return found;
 }
 
+// ---- probe records --------------------------------------------------------------------
+// Device-only, 16 bytes per index (not part of the on-disk image): bits [0,26) relative
+// slot, [26,39) entry count c, then for k = 1..7 the first entry of bucket k*IS/8 (12 bits
+// each, [39+12(k-1), 51+12(k-1))), bit 127 = "use the full-scan path" (c >= 4096 or IS < 8).
+// A probe then reads the record (L2-resident, 256 KB per 16384-index filter) and only a
+// 48-byte window of the encoding starting at its sampled bucket.
+__device__ __forceinline__ uint32_t rec_bits(const uint4 r, uint32_t pos, uint32_t n) {
+  const uint32_t w = pos >> 5, sh = pos & 31;
+  const uint32_t a = w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
+  const uint32_t b = w == 0 ? r.y : (w == 1 ? r.z : (w == 2 ? r.w : 0u));
+  const uint64_t v = ((uint64_t)a | ((uint64_t)b << 32)) >> sh;
+  return (uint32_t)(v & ((1ull << n) - 1));
+}
+__device__ __forceinline__ void rec_put(uint32_t (&r)[4], uint32_t pos, uint32_t n, uint32_t val) {
+  const uint64_t v = (uint64_t)(val & ((1u << n) - 1)) << (pos & 31);
+  const uint32_t w = pos >> 5;
+  r[w] |= (uint32_t)v;
+  if (w < 3) r[w + 1] |= (uint32_t)(v >> 32);
+}
+
+// one wave per index: popcount prefix over the unary encoding -> bucket starts at k*IS/8
+__global__ __launch_bounds__(256) void k_prec(const FilterPlan* __restrict__ plans,
+                                              const uint32_t* __restrict__ idx_filter,
+                                              const uint64_t* __restrict__ slots,
+                                              const uint8_t* __restrict__ pages,
+                                              const FilterOut* __restrict__ outs,
+                                              uint4* __restrict__ precs, uint32_t num_idx,
+                                              uint32_t lis, uint32_t page_size) {
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  if (g >= num_idx) return;
+  const uint32_t f = idx_filter[g];
+  const FilterPlan& P = plans[f];
+  if (outs && (outs[f].error || g - P.idx_base >= P.num_indices)) return;
+  const uint32_t IS = 1u << lis, S = IS / 8;
+  const uint64_t rel = slots[g];
+  const uint8_t* pg = pages + (uint64_t)P.page_base * page_size;
+  const uint32_t c = (uint32_t)pg[rel] | ((uint32_t)pg[rel + 1] << 8);
+  uint32_t r[4] = {0, 0, 0, 0};
+  rec_put(r, 0, 26, (uint32_t)rel);
+  rec_put(r, 26, 13, c);
+  if (c >= 4096 || S == 0) {
+    r[3] |= 0x80000000u;
+  } else {
+    const uint64_t ebit = (rel + 2) * 8;
+    const uint32_t nbits = c + IS;
+    uint32_t ones_before = 0;
+    for (uint32_t base = 0; base < nbits; base += 64 * WAVE) {
+      const uint32_t b0 = base + lane * 64;
+      uint64_t x = 0;
+      if (b0 < nbits) {
+        const uint64_t bp = ebit + b0;
+        const uint32_t sh = (uint32_t)(bp & 7);
+        x = ld_u64_unaligned(pg, bp >> 3) >> sh;
+        if (sh) x |= (uint64_t)pg[(bp >> 3) + 8] << (64 - sh);
+        const uint32_t nb = min(64u, nbits - b0);
+        if (nb < 64) x &= (1ull << nb) - 1;
+      }
+      const uint32_t ones = __popcll(x);
+      const uint32_t ex = wave_incl_scan(ones) - ones + ones_before;
+      for (uint32_t k = 1; k < 8; k++) {
+        const uint32_t t = k * S - 1;  // terminator of bucket k*S - 1
+        if (t >= ex && t < ex + ones) {
+          const uint32_t pos = b0 + select64_fast(x, t - ex);
+          rec_put(r, 39 + 12 * (k - 1), 12, pos - t);  // zeros before it = first entry of bucket k*S
+        }
+      }
+      ones_before = __shfl(ex + ones, WAVE - 1, WAVE);
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    uint32_t v = r[w];
+    for (int d = 1; d < WAVE; d <<= 1) v |= __shfl_xor(v, d, WAVE);
+    r[w] = v;
+  }
+  if (lane == 0) precs[g] = make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+
+// Record-guided probe: returns false when the lane must take the full-scan path.
+__device__ __forceinline__ bool probe_rec(const ProbeLane& L, const uint4 rec, uint32_t lis, uint64_t& found) {
+  const uint32_t IS = 1u << lis, S = IS / 8;
+  const uint32_t bo = L.bo, vs = L.vs, rvs = L.rvs;
+  const uint8_t* pg = L.pg;
+  const uint64_t hdr = L.hdr;
+  const uint32_t c = rec_bits(rec, 26, 13);
+  const uint32_t s = bo / S, K = s * S;
+  const uint32_t zs = s ? rec_bits(rec, 39 + 12 * (s - 1), 12) : 0u;
+  const uint64_t ebit = (hdr + 2) * 8;
+  const uint64_t A = ebit + K + zs;            // first bit of bucket K
+  const uint64_t a16 = (A >> 3) & ~15ull;
+  uint64_t W[6];
+  {
+    const v4u* q = reinterpret_cast<const v4u*>(pg + a16);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const v4u v = q[k];
+      W[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      W[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+  }
+  const uint32_t d = (uint32_t)(A - a16 * 8);  // < 136
+  // ranks (from bucket K's terminator, 1-bit #K) of 1-bits #(bo-1) and #bo
+  const uint32_t r2 = bo - K;
+  const uint32_t r1 = r2 ? r2 - 1 : 0;
+  uint32_t j1 = 6, j2 = 6, c1 = 0, cum = 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const uint32_t wb = 64u * k;
+    uint64_t x = W[k];
+    if (wb + 64 <= d) x = 0;
+    else if (wb < d) x = (x >> (d - wb)) << (d - wb);
+    W[k] = x;
+    const uint32_t pc = __popcll(x);
+    const bool h1 = (j1 == 6) && (cum + pc > r1);
+    const bool h2 = (j2 == 6) && (cum + pc > r2);
+    c1 = h1 ? cum : c1;
+    j1 = h1 ? (uint32_t)k : j1;
+    j2 = h2 ? (uint32_t)k : j2;
+    cum += pc;
+  }
+  if (j2 == 6) return false;  // bucket runs past the 48-byte window
+  auto pick6 = [&](uint32_t j) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) r |= W[k] & (0ull - (uint64_t)(j == (uint32_t)k));
+    return r;
+  };
+  const uint64_t x1 = pick6(j1);
+  const uint32_t q1 = 64u * j1 + select64_fast(x1, r1 - c1);
+  uint32_t q2;
+  if (r2 == 0) {
+    q2 = q1;
+  } else if (j2 == j1) {
+    const uint32_t b1 = q1 & 63;
+    const uint64_t rest = b1 == 63 ? 0ull : (x1 & (~0ull << (b1 + 1)));
+    q2 = 64u * j1 + (uint32_t)__builtin_ctzll(rest);
+  } else {
+    q2 = 64u * j2 + (uint32_t)__builtin_ctzll(pick6(j2));
+  }
+  // encoding-relative positions
+  const uint32_t rel0 = (uint32_t)(a16 * 8 - ebit);  // may wrap (negative): modular arithmetic
+  const uint32_t start = r2 ? (rel0 + q1) + 1 - bo : zs;
+  const uint32_t end = (rel0 + q2) - bo;
+  found = 0;
+  if (start >= end) return true;
+  // a speculative remainder load issued beside the encoding window (position estimated
+  // from the record) measured slower: +14 VGPRs cost a wave per SIMD (1.60 -> 1.88 ms)
+  const uint32_t enc = (c + IS - 1) / 8 + 4;
+  const uint64_t rbit0 = (hdr + 2 + enc) * 8;
+  const uint64_t bs = rbit0 + (uint64_t)start * rvs;
+  const uint64_t ra = (bs >> 3) & ~15ull;
+  uint64_t w0, w1, w2 = 0, w3 = 0;
+  ld_win(pg, ra, w0, w1);
+  const uint64_t last_bit = rbit0 + (uint64_t)end * rvs - ra * 8;
+  if (last_bit > 128) ld_win(pg, ra + 16, w2, w3);
+  const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
+  const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
+  for (uint32_t pos = start; pos < end; pos++) {
+    const uint64_t bb = rbit0 + (uint64_t)pos * rvs - ra * 8;
+    uint32_t rv;
+    if (bb + rvs <= 256) {
+      const uint32_t j = (uint32_t)(bb >> 6), sh = (uint32_t)(bb & 63);
+      uint64_t v = pick4(j, w0, w1, w2, w3) >> sh;
+      if (sh + rvs > 64) v |= pick4(j + 1, w0, w1, w2, w3) << (64 - sh);
+      rv = (uint32_t)v & rvmask;
+    } else {
+      rv = ld_bits(pg, rbit0 + (uint64_t)pos * rvs, rvs);
+    }
+    if ((rv >> vs) == L.remainder) {
+      const uint32_t v = rv & vmask;
+      if (v < 64) found |= 1ull << v;
+    }
+  }
+  return true;
+}
+
 // XCD-aware block -> chunk remap (bijective for any grid): the blocks that share an XCD
 // (b % 8, round-robin dispatch) process one contiguous eighth of the probe array, so an
 // XCD's L2 holds the images of the filters its probes hit (MI355X_MICROARCH.md, XCD L2).
@@ -1077,13 +1276,14 @@ constexpr int PROBE_NT = 256;
 template <int KIND, bool STAGE = false>
 __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
                                                     const uint8_t* __restrict__ pages,
-                                                    const uint64_t* __restrict__ slots,
+                                                    const uint4* __restrict__ precs,
                                                     const void* __restrict__ in0,
                                                     const uint64_t* __restrict__ offs, uint32_t key_len,
                                                     const uint32_t* __restrict__ filter_id, uint64_t n,
                                                     uint64_t* __restrict__ found, uint32_t fp_size,
                                                     uint32_t seed, uint32_t lis, uint32_t page_size,
-                                                    uint32_t num_filters, const FilterOut* __restrict__ outs) {
+                                                    uint32_t num_filters, const FilterOut* __restrict__ outs,
+                                                    uint32_t ablate) {
   __shared__ __attribute__((aligned(16))) v4u s_blk[STAGE ? PROBE_NT * 8 : 1];  // 128 B per probe
   const uint64_t i = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -1095,6 +1295,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     live = fid < num_filters && !(outs && outs[fid].error);  // unknown / failed filter: 0
   }
   ProbeLane L{};
+  uint4 rec = make_uint4(0, 0, 0, 0);
   if (live) {
     uint32_t h;
     if constexpr (KIND == IN_KEYS24) {
@@ -1114,7 +1315,15 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     } else {
       h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + i);
     }
-    L = probe_locate(pplans[fid], pages, slots, h, fp_size, lis, page_size);
+    if (ablate == 1) {  // diagnostic: key stream + hash only
+      if (i < n) __builtin_nontemporal_store((uint64_t)h, found + i);
+      return;
+    }
+    L = probe_locate(pplans[fid], pages, precs, h, fp_size, lis, page_size, rec);
+    if (ablate == 2) {  // diagnostic: + index slot
+      __builtin_nontemporal_store(L.hdr, found + i);
+      return;
+    }
   }
   // (B) cooperative staging: instruction k moves probes 8k..8k+7, lane -> (probe, 16-B part)
   if constexpr (STAGE) {
@@ -1134,13 +1343,24 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     __builtin_nontemporal_store((uint64_t)0, found + i);
     return;
   }
+  if (!STAGE && ablate != 3 && !(rec.w & 0x80000000u)) {
+    uint64_t fr;
+    if (probe_rec(L, rec, lis, fr)) {
+      __builtin_nontemporal_store(fr, found + i);
+      return;
+    }
+  }
   uint64_t W[16];
   const v4u* src = STAGE ? wbuf + lane * 8 : reinterpret_cast<const v4u*>(L.pg + (L.hdr & ~15ull));
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const v4u v = src[k];
+  for (int k = 0; k < 8; k++) {  // all 8 loads at once: one dependency level (a second,
+    const v4u v = src[k];        // conditional level measured 2x slower on MI355X)
     W[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
     W[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
+  if (ablate == 3) {  // diagnostic: + block head, no select / remainders
+    __builtin_nontemporal_store(W[0] ^ W[5] ^ W[11] ^ W[15], found + i);
+    return;
   }
   const uint64_t r = probe_finish(L, W, lis);
   __builtin_nontemporal_store(r, found + i);
@@ -1222,7 +1442,18 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
                      a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages, a.lis,
                      a.page_size);
   CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_prec, dim3((a.num_idx + 3) / 4), dim3(256), 0, (hipStream_t)a.stream, a.plans,
+                     a.idx_filter, a.slots, a.pages, a.outs, a.precs, a.num_idx, a.lis, a.page_size);
+  CHECK_LAUNCH();
   REC(EV_B_ASSEMBLE);
+  return 0;
+}
+
+extern "C" int rf_launch_prec(const LaunchArgs* pa) {
+  const LaunchArgs& a = *pa;
+  hipLaunchKernelGGL(k_prec, dim3((a.num_idx + 3) / 4), dim3(256), 0, (hipStream_t)a.stream, a.plans,
+                     a.idx_filter, a.slots, a.pages, a.outs, a.precs, a.num_idx, a.lis, a.page_size);
+  CHECK_LAUNCH();
   return 0;
 }
 
@@ -1248,11 +1479,11 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
   dim3 g((uint32_t)((n + PROBE_NT - 1) / PROBE_NT)), b(PROBE_NT);
   REC(EV_P_START);
   switch (kind) {
-    case IN_KEYS24: hipLaunchKernelGGL(k_probe<IN_KEYS24>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    case IN_KEYS_W: hipLaunchKernelGGL(k_probe<IN_KEYS_W>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    case IN_KEYS_B: hipLaunchKernelGGL(k_probe<IN_KEYS_B>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    case IN_VAR:    hipLaunchKernelGGL(k_probe<IN_VAR>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
-    default:        hipLaunchKernelGGL(k_probe<IN_HASH>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.slots, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs); break;
+    case IN_KEYS24: hipLaunchKernelGGL(k_probe<IN_KEYS24>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
+    case IN_KEYS_W: hipLaunchKernelGGL(k_probe<IN_KEYS_W>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
+    case IN_KEYS_B: hipLaunchKernelGGL(k_probe<IN_KEYS_B>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
+    case IN_VAR:    hipLaunchKernelGGL(k_probe<IN_VAR>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
+    default:        hipLaunchKernelGGL(k_probe<IN_HASH>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
   }
   CHECK_LAUNCH();
   REC(EV_P_END);

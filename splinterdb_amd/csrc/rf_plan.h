@@ -84,11 +84,15 @@ struct LaunchArgs {
   uint32_t* first_old;  // wide mode: per index, smallest old entry (valid if has_old)
   uint32_t* has_old;
   uint64_t* slots;
+  uint4* precs;             // device-only probe records, one per index
+  const uint32_t* idx_filter;
+  uint32_t num_idx;
   uint32_t* page_first;
   const uint32_t* pg_filter;
   uint32_t num_page_slots;
   uint8_t* pages;
   FilterOut* outs;
+  uint32_t ablate;  // probe diagnostics (0 = normal)
   void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)
 };
 

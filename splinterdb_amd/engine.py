@@ -33,7 +33,7 @@ EXPORTED = [
     "rf_amd_batch_build_var_keys", "rf_amd_batch_build_hashes", "rf_amd_batch_probe_keys",
     "rf_amd_batch_probe_var_keys", "rf_amd_batch_probe_hashes", "rf_amd_batch_info",
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
-    "rf_amd_batch_set_timing", "rf_amd_batch_timings",
+    "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_debug_probe_ablate",
     "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",
     "rf_amd_image_free",
     "rf_amd_max_fingerprints", "rf_amd_estimate_unique_keys_from_count",
@@ -99,6 +99,8 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_image_ptrs.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(vp)]
     L.rf_amd_batch_set_timing.argtypes = [vp, i32]
     L.rf_amd_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), u32]
+    L.rf_amd_debug_probe_ablate.argtypes = [u32]
+    L.rf_amd_debug_probe_ablate.restype = None
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
     L.rf_amd_filter_add.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),

@@ -1,0 +1,36 @@
+"""Diagnostic: time k_probe truncated after each step (hash / slot / block head / full),
+interleaved rounds in one process (cdna_hip_programming.md rule 24). C2 shape."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from splinterdb_amd import engine as E  # noqa: E402
+from splinterdb_amd import keys as K  # noqa: E402
+
+F, n = 8, 8_000_000
+N = F * n
+cfg = E.routing_config_init()
+dev = torch.device("cuda", 0)
+keys = K.seq_keys_torch(0, N, 24, dev)
+fid = (torch.arange(N, device=dev) // n).to(torch.int32)
+found = torch.empty(N, dtype=torch.int64, device=dev)
+b = E.FilterBatch(cfg, [n] * F)
+b.set_timing(True)
+b.build_keys(keys, 24)
+torch.cuda.synchronize()
+L = E.load_library()
+res = {m: [] for m in (1, 2, 3, 0)}
+for rnd in range(6):
+    for m in (1, 2, 3, 0):
+        L.rf_amd_debug_probe_ablate(m)
+        b.probe_keys(keys, 24, fid, N, found)
+        torch.cuda.synchronize()
+        res[m].append(b.timings()["probe"])
+L.rf_amd_debug_probe_ablate(0)
+out = {("hash", "slot", "blockhead", "full")[i]: round(float(np.median(res[m][1:])), 4)
+       for i, m in enumerate((1, 2, 3, 0))}
+print(json.dumps(out))
