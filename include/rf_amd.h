@@ -115,8 +115,8 @@ uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
  * stage did not run. */
 #define RF_AMD_NUM_TIMINGS 9
 int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
-/* diagnostics: truncate later probes after 1 = hashing, 2 = the index slot, 3 = the
- * block-head load (results are then NOT found_values); 0 restores normal probes */
+/* diagnostics: truncate later probes after 1 = hashing, 2 = the probe-record load
+ * (results are then NOT found_values); 0 restores normal probes */
 void rf_amd_debug_probe_ablate(uint32_t mode);
 int rf_amd_batch_timings(rf_amd_batch *b, float *ms, uint32_t n);
 

@@ -300,6 +300,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.wide = b->wide;
   a.plans = b->d_plans.as<FilterPlan>();
   a.pplans = b->d_pplans.as<uint4>();
+  a.pplans_mut = b->d_pplans.as<uint4>();
   a.num_filters = b->F;
   a.tile_filter = b->d_tile_filter.as<uint32_t>();
   a.tile_start = b->d_tile_start.as<uint32_t>();
@@ -394,7 +395,8 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   HIPCHK(hipSetDevice(b->eng->device));
   hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
   LaunchArgs a = make_args(b, st);
-  a.ablate = g_probe_ablate;
+  a.ablate = g_probe_ablate & 0xff;
+  a.occ = g_probe_ablate >> 8;
   int rc = rf_launch_probe(&a, kind, in0, offs, key_len, fid, n, found);
   if (rc) return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
   return 0;
@@ -415,7 +417,8 @@ extern "C" int rf_amd_batch_probe_hashes(rf_amd_batch* b, const uint32_t* d_hash
   return do_probe(b, IN_HASH, d_hashes, nullptr, 4, d_filter_id, n, d_found, stream);
 }
 
-// Diagnostic: 1 = hash only, 2 = + index slot, 3 = + block head; 0 = normal probe.
+// Diagnostic: low byte 1 = hash only, 2 = + probe record; 0 = normal probe. Bits 8+: cap
+// the probe kernel at that many waves per SIMD via LDS padding (occupancy experiments).
 extern "C" void rf_amd_debug_probe_ablate(uint32_t mode) { g_probe_ablate = mode; }
 
 extern "C" int rf_amd_batch_set_timing(rf_amd_batch* b, int enable) {

@@ -572,6 +572,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
                                                       const uint32_t* __restrict__ sorted32,
                                                       const uint32_t* __restrict__ first_old,
                                                       const uint32_t* __restrict__ has_old,
+                                                      uint4* __restrict__ pplans,
                                                       uint64_t* __restrict__ slots,
                                                       uint32_t* __restrict__ page_first,
                                                       FilterOut* __restrict__ outs,
@@ -614,9 +615,13 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   }
   __syncthreads();
   if (s_err) {
-    if (threadIdx.x == 0) outs[f].error |= s_err;
+    if (threadIdx.x == 0) {
+      outs[f].error |= s_err;
+      pplans[f].w = s_err;  // probes of a failed filter find nothing
+    }
     return;
   }
+  if (threadIdx.x == 0) pplans[f].w = 0;
   // next(j) by binary search on the prefix sums
   for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT) {
     uint32_t q = n;
@@ -721,7 +726,10 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   if (threadIdx.x == 0) {
     if (npages <= P.page_cap) pf[npages] = n;
     outs[f].num_pages = npages;
-    if (npages > P.page_cap) outs[f].error |= ERR_PAGE_CAP;
+    if (npages > P.page_cap) {
+      outs[f].error |= ERR_PAGE_CAP;
+      pplans[f].w = ERR_PAGE_CAP;
+    }
   }
 }
 
@@ -955,125 +963,54 @@ __device__ __forceinline__ ProbeLane probe_locate(const uint4 pp, const uint8_t*
   L.remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
   L.pg = pages + (uint64_t)pp.y * page_size;
   rec = precs[pp.z + index];
+  // one 16-byte load: without this the compiler splits it into two 8-byte loads on either
+  // side of a branch (an extra dependent round trip: 1.60 -> 1.84 ms at C2)
+  asm volatile("" : "+v"(rec.x), "+v"(rec.y), "+v"(rec.z), "+v"(rec.w));
   L.hdr = rec.x & ((1u << 26) - 1);
   return L;
 }
 
-// W = the 128 bytes at (hdr & ~15) as 16 little-endian u64
-__device__ __forceinline__ uint64_t probe_finish(const ProbeLane& L, uint64_t (&W)[16], uint32_t lis) {
+// Full-scan fallback (records flag c >= 4096, or the bucket runs past the record path's
+// 48-byte window): 128-bit windows streamed from the header, then per-entry bit reads.
+// Kept lean (no large register arrays) so it does not cost the common path occupancy.
+__device__ __forceinline__ uint64_t probe_stream(uint32_t bo, uint32_t remainder, uint32_t vs, uint32_t rvs,
+                                                 const uint8_t* pg, uint64_t hdr, uint32_t lis) {
   const uint32_t index_size = 1u << lis;
-  const uint32_t bo = L.bo, vs = L.vs, rvs = L.rvs;
-  const uint8_t* pg = L.pg;
-  const uint64_t hdr = L.hdr;
-  const uint64_t a0 = hdr & ~15ull;
-  const uint32_t hs = (uint32_t)(hdr - a0) * 8;  // header bit offset in the 1024-bit span
-  uint32_t c;
-  {
-    const uint32_t j = hs >> 6, sh = hs & 63;  // hs <= 120: words 0..1 (+2 when straddling)
-    uint64_t v = (j == 0 ? W[0] : W[1]) >> sh;
-    if (sh > 48) v |= (j == 0 ? W[1] : W[2]) << (64 - sh);
-    c = (uint32_t)(v & 0xffff);
-  }
+  const uint32_t c = (uint32_t)pg[hdr] | ((uint32_t)pg[hdr + 1] << 8);
   const uint32_t enc = (c + index_size - 1) / 8 + 4;
-  const uint32_t e0 = hs + 16;  // encoding bit 0 in span coordinates
+  const uint64_t a0 = (hdr + 2) & ~15ull;
+  const uint32_t e0 = (uint32_t)((hdr + 2 - a0) * 8);  // encoding bit 0 in window coordinates
   const uint32_t target_lo = bo ? bo - 1 : 0;
   uint32_t start = 0, end = 0, cum = 0;
-  bool have_start = (bo == 0), done = false;
-  if (e0 + c + index_size <= 1024) {
-    // Select over the registers: per-word popcounts -> the words holding 1-bit #(bo-1) and
-    // #bo (compile-time indices only) -> one bisection select + one ctz. Bits before the
-    // encoding (header, previous block) are masked off.
-    uint32_t j1 = 16, j2 = 16, c1 = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const uint32_t wb = 64u * k;
-      uint64_t x = W[k];
-      if (wb + 64 <= e0) x = 0;
-      else if (wb < e0) x = (x >> (e0 - wb)) << (e0 - wb);
-      W[k] = x;
-      const uint32_t pc = __popcll(x);
-      const bool h1 = (j1 == 16) && (cum + pc > target_lo);
-      const bool h2 = (j2 == 16) && (cum + pc > bo);
-      c1 = h1 ? cum : c1;
-      j1 = h1 ? (uint32_t)k : j1;
-      j2 = h2 ? (uint32_t)k : j2;
-      cum += pc;
+  bool have_start = (bo == 0);
+  const uint32_t nwin = (e0 + c + index_size + 127) / 128 + 1;
+  for (uint32_t k = 0;; k++) {
+    if (k > nwin) return 0;  // corrupt image: never hang
+    uint64_t lo, hi;
+    ld_win(pg, a0 + 16ull * k, lo, hi);
+    if (k == 0 && e0) {
+      if (e0 >= 64) { lo = 0; hi = (hi >> (e0 - 64)) << (e0 - 64); }
+      else { lo = (lo >> e0) << e0; }
     }
-    if (j2 == 16) return 0;  // corrupt image
-    // word j of W without a runtime index (a select chain gets rewritten into an indexed
-    // load, which sends W to scratch): OR of words masked by (j == k)
-    auto pick16 = [&](uint32_t j) {
-      uint64_t r = 0;
-#pragma unroll
-      for (int k = 0; k < 16; k++) r |= W[k] & (0ull - (uint64_t)(j == (uint32_t)k));
-      return r;
-    };
-    const uint64_t x1 = pick16(j1);
-    const uint32_t p1 = 64u * j1 + select64_fast(x1, target_lo - c1);  // 1-bit #(bo-1) or #0
-    uint32_t p2;
-    if (bo == 0) {
-      p2 = p1;
-    } else if (j2 == j1) {  // 1-bit #bo follows #(bo-1) in the same word
-      const uint32_t b1 = p1 & 63;
-      const uint64_t rest = b1 == 63 ? 0ull : (x1 & (~0ull << (b1 + 1)));
-      p2 = 64u * j1 + (uint32_t)__builtin_ctzll(rest);
-    } else {  // ... or is the first 1-bit of word j2
-      p2 = 64u * j2 + (uint32_t)__builtin_ctzll(pick16(j2));
+    const uint32_t pc = __popcll(lo) + __popcll(hi);
+    const uint32_t base = 128u * k - e0;
+    if (!have_start && cum + pc > target_lo) {
+      start = base + select128(lo, hi, target_lo - cum) + 1 - bo;
+      have_start = true;
     }
-    start = bo ? (p1 - e0) + 1 - bo : 0;
-    end = (p2 - e0) - bo;
-  } else {
-    // long encodings (> ~860 entries in the index): stream 128-bit windows
-    const uint32_t nwin = (e0 + c + index_size + 127) / 128 + 1;
-    for (uint32_t k = 0;; k++) {
-      if (k > nwin) return 0;
-      uint64_t lo, hi;
-      ld_win(pg, a0 + 16ull * k, lo, hi);
-      const uint32_t wb = 128u * k;
-      if (wb + 128 <= e0) { lo = 0; hi = 0; }
-      else if (wb < e0) {
-        const uint32_t cut = e0 - wb;
-        if (cut >= 64) { lo = 0; hi = (hi >> (cut - 64)) << (cut - 64); }
-        else { lo = (lo >> cut) << cut; }
-      }
-      const uint32_t pc = __popcll(lo) + __popcll(hi);
-      const uint32_t base = wb - e0;
-      if (!have_start && cum + pc > target_lo) {
-        start = base + select128(lo, hi, target_lo - cum) + 1 - bo;
-        have_start = true;
-      }
-      if (cum + pc > bo) {
-        end = base + select128(lo, hi, bo - cum) - bo;
-        break;
-      }
-      cum += pc;
+    if (cum + pc > bo) {
+      end = base + select128(lo, hi, bo - cum) - bo;
+      break;
     }
+    cum += pc;
   }
   if (start >= end) return 0;
-  // remainders [start, end): the 16-byte window holding the first one, plus the next
-  // window only for lanes whose run crosses it
   const uint64_t rbit0 = (hdr + 2 + enc) * 8;
-  const uint64_t bs = rbit0 + (uint64_t)start * rvs;
-  const uint64_t ra = (bs >> 3) & ~15ull;
-  uint64_t w0, w1, w2 = 0, w3 = 0;
-  ld_win(pg, ra, w0, w1);
-  const uint64_t last_bit = rbit0 + (uint64_t)end * rvs - ra * 8;  // exclusive, span-relative
-  if (last_bit > 128) ld_win(pg, ra + 16, w2, w3);
   const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
-  const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
   uint64_t found = 0;
   for (uint32_t pos = start; pos < end; pos++) {
-    const uint64_t b = rbit0 + (uint64_t)pos * rvs - ra * 8;
-    uint32_t rv;
-    if (b + rvs <= 256) {
-      const uint32_t j = (uint32_t)(b >> 6), sh = (uint32_t)(b & 63);
-      uint64_t v = pick4(j, w0, w1, w2, w3) >> sh;
-      if (sh + rvs > 64) v |= pick4(j + 1, w0, w1, w2, w3) << (64 - sh);
-      rv = (uint32_t)v & rvmask;
-    } else {
-      rv = ld_bits(pg, rbit0 + (uint64_t)pos * rvs, rvs);
-    }
-    if ((rv >> vs) == L.remainder) {
+    const uint32_t rv = ld_bits(pg, rbit0 + (uint64_t)pos * rvs, rvs);
+    if ((rv >> vs) == remainder) {
       const uint32_t v = rv & vmask;
       if (v < 64) found |= 1ull << v;
     }
@@ -1268,12 +1205,13 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
 }
 
 constexpr int PROBE_NT = 256;
+constexpr int PROBE_LDS_PAD = 24 * 1024;
 
-// STAGE: stage block heads through LDS cooperatively (step B) instead of per-lane loads.
-// Measured on MI355X (C2, 64M probes): per-lane 2.34 ms, staged 3.09 ms -- the kernel is
-// bound by random L2 line fetches (~3.5 per probe), not by load-instruction issue, so the
-// per-lane form (full occupancy, no barrier) is the default.
-template <int KIND, bool STAGE = false>
+// One lane per probe. (A cooperative variant that staged 128-byte block heads through LDS,
+// 8 lanes per block, measured slower on MI355X -- 3.09 vs 2.34 ms at C2 -- the kernel is
+// bound by random L2 line fetches, not load-instruction issue; it was removed.)
+// OCC_LDS > 0 pads LDS to cap workgroups per CU (occupancy experiments; 0 = none).
+template <int KIND, int OCC_LDS = 0>
 __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
                                                     const uint8_t* __restrict__ pages,
                                                     const uint4* __restrict__ precs,
@@ -1282,87 +1220,52 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
                                                     const uint32_t* __restrict__ filter_id, uint64_t n,
                                                     uint64_t* __restrict__ found, uint32_t fp_size,
                                                     uint32_t seed, uint32_t lis, uint32_t page_size,
-                                                    uint32_t num_filters, const FilterOut* __restrict__ outs,
-                                                    uint32_t ablate) {
-  __shared__ __attribute__((aligned(16))) v4u s_blk[STAGE ? PROBE_NT * 8 : 1];  // 128 B per probe
+                                                    uint32_t num_filters, uint32_t ablate) {
+  if constexpr (OCC_LDS > 0) {
+    __shared__ uint32_t s_pad[OCC_LDS / 4];
+    if (ablate == 0xdead) s_pad[threadIdx.x] = 0;  // keeps the pad allocated
+  }
   const uint64_t i = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
-  v4u* wbuf = s_blk + (threadIdx.x - lane) * 8;  // this wave's 64 x 128 B
-  bool live = i < n;
-  uint32_t fid = 0;
-  if (live) {
-    fid = __builtin_nontemporal_load(filter_id + i);
-    live = fid < num_filters && !(outs && outs[fid].error);  // unknown / failed filter: 0
-  }
-  ProbeLane L{};
-  uint4 rec = make_uint4(0, 0, 0, 0);
-  if (live) {
-    uint32_t h;
-    if constexpr (KIND == IN_KEYS24) {
-      const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) + i * 24);
-      const v2u a = __builtin_nontemporal_load(kp), b = __builtin_nontemporal_load(kp + 1),
-                c = __builtin_nontemporal_load(kp + 2);
-      uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-      h = xxh32_24(w, seed);
-    } else if constexpr (KIND == IN_KEYS_W) {
-      h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + i * key_len),
-                      key_len, seed);
-    } else if constexpr (KIND == IN_KEYS_B) {
-      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + i * key_len, key_len, seed);
-    } else if constexpr (KIND == IN_VAR) {
-      const uint64_t o0 = offs[i], o1 = offs[i + 1];
-      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
-    } else {
-      h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + i);
-    }
-    if (ablate == 1) {  // diagnostic: key stream + hash only
-      if (i < n) __builtin_nontemporal_store((uint64_t)h, found + i);
-      return;
-    }
-    L = probe_locate(pplans[fid], pages, precs, h, fp_size, lis, page_size, rec);
-    if (ablate == 2) {  // diagnostic: + index slot
-      __builtin_nontemporal_store(L.hdr, found + i);
-      return;
-    }
-  }
-  // (B) cooperative staging: instruction k moves probes 8k..8k+7, lane -> (probe, 16-B part)
-  if constexpr (STAGE) {
-    // byte offset (from `pages`) of the probe's 16-byte header window; ~0 = no probe
-    const uint64_t my_off = live ? (uint64_t)(L.pg - pages) + (L.hdr & ~15ull) : ~0ull;
-    const uint32_t lo32 = (uint32_t)my_off, hi32 = (uint32_t)(my_off >> 32);
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int p = 8 * k + (int)(lane >> 3);
-      const uint64_t off = (uint64_t)__shfl(lo32, p, WAVE) | ((uint64_t)__shfl(hi32, p, WAVE) << 32);
-      if (off != ~0ull) wbuf[p * 8 + (lane & 7)] = *reinterpret_cast<const v4u*>(pages + off + 16 * (lane & 7));
-    }
-    __syncthreads();
-  }
   if (i >= n) return;
-  if (!live) {
+  // the key (or hash) and the filter id are independent loads: issue them together
+  uint32_t h;
+  const uint32_t fid = __builtin_nontemporal_load(filter_id + i);
+  if constexpr (KIND == IN_KEYS24) {
+    const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) + i * 24);
+    const v2u a = __builtin_nontemporal_load(kp), b = __builtin_nontemporal_load(kp + 1),
+              c = __builtin_nontemporal_load(kp + 2);
+    uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    h = xxh32_24(w, seed);
+  } else if constexpr (KIND == IN_KEYS_W) {
+    h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + i * key_len),
+                    key_len, seed);
+  } else if constexpr (KIND == IN_KEYS_B) {
+    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + i * key_len, key_len, seed);
+  } else if constexpr (KIND == IN_VAR) {
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
+  } else {
+    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + i);
+  }
+  // unknown filter, or one whose build failed (k_layout sets pp.w): nothing found
+  const uint4 pp = fid < num_filters ? pplans[fid] : make_uint4(0, 0, 0, 1);
+  if (pp.w) {
     __builtin_nontemporal_store((uint64_t)0, found + i);
     return;
   }
-  if (!STAGE && ablate != 3 && !(rec.w & 0x80000000u)) {
-    uint64_t fr;
-    if (probe_rec(L, rec, lis, fr)) {
-      __builtin_nontemporal_store(fr, found + i);
-      return;
-    }
-  }
-  uint64_t W[16];
-  const v4u* src = STAGE ? wbuf + lane * 8 : reinterpret_cast<const v4u*>(L.pg + (L.hdr & ~15ull));
-#pragma unroll
-  for (int k = 0; k < 8; k++) {  // all 8 loads at once: one dependency level (a second,
-    const v4u v = src[k];        // conditional level measured 2x slower on MI355X)
-    W[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    W[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
-  }
-  if (ablate == 3) {  // diagnostic: + block head, no select / remainders
-    __builtin_nontemporal_store(W[0] ^ W[5] ^ W[11] ^ W[15], found + i);
+  if (ablate == 1) {  // diagnostic: key stream + hash only
+    __builtin_nontemporal_store((uint64_t)h, found + i);
     return;
   }
-  const uint64_t r = probe_finish(L, W, lis);
+  uint4 rec;
+  const ProbeLane L = probe_locate(pp, pages, precs, h, fp_size, lis, page_size, rec);
+  if (ablate == 2) {  // diagnostic: + probe record
+    __builtin_nontemporal_store(L.hdr ^ rec.y, found + i);
+    return;
+  }
+  uint64_t r;
+  if ((rec.w & 0x80000000u) || !probe_rec(L, rec, lis, r))
+    r = probe_stream(L.bo, L.remainder, L.vs, L.rvs, L.pg, L.hdr, lis);
   __builtin_nontemporal_store(r, found + i);
 }
 
@@ -1435,7 +1338,7 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
                   : launch_rest_t<uint32_t>(a, (uint32_t*)a.ent, (uint32_t*)a.part);
   if (rc) return rc;
   hipLaunchKernelGGL(k_layout, dim3(a.num_filters), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, a.plans, a.idx_cnt,
-                     a.idx_start, a.sorted32, a.first_old, a.has_old, a.slots, a.page_first, a.outs, a.lis, a.page_size);
+                     a.idx_start, a.sorted32, a.first_old, a.has_old, a.pplans_mut, a.slots, a.page_first, a.outs, a.lis, a.page_size);
   CHECK_LAUNCH();
   REC(EV_B_LAYOUT);
   hipLaunchKernelGGL(k_assemble, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans, a.pg_filter,
@@ -1478,13 +1381,24 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
   if (n == 0) return 0;
   dim3 g((uint32_t)((n + PROBE_NT - 1) / PROBE_NT)), b(PROBE_NT);
   REC(EV_P_START);
-  switch (kind) {
-    case IN_KEYS24: hipLaunchKernelGGL(k_probe<IN_KEYS24>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
-    case IN_KEYS_W: hipLaunchKernelGGL(k_probe<IN_KEYS_W>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
-    case IN_KEYS_B: hipLaunchKernelGGL(k_probe<IN_KEYS_B>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
-    case IN_VAR:    hipLaunchKernelGGL(k_probe<IN_VAR>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
-    default:        hipLaunchKernelGGL(k_probe<IN_HASH>, g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.outs, a.ablate); break;
+#define PK(K, L) hipLaunchKernelGGL((k_probe<K, L>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
+  if (kind == IN_KEYS24 && a.occ) {  // occupancy experiment variants (waves/SIMD cap)
+    const int o = a.occ;
+    if (o == 8) PK(IN_KEYS24, 0); else if (o == 6) PK(IN_KEYS24, 24 * 1024); else if (o == 5) PK(IN_KEYS24, 30 * 1024);
+    else if (o == 4) PK(IN_KEYS24, 38 * 1024); else if (o == 3) PK(IN_KEYS24, 50 * 1024);
+    else PK(IN_KEYS24, 70 * 1024);
+  } else {
+    // production: 24 KiB LDS pad = 6 workgroups (6 waves/SIMD) per CU; 8 waves measured
+    // 4 % slower (more outstanding random fetches thrash the XCD L2), 5 equal, 4 slower
+    switch (kind) {
+      case IN_KEYS24: PK(IN_KEYS24, PROBE_LDS_PAD); break;
+      case IN_KEYS_W: PK(IN_KEYS_W, PROBE_LDS_PAD); break;
+      case IN_KEYS_B: PK(IN_KEYS_B, PROBE_LDS_PAD); break;
+      case IN_VAR: PK(IN_VAR, PROBE_LDS_PAD); break;
+      default: PK(IN_HASH, PROBE_LDS_PAD); break;
+    }
   }
+#undef PK
   CHECK_LAUNCH();
   REC(EV_P_END);
   return 0;

@@ -59,7 +59,8 @@ struct LaunchArgs {
   int kind;
   int wide;  // 64-bit entries (old/new flag) -- only for incremental adds
   const FilterPlan* plans;
-  const uint4* pplans;  // packed probe plan per filter {vs|rem<<8|rvs<<16, page_base, idx_base, 0}
+  const uint4* pplans;  // packed probe plan per filter {vs|rem<<8|rvs<<16, page_base, idx_base, error}
+  uint4* pplans_mut;
   uint32_t num_filters;
   const uint32_t* tile_filter;
   const uint32_t* tile_start;
@@ -93,6 +94,7 @@ struct LaunchArgs {
   uint8_t* pages;
   FilterOut* outs;
   uint32_t ablate;  // probe diagnostics (0 = normal)
+  uint32_t occ;     // probe occupancy experiment (0 = normal)
   void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)
 };
 

@@ -1,5 +1,4 @@
-"""Diagnostic: time k_probe truncated after each step (hash / slot / block head / full),
-interleaved rounds in one process (cdna_hip_programming.md rule 24). C2 shape."""
+"""Diagnostic: k_probe at capped occupancy (waves/SIMD via LDS padding), interleaved."""
 import json
 import os
 import sys
@@ -23,14 +22,18 @@ b.set_timing(True)
 b.build_keys(keys, 24)
 torch.cuda.synchronize()
 L = E.load_library()
-res = {m: [] for m in (1, 2, 0)}
+ref = None
+modes = [8, 6, 5, 4, 3, 2]
+res = {m: [] for m in modes}
 for rnd in range(6):
-    for m in (1, 2, 0):
-        L.rf_amd_debug_probe_ablate(m)
+    for m in modes:
+        L.rf_amd_debug_probe_ablate(m << 8)
         b.probe_keys(keys, 24, fid, N, found)
         torch.cuda.synchronize()
         res[m].append(b.timings()["probe"])
+        if ref is None:
+            ref = found.clone()
+        else:
+            assert torch.equal(ref, found)
 L.rf_amd_debug_probe_ablate(0)
-out = {("hash", "record", "full")[i]: round(float(np.median(res[m][1:])), 4)
-       for i, m in enumerate((1, 2, 0))}
-print(json.dumps(out))
+print(json.dumps({f"occ{m}": round(float(np.median(v[1:])), 4) for m, v in res.items()}))
