@@ -161,8 +161,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
   // The tile is sorted by coarse bucket in LDS, then each bucket's run is written by
   // consecutive lanes: whole 64-byte granules instead of scattered 4-byte stores.
   __shared__ EntT s_stage[TILE_KEYS];
-  __shared__ uint32_t s_off[MAX_CB];
-  __shared__ uint32_t s_base[MAX_CB];
+  __shared__ uint32_t s_off[MAX_CB];  // local offsets, then (global base - local offset)
   __shared__ uint32_t s_tmp[SCAT_NT / WAVE + 1];
   constexpr int PER = TILE_KEYS / SCAT_NT;
   constexpr int BPT = MAX_CB / SCAT_NT;
@@ -209,12 +208,14 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
   }
   uint32_t valid_total;
   uint32_t run = block_excl_scan<SCAT_NT>(sum, s_tmp, &valid_total);
+  uint32_t gbase[BPT];
 #pragma unroll
   for (int k = 0; k < BPT; k++) {
     const uint32_t b = threadIdx.x * BPT + k;
+    gbase[k] = 0;
     if (b < num_cb) {
       s_off[b] = run;
-      if (cnt[k]) s_base[b] = atomicAdd(&cb_cursor[P.cb_base + b], cnt[k]) - run;
+      if (cnt[k]) gbase[k] = atomicAdd(&cb_cursor[P.cb_base + b], cnt[k]) - run;
       run += cnt[k];
     }
   }
@@ -224,10 +225,16 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
     if (cbv[k] != ~0u) s_stage[s_off[cbv[k]] + rank[k]] = v[k];
   }
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < BPT; k++) {
+    const uint32_t b = threadIdx.x * BPT + k;
+    if (b < num_cb) s_off[b] = gbase[k];
+  }
+  __syncthreads();
   EntT* dst = part + P.e_first;
   for (uint32_t j = threadIdx.x; j < valid_total; j += SCAT_NT) {
     const EntT x = s_stage[j];
-    dst[s_base[cb_of(x)] + j] = x;
+    dst[s_off[cb_of(x)] + j] = x;
   }
 }
 
@@ -610,9 +617,11 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = threadIdx.x * PER + k;
-    if (j <= n) s_excl[j] = run;  // j == n writes the total
+    if (j < n) s_excl[j] = run;
     run += sz[k];
   }
+  // the total at j == n: no thread owns it when n == MAX_INDICES
+  if (threadIdx.x == 0) s_excl[n] = total;
   __syncthreads();
   if (s_err) {
     if (threadIdx.x == 0) {

@@ -19,7 +19,7 @@ constexpr int TILE_NT = 256;
 constexpr int TILE_KEYS = 16384;  // keys per K1/K3 tile
 constexpr int SCAT_NT = 512;
 constexpr int SORT_NT = 512;
-constexpr int SORT_CAP = 12288;  // entries per coarse bucket held in LDS
+constexpr int SORT_CAP = 9216;   // entries per coarse bucket held in LDS (means 4096..8192, sd < 91)
 constexpr int BIG_NT = 1024;
 constexpr int BIG_GRID = 64;
 constexpr int LAYOUT_NT = 1024;
