@@ -1,0 +1,22 @@
+#!/bin/bash
+# One round's measurement evidence on the GPU box (run from the repo root via gpurun):
+#   1. PMC passes FETCH_SIZE and WRITE_SIZE, separately (MI355X_MICROARCH.md HBM section),
+#      summarised to per-launch HBM bytes per kernel;
+#   2. rocprofv3 --kernel-trace --stats of the default bench command;
+#   3. the bench lines (c2 with the CPU baseline, c3, c4) with roofline traffic from (1).
+# usage: bash tools/profile_round.sh <tag>      (outputs under gpurun_out/prof_<tag>/)
+set -o pipefail
+TAG=${1:-r01}
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/prof_$TAG
+mkdir -p $O
+BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pf -o c2 -- python3 $BENCH > $O/pf.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pw -o c2 -- python3 $BENCH > $O/pw.log 2>&1 || { echo "pmc write failed"; exit 1; }
+python3 profiles/pmc_summary.py $O/pf/c2_counter_collection.csv $O/pw/c2_counter_collection.csv $O/pmc_$TAG.json || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o c2 -- python3 $BENCH > $O/kt.log 2>&1 || { echo "kernel trace failed"; exit 1; }
+timeout -k 10 400 python3 bench.py --pmc $O/pmc_$TAG.json > $O/bench_c2.json 2> $O/bench_c2.err || { echo "bench c2 failed"; exit 1; }
+timeout -k 10 300 python3 bench.py --workload c3 --no-cpu-baseline --pmc none > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench c3 failed"; exit 1; }
+timeout -k 10 300 python3 bench.py --workload c4 --no-cpu-baseline --pmc none > $O/bench_c4.json 2> $O/bench_c4.err || { echo "bench c4 failed"; exit 1; }
+cat $O/bench_c2.json
