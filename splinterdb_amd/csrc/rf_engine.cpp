@@ -22,7 +22,7 @@ using namespace rf;
 extern "C" int rf_launch_build(const LaunchArgs* a);
 extern "C" int rf_launch_old_decode(const LaunchArgs* a, uint32_t f, uint32_t old_num_indices,
                                     uint32_t* d_cnt, uint32_t* d_pos);
-extern "C" int rf_launch_prec(const LaunchArgs* a);
+extern "C" int rf_launch_plines(const LaunchArgs* a);
 extern "C" int rf_launch_probe(const LaunchArgs* a, int kind, const void* in0, const uint64_t* offs,
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found);
 
@@ -73,9 +73,11 @@ struct rf_amd_batch {
   std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter, idx_filter;
   uint64_t E = 0, keys_total = 0;
   uint32_t CB = 0, I = 0, PS = 0, PF = 0;
+  uint64_t NL = 0;         // probe lines (64 B each)
+  uint32_t line_lmax = 0;  // max probe lines per index
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
-      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_precs, d_idx_filter;
+      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter;
   std::vector<uint32_t> old_num_indices;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing (rf_amd_batch_set_timing)
@@ -122,6 +124,19 @@ static int check_cfg(const rf_amd_config* cfg) {
 
 static uint32_t vsize_of(uint32_t value) { return value == 0 ? 0 : 32 - __builtin_clz(value); }
 
+// Probe-line group size (k_plines): the largest G = 2^g <= min(IS, 64) whose 64-byte line
+// (16-bit header + n + G encoding bits + n*rvs remainder bits) holds mean + 5 sd + 2
+// entries, n ~ Poisson(lam*G) with lam = fingerprints per bucket (< 2 by the choice of
+// log_num_buckets). Returns g + 1, or 0 = no lines (rvs > 32: probes walk the image).
+static uint32_t line_log_group(uint32_t lis, uint32_t rvs, double lam) {
+  if (rvs > 32) return 0;
+  for (int g = (int)(lis < 6 ? lis : 6); g >= 0; g--) {
+    const double G = (double)(1u << g), mean = lam * G;
+    if (mean + 5.0 * sqrt(mean) + 2.0 <= (512.0 - 16.0 - G) / (rvs + 1.0)) return (uint32_t)g + 1;
+  }
+  return 0;
+}
+
 extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t num_filters,
                                    const uint32_t* num_new, const uint16_t* value,
                                    rf_amd_batch* const* old_batch, const uint32_t* old_index,
@@ -140,6 +155,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   const uint32_t IS = 1u << lis;
   uint64_t e_first = 0, key_first = 0;
   uint32_t cb_base = 0, idx_base = 0, page_base = 0, pf_base = 0;
+  uint64_t line_base = 0;
   for (uint32_t f = 0; f < num_filters; f++) {
     FilterPlan& p = b->plans[f];
     memset(&p, 0, sizeof(p));
@@ -192,6 +208,12 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     p.page_cap = (uint32_t)cap;
     p.page_base = page_base;
     p.pf_base = pf_base;
+    p.lg_line = line_log_group(lis, p.rvs, (double)nfp / (double)(1ull << lnb));
+    p.line_base = (uint32_t)line_base;
+    if (p.lg_line) {
+      line_base += (uint64_t)p.num_indices << (lis - (p.lg_line - 1));
+      b->line_lmax = std::max(b->line_lmax, IS >> (p.lg_line - 1));
+    }
     if (op) {
       p.old_num_indices = op->num_indices;
       p.old_vs = op->vs;
@@ -225,6 +247,11 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   b->I = idx_base;
   b->PS = page_base;
   b->PF = pf_base;
+  if (line_base > 0xffffffffull) {
+    delete b;
+    return fail(RF_AMD_EINVAL, "batch too large (probe lines > 2^32)");
+  }
+  b->NL = line_base;
   const size_t esz = b->wide ? 8 : 4;
   int rc = 0;
   rc |= b->d_plans.alloc(sizeof(FilterPlan) * num_filters);
@@ -241,7 +268,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   rc |= b->d_idx_cnt.alloc(4 * b->I);
   rc |= b->d_idx_start.alloc(4 * b->I);
   rc |= b->d_slots.alloc(8 * b->I);
-  rc |= b->d_precs.alloc(16ull * b->I);
+  rc |= b->d_lines.alloc(64ull * b->NL + 64);
   rc |= b->d_idx_filter.alloc(4ull * b->I);
   rc |= b->d_page_first.alloc(4 * b->PF);
   rc |= b->d_pg_filter.alloc(4 * b->PS);
@@ -267,7 +294,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   std::vector<uint4> pp(num_filters);
   for (uint32_t f = 0; f < num_filters; f++) {
     const FilterPlan& q = b->plans[f];
-    pp[f] = make_uint4(q.vs | (q.rem << 8) | (q.rvs << 16), q.page_base, q.idx_base, 0);
+    pp[f] = make_uint4(q.vs | (q.rem << 8) | (q.rvs << 16) | (q.lg_line << 24), q.line_base, q.idx_base, 0);
   }
   UP(b->d_pplans, pp);
   UP(b->d_tile_filter, b->tile_filter);
@@ -326,7 +353,8 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.first_old = b->d_first_old.as<uint32_t>();
   a.has_old = b->d_has_old.as<uint32_t>();
   a.slots = b->d_slots.as<uint64_t>();
-  a.precs = b->d_precs.as<uint4>();
+  a.lines = b->d_lines.as<uint4>();
+  a.line_lmax = b->line_lmax;
   a.idx_filter = b->d_idx_filter.as<uint32_t>();
   a.num_idx = b->I;
   a.page_first = b->d_page_first.as<uint32_t>();
@@ -540,13 +568,18 @@ static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf
   p.rvs = p.rem + p.vs;
   p.num_indices = 1u << (lnb - lis);
   p.page_cap = img->info.num_pages;
+  p.lg_line = line_log_group(lis, p.rvs, (double)img->info.num_fingerprints / (double)(1ull << lnb));
   b->PS = img->info.num_pages;
   b->I = p.num_indices;
+  if (p.lg_line) {
+    b->NL = (uint64_t)p.num_indices << (lis - (p.lg_line - 1));
+    b->line_lmax = (1u << lis) >> (p.lg_line - 1);
+  }
   int rc = b->d_plans.alloc(sizeof(FilterPlan));
   rc |= b->d_pplans.alloc(16);
   rc |= b->d_pages.alloc((size_t)img->info.num_pages * cfg->page_size + 256);
   rc |= b->d_slots.alloc(8ull * p.num_indices);
-  rc |= b->d_precs.alloc(16ull * p.num_indices);
+  rc |= b->d_lines.alloc(64ull * b->NL + 64);
   rc |= b->d_idx_filter.alloc(4ull * p.num_indices);
   if (rc) {
     delete b;
@@ -559,11 +592,12 @@ static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf
                         hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(b->d_slots.p, img->slots, 8ull * p.num_indices, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(b->d_plans.p, &p, sizeof(p), hipMemcpyHostToDevice, st));
-  const uint4 pp1 = make_uint4(p.vs | (p.rem << 8) | (p.rvs << 16), 0, 0, 0);
+  const uint4 pp1 = make_uint4(p.vs | (p.rem << 8) | (p.rvs << 16) | (p.lg_line << 24), 0, 0, 0);
   HIPCHK(hipMemcpyAsync(b->d_pplans.p, &pp1, sizeof(pp1), hipMemcpyHostToDevice, st));
   {
     LaunchArgs a = make_args(b, st);
-    if (int lrc = rf_launch_prec(&a)) return fail(RF_AMD_EINVAL, std::string("prec launch: ") + hipGetErrorString((hipError_t)lrc));
+    if (int lrc = rf_launch_plines(&a))
+      return fail(RF_AMD_EINVAL, std::string("probe-line launch: ") + hipGetErrorString((hipError_t)lrc));
   }
   HIPCHK(hipStreamSynchronize(st));
   b->built = true;

@@ -19,7 +19,9 @@
 //                     written with 16-byte stores
 //   K0 k_old_*        incremental add: decode the old filter (:496-544) into entries
 //
-// Probe: k_probe, one lane per probe (routing_filter_lookup, :985-1073).
+// Probe lines: k_plines, one wave per index: device-only 64-byte lines per bucket group
+//                     cut from the image (see "probe lines" below)
+// Probe: k_probe, one lane per probe (routing_filter_lookup, :986-1073).
 //
 // The coarse bucket of an entry is its top `cbits` bits; K4 sorts the low bits, so the
 // result depends only on the multiset of entries, exactly like the reference's sort.
@@ -944,43 +946,11 @@ __device__ __forceinline__ uint64_t pick4(uint32_t j, uint64_t a, uint64_t b, ui
   return j == 0 ? a : (j == 1 ? b : (j == 2 ? c : d));
 }
 
-// Probe = routing_filter_lookup on a built image, given the key's 32-bit hash, in three
-// steps: (A) per lane: fingerprint -> index / bucket / remainder, index slot -> header
-// address; (B) per wave, cooperatively: the 128 bytes from each probe's header window are
-// staged in LDS, 8 lanes per probe (8 probes per 16-byte-per-lane load instruction, so a
-// wave touches ~100 cache lines instead of 512 for per-lane loads); (C) per lane: unary
-// select over the staged bits, then the bucket's packed remainders.
-struct ProbeLane {
-  uint32_t bo, remainder, vs, rvs;
-  const uint8_t* pg;  // the filter's page base
-  uint64_t hdr;       // header byte offset in pg
-};
-
-__device__ __forceinline__ ProbeLane probe_locate(const uint4 pp, const uint8_t* pages, const uint4* precs,
-                                                  uint32_t h, uint32_t fp_size, uint32_t lis,
-                                                  uint32_t page_size, uint4& rec) {
-  ProbeLane L;
-  L.vs = pp.x & 0xff;
-  const uint32_t rem = (pp.x >> 8) & 0xff;
-  L.rvs = (pp.x >> 16) & 0xff;
-  const uint32_t index_size = 1u << lis;
-  const uint32_t fp = h >> (32 - fp_size);
-  const uint32_t x = fp << L.vs;
-  L.bo = (L.rvs >= 32 ? 0u : x >> L.rvs) & (index_size - 1);
-  const uint32_t irvs = L.rvs + lis;
-  const uint32_t index = irvs >= 32 ? 0u : x >> irvs;
-  L.remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-  L.pg = pages + (uint64_t)pp.y * page_size;
-  rec = precs[pp.z + index];
-  // one 16-byte load: without this the compiler splits it into two 8-byte loads on either
-  // side of a branch (an extra dependent round trip: 1.60 -> 1.84 ms at C2)
-  asm volatile("" : "+v"(rec.x), "+v"(rec.y), "+v"(rec.z), "+v"(rec.w));
-  L.hdr = rec.x & ((1u << 26) - 1);
-  return L;
-}
-
-// Full-scan fallback (records flag c >= 4096, or the bucket runs past the record path's
-// 48-byte window): 128-bit windows streamed from the header, then per-entry bit reads.
+// Probe = routing_filter_lookup (src/routing_filter.c:986-1073) on a built image, given
+// the key's 32-bit hash. The common path reads one 64-byte probe line (below); the rare
+// rest (overflowed lines, filters without lines) walks the image itself via the index slot.
+// Full-scan fallback on the image (line overflowed, or the filter has no lines): 128-bit
+// windows streamed from the index header, then per-entry bit reads.
 // Kept lean (no large register arrays) so it does not cost the common path occupancy.
 __device__ __forceinline__ uint64_t probe_stream(uint32_t bo, uint32_t remainder, uint32_t vs, uint32_t rvs,
                                                  const uint8_t* pg, uint64_t hdr, uint32_t lis) {
@@ -1027,136 +997,146 @@ __device__ __forceinline__ uint64_t probe_stream(uint32_t bo, uint32_t remainder
   return found;
 }
 
-// ---- probe records --------------------------------------------------------------------
-// Device-only, 16 bytes per index (not part of the on-disk image): bits [0,26) relative
-// slot, [26,39) entry count c, then for k = 1..7 the first entry of bucket k*IS/8 (12 bits
-// each, [39+12(k-1), 51+12(k-1))), bit 127 = "use the full-scan path" (c >= 4096 or IS < 8).
-// A probe then reads the record (L2-resident, 256 KB per 16384-index filter) and only a
-// 48-byte window of the encoding starting at its sampled bucket.
-__device__ __forceinline__ uint32_t rec_bits(const uint4 r, uint32_t pos, uint32_t n) {
-  const uint32_t w = pos >> 5, sh = pos & 31;
-  const uint32_t a = w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
-  const uint32_t b = w == 0 ? r.y : (w == 1 ? r.z : (w == 2 ? r.w : 0u));
-  const uint64_t v = ((uint64_t)a | ((uint64_t)b << 32)) >> sh;
-  return (uint32_t)(v & ((1ull << n) - 1));
+// ---- probe lines ---------------------------------------------------------------------
+// Device-only, not part of the on-disk image. An index's block is cut into groups of
+// G = 2^(lg_line-1) consecutive buckets; group k of the filter (buckets [kG, kG+G)) gets a
+// 64-byte line at line_base + k:
+//   bits [0,16)        n = entries in the group, or 0x8000 = overflow (use the image)
+//   bits [16,16+n+G)   the group's slice of the unary encoding (0 = entry, 1 = bucket end)
+//   then n x rvs bits  the group's packed remainder|value entries (LSB-first)
+// Both slices are contiguous bit ranges of the reference block (layout written at
+// src/routing_filter.c:622-633), so a probe touches ONE random 64-byte line instead of the index slot,
+// header, encoding window and remainder run. G is chosen on the host so that overflow is a
+// > 5-sigma event for random fingerprints (engine: line_log_group).
+__device__ __forceinline__ uint64_t bits64_at(const uint8_t* pg, uint64_t bitpos) {
+  const uint64_t by = bitpos >> 3;
+  const uint32_t sh = (uint32_t)(bitpos & 7);
+  uint64_t x = ld_u64_unaligned(pg, by) >> sh;
+  if (sh) x |= (uint64_t)pg[by + 8] << (64 - sh);
+  return x;
 }
-__device__ __forceinline__ void rec_put(uint32_t (&r)[4], uint32_t pos, uint32_t n, uint32_t val) {
-  const uint64_t v = (uint64_t)(val & ((1u << n) - 1)) << (pos & 31);
-  const uint32_t w = pos >> 5;
-  r[w] |= (uint32_t)v;
-  if (w < 3) r[w + 1] |= (uint32_t)(v >> 32);
-}
+__device__ __forceinline__ uint64_t lowmask64(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
 
-// one wave per index: popcount prefix over the unary encoding -> bucket starts at k*IS/8
-__global__ __launch_bounds__(256) void k_prec(const FilterPlan* __restrict__ plans,
-                                              const uint32_t* __restrict__ idx_filter,
-                                              const uint64_t* __restrict__ slots,
-                                              const uint8_t* __restrict__ pages,
-                                              const FilterOut* __restrict__ outs,
-                                              uint4* __restrict__ precs, uint32_t num_idx,
-                                              uint32_t lis, uint32_t page_size) {
-  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
-  if (g >= num_idx) return;
-  const uint32_t f = idx_filter[g];
+// One wave per index (4 per workgroup). Phase 1: popcount-prefix over the encoding, the
+// position after each group's last bucket terminator -> LDS. Phase 2: 4 lanes per line,
+// 16 bytes each, bit-copied from the image.
+__global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ plans,
+                                                const uint32_t* __restrict__ idx_filter,
+                                                const uint64_t* __restrict__ slots,
+                                                const uint8_t* __restrict__ pages,
+                                                const FilterOut* __restrict__ outs,
+                                                uint4* __restrict__ lines, uint32_t num_idx,
+                                                uint32_t lmax, uint32_t lis, uint32_t page_size) {
+  extern __shared__ uint32_t s_dyn[];
+  const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const uint32_t g = blockIdx.x * (blockDim.x / WAVE) + wv;
+  uint32_t* s_a = s_dyn + wv * (lmax + 1);
+  const uint32_t f = g < num_idx ? idx_filter[g] : 0u;
   const FilterPlan& P = plans[f];
-  if (outs && (outs[f].error || g - P.idx_base >= P.num_indices)) return;
-  const uint32_t IS = 1u << lis, S = IS / 8;
-  const uint64_t rel = slots[g];
+  const bool active = g < num_idx && P.lg_line != 0 && !(outs && outs[f].error) &&
+                      g - P.idx_base < P.num_indices;
+  const uint32_t IS = 1u << lis;
+  const uint32_t lgG = active ? P.lg_line - 1 : 0u, G = 1u << lgG, L = IS >> lgG;
   const uint8_t* pg = pages + (uint64_t)P.page_base * page_size;
-  const uint32_t c = (uint32_t)pg[rel] | ((uint32_t)pg[rel + 1] << 8);
-  uint32_t r[4] = {0, 0, 0, 0};
-  rec_put(r, 0, 26, (uint32_t)rel);
-  rec_put(r, 26, 13, c);
-  if (c >= 4096 || S == 0) {
-    r[3] |= 0x80000000u;
-  } else {
+  uint64_t rel = 0;
+  uint32_t c = 0;
+  if (active) {
+    rel = slots[g];
+    c = (uint32_t)pg[rel] | ((uint32_t)pg[rel + 1] << 8);
     const uint64_t ebit = (rel + 2) * 8;
     const uint32_t nbits = c + IS;
+    if (lane == 0) { s_a[0] = 0; s_a[L] = nbits; }
     uint32_t ones_before = 0;
     for (uint32_t base = 0; base < nbits; base += 64 * WAVE) {
       const uint32_t b0 = base + lane * 64;
       uint64_t x = 0;
       if (b0 < nbits) {
-        const uint64_t bp = ebit + b0;
-        const uint32_t sh = (uint32_t)(bp & 7);
-        x = ld_u64_unaligned(pg, bp >> 3) >> sh;
-        if (sh) x |= (uint64_t)pg[(bp >> 3) + 8] << (64 - sh);
+        x = bits64_at(pg, ebit + b0);
         const uint32_t nb = min(64u, nbits - b0);
-        if (nb < 64) x &= (1ull << nb) - 1;
+        x &= lowmask64(nb);
       }
       const uint32_t ones = __popcll(x);
       const uint32_t ex = wave_incl_scan(ones) - ones + ones_before;
-      for (uint32_t k = 1; k < 8; k++) {
-        const uint32_t t = k * S - 1;  // terminator of bucket k*S - 1
-        if (t >= ex && t < ex + ones) {
-          const uint32_t pos = b0 + select64_fast(x, t - ex);
-          rec_put(r, 39 + 12 * (k - 1), 12, pos - t);  // zeros before it = first entry of bucket k*S
-        }
-      }
+      // terminators t = kG - 1 (k = 1..L-1) inside [ex, ex + ones): group k starts after t
+      for (uint32_t k = (ex + G) >> lgG; k < L && k * G - 1 < ex + ones; k++)
+        s_a[k] = b0 + select64_fast(x, k * G - 1 - ex) + 1;
       ones_before = __shfl(ex + ones, WAVE - 1, WAVE);
     }
   }
+  __syncthreads();
+  if (!active) return;
+  const uint32_t rvs = P.rvs;
+  const uint64_t ebit = (rel + 2) * 8;
+  const uint32_t enc = (c + IS - 1) / 8 + 4;
+  const uint64_t rbit0 = (rel + 2 + enc) * 8;
+  const uint64_t line0 = (uint64_t)P.line_base + (uint64_t)(g - P.idx_base) * L;
+  for (uint32_t u = lane; u < 4 * L; u += WAVE) {
+    const uint32_t gl = u >> 2, qq = u & 3;
+    const uint32_t a = s_a[gl], ne = s_a[gl + 1] - a;  // encoding bits of the group = n + G
+    const uint32_t n = ne - G, E = a - gl * G;         // entries, first entry of the group
+    const uint32_t R0 = 16 + ne, tot = R0 + n * rvs;
+    const bool ovf = tot > 512;
+    uint64_t w[2];
 #pragma unroll
-  for (int w = 0; w < 4; w++) {
-    uint32_t v = r[w];
-    for (int d = 1; d < WAVE; d <<= 1) v |= __shfl_xor(v, d, WAVE);
-    r[w] = v;
+    for (int h = 0; h < 2; h++) {
+      const uint32_t o = qq * 128 + h * 64;
+      uint64_t x = (o == 0) ? (ovf ? 0x8000ull : (uint64_t)n) : 0ull;
+      if (!ovf) {
+        uint32_t lo = max(o, 16u), hi = min(o + 64, R0);
+        if (lo < hi) x |= (bits64_at(pg, ebit + a + (lo - 16)) & lowmask64(hi - lo)) << (lo - o);
+        lo = max(o, R0);
+        hi = min(o + 64, tot);
+        if (lo < hi)
+          x |= (bits64_at(pg, rbit0 + (uint64_t)E * rvs + (lo - R0)) & lowmask64(hi - lo)) << (lo - o);
+      }
+      w[h] = x;
+    }
+    lines[(line0 + gl) * 4 + qq] =
+        make_uint4((uint32_t)w[0], (uint32_t)(w[0] >> 32), (uint32_t)w[1], (uint32_t)(w[1] >> 32));
   }
-  if (lane == 0) precs[g] = make_uint4(r[0], r[1], r[2], r[3]);
 }
 
-
-// Record-guided probe: returns false when the lane must take the full-scan path.
-__device__ __forceinline__ bool probe_rec(const ProbeLane& L, const uint4 rec, uint32_t lis, uint64_t& found) {
-  const uint32_t IS = 1u << lis, S = IS / 8;
-  const uint32_t bo = L.bo, vs = L.vs, rvs = L.rvs;
-  const uint8_t* pg = L.pg;
-  const uint64_t hdr = L.hdr;
-  const uint32_t c = rec_bits(rec, 26, 13);
-  const uint32_t s = bo / S, K = s * S;
-  const uint32_t zs = s ? rec_bits(rec, 39 + 12 * (s - 1), 12) : 0u;
-  const uint64_t ebit = (hdr + 2) * 8;
-  const uint64_t A = ebit + K + zs;            // first bit of bucket K
-  const uint64_t a16 = (A >> 3) & ~15ull;
-  uint64_t W[6];
+// Line probe: bucket j of the line's group; returns false on an overflowed line.
+__device__ __forceinline__ bool probe_line(const uint4* __restrict__ lines, uint64_t line, uint32_t j,
+                                           uint32_t G, uint32_t remainder, uint32_t vs, uint32_t rvs,
+                                           uint64_t& found) {
+  uint64_t W[8];
   {
-    const v4u* q = reinterpret_cast<const v4u*>(pg + a16);
+    const v4u* q = reinterpret_cast<const v4u*>(lines + line * 4);
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < 4; k++) {
       const v4u v = q[k];
       W[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
       W[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
     }
   }
-  const uint32_t d = (uint32_t)(A - a16 * 8);  // < 136
-  // ranks (from bucket K's terminator, 1-bit #K) of 1-bits #(bo-1) and #bo
-  const uint32_t r2 = bo - K;
-  const uint32_t r1 = r2 ? r2 - 1 : 0;
-  uint32_t j1 = 6, j2 = 6, c1 = 0, cum = 0;
+  const uint32_t hdr = (uint32_t)W[0] & 0xffffu;
+  if (hdr & 0x8000u) return false;
+  const uint32_t n = hdr;
+  W[0] &= ~0xffffull;
+  // line positions of bucket terminators #(j-1) and #j (ranks among the line's 1-bits; the
+  // first G of them are the group's terminators, so remainder bits never interfere)
+  const uint32_t r2 = j, r1 = j ? j - 1 : 0;
+  uint32_t j1 = 8, j2 = 8, c1 = 0, cum = 0;
 #pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const uint32_t wb = 64u * k;
-    uint64_t x = W[k];
-    if (wb + 64 <= d) x = 0;
-    else if (wb < d) x = (x >> (d - wb)) << (d - wb);
-    W[k] = x;
-    const uint32_t pc = __popcll(x);
-    const bool h1 = (j1 == 6) && (cum + pc > r1);
-    const bool h2 = (j2 == 6) && (cum + pc > r2);
+  for (int k = 0; k < 8; k++) {
+    const uint32_t pc = __popcll(W[k]);
+    const bool h1 = (j1 == 8) && (cum + pc > r1);
+    const bool h2 = (j2 == 8) && (cum + pc > r2);
     c1 = h1 ? cum : c1;
     j1 = h1 ? (uint32_t)k : j1;
     j2 = h2 ? (uint32_t)k : j2;
     cum += pc;
   }
-  if (j2 == 6) return false;  // bucket runs past the 48-byte window
-  auto pick6 = [&](uint32_t j) {
+  auto pick8 = [&](uint32_t i) {
     uint64_t r = 0;
 #pragma unroll
-    for (int k = 0; k < 6; k++) r |= W[k] & (0ull - (uint64_t)(j == (uint32_t)k));
+    for (int k = 0; k < 8; k++) r |= W[k] & (0ull - (uint64_t)(i == (uint32_t)k));
     return r;
   };
-  const uint64_t x1 = pick6(j1);
+  found = 0;
+  if (j2 == 8) return true;  // corrupt line: never read out of range
+  const uint64_t x1 = pick8(j1);
   const uint32_t q1 = 64u * j1 + select64_fast(x1, r1 - c1);
   uint32_t q2;
   if (r2 == 0) {
@@ -1166,40 +1146,23 @@ __device__ __forceinline__ bool probe_rec(const ProbeLane& L, const uint4 rec, u
     const uint64_t rest = b1 == 63 ? 0ull : (x1 & (~0ull << (b1 + 1)));
     q2 = 64u * j1 + (uint32_t)__builtin_ctzll(rest);
   } else {
-    q2 = 64u * j2 + (uint32_t)__builtin_ctzll(pick6(j2));
+    q2 = 64u * j2 + (uint32_t)__builtin_ctzll(pick8(j2));
   }
-  // encoding-relative positions
-  const uint32_t rel0 = (uint32_t)(a16 * 8 - ebit);  // may wrap (negative): modular arithmetic
-  const uint32_t start = r2 ? (rel0 + q1) + 1 - bo : zs;
-  const uint32_t end = (rel0 + q2) - bo;
-  found = 0;
-  if (start >= end) return true;
-  // a speculative remainder load issued beside the encoding window (position estimated
-  // from the record) measured slower: +14 VGPRs cost a wave per SIMD (1.60 -> 1.88 ms)
-  const uint32_t enc = (c + IS - 1) / 8 + 4;
-  const uint64_t rbit0 = (hdr + 2 + enc) * 8;
-  const uint64_t bs = rbit0 + (uint64_t)start * rvs;
-  const uint64_t ra = (bs >> 3) & ~15ull;
-  uint64_t w0, w1, w2 = 0, w3 = 0;
-  ld_win(pg, ra, w0, w1);
-  const uint64_t last_bit = rbit0 + (uint64_t)end * rvs - ra * 8;
-  if (last_bit > 128) ld_win(pg, ra + 16, w2, w3);
+  const uint32_t start = j ? q1 - 15 - j : 0u;  // zeros before terminator j-1
+  const uint32_t end = q2 - 16 - j;             // zeros before terminator j
+  const uint32_t R0 = 16 + n + G;
   const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
   const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
   for (uint32_t pos = start; pos < end; pos++) {
-    const uint64_t bb = rbit0 + (uint64_t)pos * rvs - ra * 8;
-    uint32_t rv;
-    if (bb + rvs <= 256) {
-      const uint32_t j = (uint32_t)(bb >> 6), sh = (uint32_t)(bb & 63);
-      uint64_t v = pick4(j, w0, w1, w2, w3) >> sh;
-      if (sh + rvs > 64) v |= pick4(j + 1, w0, w1, w2, w3) << (64 - sh);
-      rv = (uint32_t)v & rvmask;
-    } else {
-      rv = ld_bits(pg, rbit0 + (uint64_t)pos * rvs, rvs);
-    }
-    if ((rv >> vs) == L.remainder) {
-      const uint32_t v = rv & vmask;
-      if (v < 64) found |= 1ull << v;
+    const uint32_t bb = R0 + pos * rvs;
+    if (bb + rvs > 512) break;  // corrupt line
+    const uint32_t wi = bb >> 6, sh = bb & 63;
+    uint64_t v = pick8(wi) >> sh;
+    if (sh + rvs > 64) v |= pick8(wi + 1) << (64 - sh);
+    const uint32_t rv = (uint32_t)v & rvmask;
+    if ((rv >> vs) == remainder) {
+      const uint32_t val = rv & vmask;
+      if (val < 64) found |= 1ull << val;
     }
   }
   return true;
@@ -1222,8 +1185,10 @@ constexpr int PROBE_LDS_PAD = 24 * 1024;
 // OCC_LDS > 0 pads LDS to cap workgroups per CU (occupancy experiments; 0 = none).
 template <int KIND, int OCC_LDS = 0>
 __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
+                                                    const FilterPlan* __restrict__ plans,
                                                     const uint8_t* __restrict__ pages,
-                                                    const uint4* __restrict__ precs,
+                                                    const uint64_t* __restrict__ slots,
+                                                    const uint4* __restrict__ lines,
                                                     const void* __restrict__ in0,
                                                     const uint64_t* __restrict__ offs, uint32_t key_len,
                                                     const uint32_t* __restrict__ filter_id, uint64_t n,
@@ -1266,15 +1231,28 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     __builtin_nontemporal_store((uint64_t)h, found + i);
     return;
   }
-  uint4 rec;
-  const ProbeLane L = probe_locate(pp, pages, precs, h, fp_size, lis, page_size, rec);
-  if (ablate == 2) {  // diagnostic: + probe record
-    __builtin_nontemporal_store(L.hdr ^ rec.y, found + i);
-    return;
+  const uint32_t vs = pp.x & 0xff, rem = (pp.x >> 8) & 0xff, rvs = (pp.x >> 16) & 0xff, lgl = pp.x >> 24;
+  const uint32_t fp = h >> (32 - fp_size);
+  const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;  // index << lis | bucket in index
+  const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+  uint64_t r = 0;
+  if (lgl) {
+    const uint32_t lgG = lgl - 1;
+    const uint64_t line = (uint64_t)pp.y + (bucket >> lgG);
+    if (ablate == 2) {  // diagnostic: + the line's first 16 bytes
+      __builtin_nontemporal_store((uint64_t)lines[line * 4].x ^ h, found + i);
+      return;
+    }
+    if (probe_line(lines, line, bucket & ((1u << lgG) - 1), 1u << lgG, remainder, vs, rvs, r)) {
+      __builtin_nontemporal_store(r, found + i);
+      return;
+    }
   }
-  uint64_t r;
-  if ((rec.w & 0x80000000u) || !probe_rec(L, rec, lis, r))
-    r = probe_stream(L.bo, L.remainder, L.vs, L.rvs, L.pg, L.hdr, lis);
+  // overflowed line (or no lines): walk the image from the index slot
+  const uint32_t index = bucket >> lis;
+  const uint64_t hdr = slots[pp.z + index];
+  const uint8_t* pg = pages + (uint64_t)plans[fid].page_base * page_size;
+  r = probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, pg, hdr, lis);
   __builtin_nontemporal_store(r, found + i);
 }
 
@@ -1324,6 +1302,8 @@ static int launch_rest_t(const LaunchArgs& a, EntT* ent, EntT* part) {
   return 0;
 }
 
+extern "C" int rf_launch_plines(const LaunchArgs* pa);
+
 extern "C" int rf_launch_build(const LaunchArgs* pa) {
   const LaunchArgs& a = *pa;
   if (a.wide) {
@@ -1354,17 +1334,18 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
                      a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages, a.lis,
                      a.page_size);
   CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_prec, dim3((a.num_idx + 3) / 4), dim3(256), 0, (hipStream_t)a.stream, a.plans,
-                     a.idx_filter, a.slots, a.pages, a.outs, a.precs, a.num_idx, a.lis, a.page_size);
-  CHECK_LAUNCH();
+  if (int rc = rf_launch_plines(&a)) return rc;
   REC(EV_B_ASSEMBLE);
   return 0;
 }
 
-extern "C" int rf_launch_prec(const LaunchArgs* pa) {
+extern "C" int rf_launch_plines(const LaunchArgs* pa) {
   const LaunchArgs& a = *pa;
-  hipLaunchKernelGGL(k_prec, dim3((a.num_idx + 3) / 4), dim3(256), 0, (hipStream_t)a.stream, a.plans,
-                     a.idx_filter, a.slots, a.pages, a.outs, a.precs, a.num_idx, a.lis, a.page_size);
+  if (!a.line_lmax) return 0;  // no filter of the batch has lines
+  const size_t lds = 4ull * (256 / WAVE) * (a.line_lmax + 1);
+  hipLaunchKernelGGL(k_plines, dim3((a.num_idx + 3) / 4), dim3(256), lds, (hipStream_t)a.stream, a.plans,
+                     a.idx_filter, a.slots, a.pages, a.outs, a.lines, a.num_idx, a.line_lmax, a.lis,
+                     a.page_size);
   CHECK_LAUNCH();
   return 0;
 }
@@ -1390,7 +1371,7 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
   if (n == 0) return 0;
   dim3 g((uint32_t)((n + PROBE_NT - 1) / PROBE_NT)), b(PROBE_NT);
   REC(EV_P_START);
-#define PK(K, L) hipLaunchKernelGGL((k_probe<K, L>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.pages, a.precs, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
+#define PK(K, L) hipLaunchKernelGGL((k_probe<K, L>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
   if (kind == IN_KEYS24 && a.occ) {  // occupancy experiment variants (waves/SIMD cap)
     const int o = a.occ;
     if (o == 8) PK(IN_KEYS24, 0); else if (o == 6) PK(IN_KEYS24, 24 * 1024); else if (o == 5) PK(IN_KEYS24, 30 * 1024);

@@ -41,6 +41,8 @@ struct FilterPlan {
   uint32_t num_indices;
   uint32_t cbits, bbits;  // coarse-bucket bits, bucket-in-coarse-bucket bits (sum = lnb)
   uint32_t cb_base, idx_base, page_base, page_cap, pf_base;
+  // probe lines (device-only, 64 B per group of 2^(lg_line-1) buckets; lg_line 0 = none)
+  uint32_t lg_line, line_base;
   // old filter (incremental add)
   uint32_t old_num_indices, old_vs, old_rvs, npo;  // npo = new indices per old index
   const uint8_t* old_pages;
@@ -59,7 +61,7 @@ struct LaunchArgs {
   int kind;
   int wide;  // 64-bit entries (old/new flag) -- only for incremental adds
   const FilterPlan* plans;
-  const uint4* pplans;  // packed probe plan per filter {vs|rem<<8|rvs<<16, page_base, idx_base, error}
+  const uint4* pplans;  // packed probe plan per filter {vs|rem<<8|rvs<<16|lg_line<<24, line_base, idx_base, error}
   uint4* pplans_mut;
   uint32_t num_filters;
   const uint32_t* tile_filter;
@@ -85,7 +87,8 @@ struct LaunchArgs {
   uint32_t* first_old;  // wide mode: per index, smallest old entry (valid if has_old)
   uint32_t* has_old;
   uint64_t* slots;
-  uint4* precs;             // device-only probe records, one per index
+  uint4* lines;             // device-only probe lines (64 B = 4 x uint4 each)
+  uint32_t line_lmax;       // max lines per index over the batch (k_plines LDS sizing)
   const uint32_t* idx_filter;
   uint32_t num_idx;
   uint32_t* page_first;

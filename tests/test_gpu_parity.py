@@ -277,6 +277,44 @@ def test_var_keys_zipf_probe(oracle):
     assert (got[:P] & np.uint64(1)).all() and lens.min() >= 8
 
 
+def test_probe_line_overflow_falls_back_to_image(oracle):
+    """Clustered fingerprints overflow some 64-byte probe lines; those probes take the
+    full-scan path on the image. Every probe must still equal the oracle's lookup."""
+    rng = np.random.default_rng(11)
+    for lis, fps, value, n in ((8, 26, 0, 200000), (10, 28, 5, 150000), (6, 24, 1, 70000)):
+        cfg = E.routing_config_init(fingerprint_size=fps, log_index_size=lis)
+        ocfg = oracle.make_config(fingerprint_size=fps, log_index_size=lis)
+        lnb = max(int(n).bit_length() - 1, lis)
+        rem = fps - lnb
+        sh = 32 - fps  # hash -> fingerprint shift
+        h = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+        # 8 clusters of 150 distinct fingerprints in 4 adjacent buckets each
+        k = 0
+        for c in range(8):
+            b0 = int(rng.integers(0, (1 << lnb) - 4))
+            for j in range(150):
+                fp = ((b0 + j % 4) << rem) | (j * 7919 % (1 << rem))
+                h[k] = np.uint32((fp << sh) | (j & ((1 << sh) - 1)))
+                k += 1
+        b = E.FilterBatch(cfg, [n], [value])
+        b.build_hashes(dev(h))
+        img = b.image(0)
+        of = oracle.filter_add(ocfg, h, value=value)
+        assert (img.num_unique, img.num_pages) == (of.num_unique, of.num_pages), lis
+        assert (img.pages == of.pages()).all(), lis
+        P = 300000
+        ph = rng.integers(0, 1 << 32, size=P, dtype=np.uint64).astype(np.uint32)
+        ph[: P // 3] = h[rng.integers(0, n, size=P // 3)]
+        ph[P // 3: P // 3 + k] = h[:k] ^ np.uint32(1 << sh)  # same buckets, other remainders
+        found = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+        b.probe_hashes(dev(ph), torch.zeros(P, dtype=torch.int32, device="cuda:0"), P, found)
+        torch.cuda.synchronize()
+        got = found.cpu().numpy().view(np.uint64)
+        want = of.lookup_hashes(ph)
+        assert (got == want).all(), (lis, int((got != want).sum()))
+        assert (got[: P // 3] >> np.uint64(value) & np.uint64(1)).all()
+
+
 def test_errors_match_reference_contract():
     cfg = E.routing_config_init()
     with pytest.raises(E.PlatformStatusError) as ei:
