@@ -111,12 +111,13 @@ uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
 
 /* per-stage timing with HIP events recorded on the launch stream. Stages of the last
  * build: 0 hash+histogram, 1 bucket scan, 2 scatter, 3 bucket sort, 4 big-bucket sort,
- * 5 layout, 6 page assembly, 7 whole build; 8 = last probe kernel. Milliseconds, -1 if a
- * stage did not run. */
+ * 5 layout, 6 page assembly + probe lines, 7 whole build; 8 = last probe kernel.
+ * Milliseconds, -1 if a stage did not run. */
 #define RF_AMD_NUM_TIMINGS 9
 int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
-/* diagnostics: truncate later probes after 1 = hashing, 2 = the probe-record load
- * (results are then NOT found_values); 0 restores normal probes */
+/* diagnostics: truncate later probes after 1 = hashing, 2 = the probe-line load
+ * (results are then NOT found_values); 0 restores normal probes. Bits 8+: cap the probe
+ * kernel at that many waves per SIMD (occupancy experiments). */
 void rf_amd_debug_probe_ablate(uint32_t mode);
 int rf_amd_batch_timings(rf_amd_batch *b, float *ms, uint32_t n);
 

@@ -77,7 +77,7 @@ struct rf_amd_batch {
   uint32_t line_lmax = 0;  // max probe lines per index
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
-      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter;
+      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill;
   std::vector<uint32_t> old_num_indices;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing (rf_amd_batch_set_timing)
@@ -125,14 +125,24 @@ static int check_cfg(const rf_amd_config* cfg) {
 static uint32_t vsize_of(uint32_t value) { return value == 0 ? 0 : 32 - __builtin_clz(value); }
 
 // Probe-line group size (k_plines): the largest G = 2^g <= min(IS, 64) whose 64-byte line
-// (16-bit header + n + G encoding bits + n*rvs remainder bits) holds mean + 5 sd + 2
+// (16-bit header + n + G encoding bits + n*rvs remainder bits) holds mean + SIGMA sd + 2
 // entries, n ~ Poisson(lam*G) with lam = fingerprints per bucket (< 2 by the choice of
-// log_num_buckets). Returns g + 1, or 0 = no lines (rvs > 32: probes walk the image).
+// log_num_buckets). Larger G = smaller line table (L2-resident sooner) but more overflowed
+// lines (those probes walk the image). SIGMA: RF_AMD_LINE_SIGMA (tuning knob), default 3.5
+// (lam is an upper bound: at C2 the real overflow margin is 4.5 sd; sigma 5 vs 3 measured
+// the same probe time, so the smaller table wins).
+// Returns g + 1, or 0 = no lines (rvs > 32: probes walk the image).
+static double line_sigma() {
+  const char* e = getenv("RF_AMD_LINE_SIGMA");
+  const double v = e ? atof(e) : 0.0;
+  return v > 0.0 ? v : 3.5;
+}
 static uint32_t line_log_group(uint32_t lis, uint32_t rvs, double lam) {
   if (rvs > 32) return 0;
+  const double sg = line_sigma();
   for (int g = (int)(lis < 6 ? lis : 6); g >= 0; g--) {
     const double G = (double)(1u << g), mean = lam * G;
-    if (mean + 5.0 * sqrt(mean) + 2.0 <= (512.0 - 16.0 - G) / (rvs + 1.0)) return (uint32_t)g + 1;
+    if (mean + sg * sqrt(mean) + 2.0 <= (512.0 - 16.0 - G) / (rvs + 1.0)) return (uint32_t)g + 1;
   }
   return 0;
 }
@@ -241,6 +251,15 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     page_base += p.page_cap;
     pf_base += p.page_cap + 1;
   }
+  if (!b->wide) {
+    // fresh build: the fused kernel partitions straight into SORT_CAP slots per coarse
+    // bucket (k_hash_scatter), so each filter's entry region is its buckets' regions
+    e_first = 0;
+    for (auto& p : b->plans) {
+      p.e_first = e_first;
+      e_first += (uint64_t)SORT_CAP << p.cbits;
+    }
+  }
   b->E = e_first;
   b->keys_total = key_first;
   b->CB = cb_base;
@@ -265,6 +284,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   rc |= b->d_cb_cursor.alloc(4 * b->CB);
   rc |= b->d_cb_filter.alloc(4 * b->CB);
   rc |= b->d_overflow.alloc(4 * (b->CB + 1));
+  rc |= b->d_spill.alloc(4);
   rc |= b->d_idx_cnt.alloc(4 * b->I);
   rc |= b->d_idx_start.alloc(4 * b->I);
   rc |= b->d_slots.alloc(8 * b->I);
@@ -348,6 +368,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.cb_filter = b->d_cb_filter.as<uint32_t>();
   a.num_cb = b->CB;
   a.overflow = b->d_overflow.as<uint32_t>();
+  a.spill = b->d_spill.p ? b->d_spill.as<uint32_t>() : nullptr;
   a.idx_cnt = b->d_idx_cnt.as<uint32_t>();
   a.idx_start = b->d_idx_start.as<uint32_t>();
   a.first_old = b->d_first_old.as<uint32_t>();
@@ -372,6 +393,7 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   if (b->keys_total && !in0) return fail(RF_AMD_EINVAL, "null input");
   HIPCHK(hipSetDevice(b->eng->device));
   hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  (void)hipGetLastError();  // launch checks below must see only their own errors
   LaunchArgs a = make_args(b, st);
   a.kind = kind;
   a.in0 = in0;
@@ -381,6 +403,10 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   HIPCHK(hipMemsetAsync(b->d_cb_count.p, 0, 4 * (size_t)b->CB, st));
   HIPCHK(hipMemsetAsync(b->d_outs.p, 0, sizeof(FilterOut) * b->F, st));
   HIPCHK(hipMemsetAsync(b->d_overflow.p, 0, 4, st));
+  if (!b->wide) {
+    HIPCHK(hipMemsetAsync(b->d_cb_cursor.p, 0, 4 * (size_t)b->CB, st));
+    HIPCHK(hipMemsetAsync(b->d_spill.p, 0, 4, st));
+  }
   if (b->wide) {
     HIPCHK(hipMemsetAsync(b->d_ent.p, 0xff, b->d_ent.n, st));
     for (uint32_t f = 0; f < b->F; f++) {
@@ -422,6 +448,7 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   if (n && (!in0 || !fid || !found)) return fail(RF_AMD_EINVAL, "null probe buffer");
   HIPCHK(hipSetDevice(b->eng->device));
   hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  (void)hipGetLastError();
   LaunchArgs a = make_args(b, st);
   a.ablate = g_probe_ablate & 0xff;
   a.occ = g_probe_ablate >> 8;
@@ -475,6 +502,7 @@ extern "C" int rf_amd_batch_timings(rf_amd_batch* b, float* ms, uint32_t n) {
     float t = 0;
     if (hipEventElapsedTime(&t, b->events[pairs[i][0]], b->events[pairs[i][1]]) == hipSuccess) ms[i] = t;
   }
+  (void)hipGetLastError();  // a stage not run yet (e.g. no probe) must not poison later launches
   return 0;
 }
 

@@ -33,6 +33,42 @@
 
 using namespace rf;
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+// XXH32 of input k (btree_pack / routing_filter_lookup hashing, src/btree.c:4020-4024,
+// src/routing_filter.c:1004-1005). NT = non-temporal streaming loads (probe key stream).
+template <int KIND, bool NT = false>
+__device__ __forceinline__ uint32_t hash_key(const void* __restrict__ in0, const uint64_t* __restrict__ offs,
+                                             uint32_t key_len, uint32_t seed, uint64_t k) {
+  if constexpr (KIND == IN_KEYS24) {
+    const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) + k * 24);
+    v2u a, b, c;
+    if constexpr (NT) {
+      a = __builtin_nontemporal_load(kp);
+      b = __builtin_nontemporal_load(kp + 1);
+      c = __builtin_nontemporal_load(kp + 2);
+    } else {
+      a = kp[0];
+      b = kp[1];
+      c = kp[2];
+    }
+    uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    return xxh32_24(w, seed);
+  } else if constexpr (KIND == IN_KEYS_W) {
+    return xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + k * key_len),
+                       key_len, seed);
+  } else if constexpr (KIND == IN_KEYS_B) {
+    return xxh32_bytes(static_cast<const uint8_t*>(in0) + k * key_len, key_len, seed);
+  } else if constexpr (KIND == IN_VAR) {
+    const uint64_t o0 = offs[k], o1 = offs[k + 1];
+    return xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
+  } else {  // IN_HASH
+    if constexpr (NT) return __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + k);
+    else return static_cast<const uint32_t*>(in0)[k];
+  }
+}
+
 // ======================================================================================
 // K1: hash + coarse-bucket histogram
 // ======================================================================================
@@ -44,8 +80,10 @@ __global__ __launch_bounds__(TILE_NT) void k_hash_count(const FilterPlan* __rest
                                                         const uint64_t* __restrict__ offs,
                                                         uint32_t key_len, uint32_t fp_size,
                                                         uint32_t seed, EntT* __restrict__ ent,
-                                                        uint32_t* __restrict__ cb_count) {
+                                                        uint32_t* __restrict__ cb_count,
+                                                        const uint32_t* __restrict__ gate) {
   __shared__ uint32_t s_hist[MAX_CB];
+  if (gate && *gate == 0) return;  // fallback pass of the fused build: not needed
   const uint32_t t = blockIdx.x;
   const FilterPlan& P = plans[tile_filter[t]];
   const uint32_t start = tile_start[t];
@@ -55,24 +93,7 @@ __global__ __launch_bounds__(TILE_NT) void k_hash_count(const FilterPlan* __rest
   __syncthreads();
   const uint32_t esh = fp_size + P.vs - P.cbits;  // entry >> esh = coarse bucket
   for (uint32_t j = threadIdx.x; j < count; j += TILE_NT) {
-    const uint64_t k = P.key_first + start + j;
-    uint32_t h;
-    if constexpr (KIND == IN_KEYS24) {
-      const uint2* kp = reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(in0) + k * 24);
-      uint2 a = kp[0], b = kp[1], c = kp[2];
-      uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-      h = xxh32_24(w, seed);
-    } else if constexpr (KIND == IN_KEYS_W) {
-      h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + k * key_len),
-                      key_len, seed);
-    } else if constexpr (KIND == IN_KEYS_B) {
-      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + k * key_len, key_len, seed);
-    } else if constexpr (KIND == IN_VAR) {
-      const uint64_t o0 = offs[k], o1 = offs[k + 1];
-      h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
-    } else {  // IN_HASH
-      h = static_cast<const uint32_t*>(in0)[k];
-    }
+    const uint32_t h = hash_key<KIND>(in0, offs, key_len, seed, P.key_first + start + j);
     const uint32_t e = ((h >> (32 - fp_size)) << P.vs) | P.value;
     if constexpr (sizeof(EntT) == 8) {
       ent[P.e_first + start + j] = ((uint64_t)e << 1) | 1ull;  // new entry: flag 1
@@ -122,10 +143,13 @@ __global__ __launch_bounds__(TILE_NT) void k_old_count(const FilterPlan* __restr
 // K2: per-filter exclusive scan of coarse-bucket counts
 // ======================================================================================
 __global__ __launch_bounds__(256) void k_cb_scan(const FilterPlan* __restrict__ plans,
-                                                 const uint32_t* __restrict__ cb_count,
+                                                 const uint32_t* counts,  // may alias cb_count / cb_cursor
+                                                 uint32_t* cb_count,
                                                  uint32_t* __restrict__ cb_start,
-                                                 uint32_t* __restrict__ cb_cursor) {
+                                                 uint32_t* cb_cursor,
+                                                 const uint32_t* __restrict__ gate) {
   __shared__ uint32_t s_tmp[256 / WAVE + 1];
+  if (gate && *gate == 0) return;
   const FilterPlan& P = plans[blockIdx.x];
   const uint32_t num_cb = 1u << P.cbits;
   constexpr uint32_t PER = MAX_CB / 256;
@@ -133,7 +157,7 @@ __global__ __launch_bounds__(256) void k_cb_scan(const FilterPlan* __restrict__ 
 #pragma unroll
   for (uint32_t k = 0; k < PER; k++) {
     const uint32_t i = threadIdx.x * PER + k;
-    v[k] = i < num_cb ? cb_count[P.cb_base + i] : 0u;
+    v[k] = i < num_cb ? counts[P.cb_base + i] : 0u;
     sum += v[k];
   }
   uint32_t total;
@@ -142,6 +166,7 @@ __global__ __launch_bounds__(256) void k_cb_scan(const FilterPlan* __restrict__ 
   for (uint32_t k = 0; k < PER; k++) {
     const uint32_t i = threadIdx.x * PER + k;
     if (i < num_cb) {
+      cb_count[P.cb_base + i] = v[k];
       cb_start[P.cb_base + i] = run;
       cb_cursor[P.cb_base + i] = run;
     }
@@ -159,12 +184,14 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
                                                      uint32_t region_is_old, uint32_t fp_size,
                                                      const EntT* __restrict__ ent,
                                                      EntT* __restrict__ part,
-                                                     uint32_t* __restrict__ cb_cursor) {
+                                                     uint32_t* __restrict__ cb_cursor,
+                                                     const uint32_t* __restrict__ gate) {
   // The tile is sorted by coarse bucket in LDS, then each bucket's run is written by
   // consecutive lanes: whole 64-byte granules instead of scattered 4-byte stores.
   __shared__ EntT s_stage[TILE_KEYS];
   __shared__ uint32_t s_off[MAX_CB];  // local offsets, then (global base - local offset)
   __shared__ uint32_t s_tmp[SCAT_NT / WAVE + 1];
+  if (gate && *gate == 0) return;
   constexpr int PER = TILE_KEYS / SCAT_NT;
   constexpr int BPT = MAX_CB / SCAT_NT;
   const uint32_t t = blockIdx.x;
@@ -241,6 +268,97 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
 }
 
 // ======================================================================================
+// K1+K3 fused (fresh builds, 32-bit entries): hash a tile, rank its entries by coarse
+// bucket in LDS, reserve each bucket's run with one atomic, and write the runs straight
+// into the bucket's fixed region of SORT_CAP slots at part[e_first + cb * SORT_CAP] --
+// no entry array round trip and no separate count/scan pass. A bucket that would exceed
+// SORT_CAP (duplicate-heavy or adversarial input) raises *spill; the exact count -> scan
+// -> scatter pipeline (K1, K2, K3 gated on *spill) then rebuilds the partition.
+// ======================================================================================
+template <int KIND>
+__global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __restrict__ plans,
+                                                          const uint32_t* __restrict__ tile_filter,
+                                                          const uint32_t* __restrict__ tile_start,
+                                                          const void* __restrict__ in0,
+                                                          const uint64_t* __restrict__ offs,
+                                                          uint32_t key_len, uint32_t fp_size, uint32_t seed,
+                                                          uint32_t* __restrict__ part,
+                                                          uint32_t* __restrict__ cb_fill,
+                                                          uint32_t* __restrict__ spill) {
+  __shared__ uint32_t s_stage[TILE_KEYS];
+  __shared__ uint32_t s_off[MAX_CB];  // local counts -> local starts -> (global slot - local start)
+  __shared__ uint32_t s_tmp[SCAT_NT / WAVE + 1];
+  constexpr int PER = TILE_KEYS / SCAT_NT;
+  constexpr int BPT = MAX_CB / SCAT_NT;
+  const uint32_t t = blockIdx.x;
+  const FilterPlan& P = plans[tile_filter[t]];
+  const uint32_t start = tile_start[t];
+  const uint32_t count = min((uint32_t)TILE_KEYS, P.num_new - start);
+  const uint32_t num_cb = 1u << P.cbits;
+  for (uint32_t i = threadIdx.x; i < num_cb; i += SCAT_NT) s_off[i] = 0;
+  __syncthreads();
+  const uint32_t esh = fp_size + P.vs - P.cbits;  // entry >> esh = coarse bucket
+  auto cb_of = [&](uint32_t e) -> uint32_t { return P.cbits ? (e >> esh) : 0u; };
+  uint32_t v[PER], rank[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x + k * SCAT_NT;
+    if (j < count) {
+      const uint32_t h = hash_key<KIND>(in0, offs, key_len, seed, P.key_first + start + j);
+      v[k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+      rank[k] = atomicAdd(&s_off[cb_of(v[k])], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t cnt[BPT], sum = 0;
+#pragma unroll
+  for (int k = 0; k < BPT; k++) {
+    const uint32_t b = threadIdx.x * BPT + k;
+    cnt[k] = b < num_cb ? s_off[b] : 0u;
+    sum += cnt[k];
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan<SCAT_NT>(sum, s_tmp, &total);
+  uint32_t gslot[BPT];
+  bool over = false;
+#pragma unroll
+  for (int k = 0; k < BPT; k++) {
+    const uint32_t b = threadIdx.x * BPT + k;
+    gslot[k] = 0;
+    if (b < num_cb) {
+      s_off[b] = run;
+      if (cnt[k]) {
+        const uint32_t g = atomicAdd(&cb_fill[P.cb_base + b], cnt[k]);
+        over |= g + cnt[k] > (uint32_t)SORT_CAP;
+        gslot[k] = g - run;
+      }
+      run += cnt[k];
+    }
+  }
+  if (over) atomicOr(spill, 1u);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t j = threadIdx.x + k * SCAT_NT;
+    if (j < count) s_stage[s_off[cb_of(v[k])] + rank[k]] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < BPT; k++) {
+    const uint32_t b = threadIdx.x * BPT + k;
+    if (b < num_cb) s_off[b] = gslot[k];
+  }
+  __syncthreads();
+  uint32_t* dst = part + P.e_first;
+  for (uint32_t j = threadIdx.x; j < total; j += SCAT_NT) {
+    const uint32_t x = s_stage[j];
+    const uint32_t cb = cb_of(x);
+    const uint32_t slot = s_off[cb] + j;  // position inside the bucket's region
+    if (slot < (uint32_t)SORT_CAP) dst[(uint64_t)cb * SORT_CAP + slot] = x;
+  }
+}
+
+// ======================================================================================
 // K4: per coarse bucket sort / dedupe / index counts
 // ======================================================================================
 template <typename EntT>
@@ -311,7 +429,8 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
                                                      FilterOut* __restrict__ outs,
                                                      uint32_t* __restrict__ overflow,
                                                      uint32_t lis, uint32_t* __restrict__ first_old,
-                                                     uint32_t* __restrict__ has_old) {
+                                                     uint32_t* __restrict__ has_old,
+                                                     const uint32_t* __restrict__ spill) {
   constexpr int PER = SORT_CAP / SORT_NT;
   __shared__ EntT s_b[SORT_CAP];
   __shared__ uint32_t s_bin[MAX_BINS + 1];
@@ -323,7 +442,9 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
   const FilterPlan& P = plans[f];
   const uint32_t n = cb_count[cb];
   const uint32_t cbl = cb - P.cb_base;
-  CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_start[cb], P.e_first};
+  // fused build without spill: fixed SORT_CAP regions; otherwise the scanned starts
+  const uint32_t cb_rel = (spill && *spill == 0) ? cbl * (uint32_t)SORT_CAP : cb_start[cb];
+  CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_rel, P.e_first};
   if (n > SORT_CAP) {  // handled by k_cb_sort_big
     if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
     return;
@@ -933,9 +1054,6 @@ __device__ __forceinline__ uint32_t select128(uint64_t lo, uint64_t hi, uint32_t
   return r < c ? select64_fast(lo, r) : 64 + select64_fast(hi, r - c);
 }
 
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-
 // one 16-byte aligned window of the page bytes as two little-endian u64
 __device__ __forceinline__ void ld_win(const uint8_t* pg, uint64_t a16, uint64_t& lo, uint64_t& hi) {
   const v4u v = *reinterpret_cast<const v4u*>(pg + a16);
@@ -1177,7 +1295,7 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
 }
 
 constexpr int PROBE_NT = 256;
-constexpr int PROBE_LDS_PAD = 24 * 1024;
+constexpr int PROBE_LDS_PAD = 0;
 
 // One lane per probe. (A cooperative variant that staged 128-byte block heads through LDS,
 // 8 lanes per block, measured slower on MI355X -- 3.09 vs 2.34 ms at C2 -- the kernel is
@@ -1202,25 +1320,8 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
   const uint64_t i = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // the key (or hash) and the filter id are independent loads: issue them together
-  uint32_t h;
   const uint32_t fid = __builtin_nontemporal_load(filter_id + i);
-  if constexpr (KIND == IN_KEYS24) {
-    const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) + i * 24);
-    const v2u a = __builtin_nontemporal_load(kp), b = __builtin_nontemporal_load(kp + 1),
-              c = __builtin_nontemporal_load(kp + 2);
-    uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-    h = xxh32_24(w, seed);
-  } else if constexpr (KIND == IN_KEYS_W) {
-    h = xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + i * key_len),
-                    key_len, seed);
-  } else if constexpr (KIND == IN_KEYS_B) {
-    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + i * key_len, key_len, seed);
-  } else if constexpr (KIND == IN_VAR) {
-    const uint64_t o0 = offs[i], o1 = offs[i + 1];
-    h = xxh32_bytes(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
-  } else {
-    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + i);
-  }
+  const uint32_t h = hash_key<KIND, true>(in0, offs, key_len, seed, i);
   // unknown filter, or one whose build failed (k_layout sets pp.w): nothing found
   const uint4 pp = fid < num_filters ? pplans[fid] : make_uint4(0, 0, 0, 1);
   if (pp.w) {
@@ -1262,36 +1363,48 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
 #define CHECK_LAUNCH() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
 #define REC(slot) do { if (a.events) (void)hipEventRecord((hipEvent_t)a.events[slot], (hipStream_t)a.stream); } while (0)
 
-template <typename EntT>
-static int launch_hash_count_t(int kind, const LaunchArgs& a, EntT* ent) {
-  dim3 g(a.num_tiles), b(TILE_NT);
-  switch (kind) {
-    case IN_KEYS24: hipLaunchKernelGGL((k_hash_count<IN_KEYS24, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
-    case IN_KEYS_W: hipLaunchKernelGGL((k_hash_count<IN_KEYS_W, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
-    case IN_KEYS_B: hipLaunchKernelGGL((k_hash_count<IN_KEYS_B, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
-    case IN_VAR:    hipLaunchKernelGGL((k_hash_count<IN_VAR, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
-    default:        hipLaunchKernelGGL((k_hash_count<IN_HASH, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, a.cb_count); break;
+// dispatch on the input kind (template parameter of the hashing kernels)
+#define KIND_SWITCH(kind, L)           \
+  switch (kind) {                      \
+    case IN_KEYS24: L(IN_KEYS24); break; \
+    case IN_KEYS_W: L(IN_KEYS_W); break; \
+    case IN_KEYS_B: L(IN_KEYS_B); break; \
+    case IN_VAR: L(IN_VAR); break;       \
+    default: L(IN_HASH); break;          \
   }
+
+// counts: per coarse bucket counter array (atomically accumulated); gate: see k_hash_count
+template <typename EntT>
+static int launch_hash_count_t(const LaunchArgs& a, EntT* ent, uint32_t* counts, const uint32_t* gate) {
+  dim3 g(a.num_tiles), b(TILE_NT);
+#define L(K) hipLaunchKernelGGL((k_hash_count<K, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, \
+                                a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, counts, gate)
+  KIND_SWITCH(a.kind, L);
+#undef L
   CHECK_LAUNCH();
   return 0;
 }
 
 template <typename EntT>
-static int launch_rest_t(const LaunchArgs& a, EntT* ent, EntT* part) {
+static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* gate) {
   if (a.num_tiles) {
     hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.tile_filter, a.tile_start, 0u, a.fp_size, ent, part, a.cb_cursor);
+                       a.tile_filter, a.tile_start, 0u, a.fp_size, ent, part, a.cb_cursor, gate);
     CHECK_LAUNCH();
   }
   if (a.num_old_tiles) {
     hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_old_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.old_tile_filter, a.old_tile_start, 1u, a.fp_size, ent, part, a.cb_cursor);
+                       a.old_tile_filter, a.old_tile_start, 1u, a.fp_size, ent, part, a.cb_cursor, gate);
     CHECK_LAUNCH();
   }
-  REC(EV_B_SCATTER);
+  return 0;
+}
+
+template <typename EntT>
+static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* spill) {
   hipLaunchKernelGGL((k_cb_sort<EntT>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
                      a.cb_count, a.cb_start, part, a.sorted32, a.idx_cnt, a.idx_start, a.outs, a.overflow,
-                     a.lis, a.first_old, a.has_old);
+                     a.lis, a.first_old, a.has_old, spill);
   CHECK_LAUNCH();
   REC(EV_B_SORT);
   hipLaunchKernelGGL((k_cb_sort_big<EntT>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
@@ -1307,25 +1420,47 @@ extern "C" int rf_launch_plines(const LaunchArgs* pa);
 extern "C" int rf_launch_build(const LaunchArgs* pa) {
   const LaunchArgs& a = *pa;
   if (a.wide) {
+    // incremental add: 64-bit entries; old entries first (decoded by rf_launch_old_decode)
     uint64_t* ent = (uint64_t*)a.ent;
-    // old entries first (they were decoded into the old region by rf_launch_old_decode)
+    uint64_t* part = (uint64_t*)a.part;
     if (a.num_old_tiles) {
       hipLaunchKernelGGL(k_old_count, dim3(a.num_old_tiles), dim3(TILE_NT), 0, (hipStream_t)a.stream, a.plans,
                          a.old_tile_filter, a.old_tile_start, a.fp_size, ent, a.cb_count);
       CHECK_LAUNCH();
     }
-    if (a.num_tiles) { int rc = launch_hash_count_t<uint64_t>(a.kind, a, ent); if (rc) return rc; }
+    if (a.num_tiles) { int rc = launch_hash_count_t<uint64_t>(a, ent, a.cb_count, nullptr); if (rc) return rc; }
+    REC(EV_B_HASH);
+    hipLaunchKernelGGL(k_cb_scan, dim3(a.num_filters), dim3(256), 0, (hipStream_t)a.stream, a.plans, a.cb_count,
+                       a.cb_count, a.cb_start, a.cb_cursor, nullptr);
+    CHECK_LAUNCH();
+    REC(EV_B_SCAN);
+    if (int rc = launch_scatter_t<uint64_t>(a, ent, part, nullptr)) return rc;
+    REC(EV_B_SCATTER);
+    if (int rc = launch_sort_t<uint64_t>(a, ent, part, nullptr)) return rc;
   } else {
-    if (a.num_tiles) { int rc = launch_hash_count_t<uint32_t>(a.kind, a, (uint32_t*)a.ent); if (rc) return rc; }
+    // fresh build: fused hash + partition into fixed regions (cb_count = fills)
+    uint32_t* ent = (uint32_t*)a.ent;
+    uint32_t* part = (uint32_t*)a.part;
+    if (a.num_tiles) {
+#define L(K) hipLaunchKernelGGL((k_hash_scatter<K>), dim3(a.num_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, \
+                                a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, \
+                                part, a.cb_count, a.spill)
+      KIND_SWITCH(a.kind, L);
+#undef L
+      CHECK_LAUNCH();
+    }
+    REC(EV_B_HASH);
+    // spill fallback (every kernel returns at once unless *spill): exact counts into
+    // cb_cursor, scan -> cb_count / cb_start / cb_cursor, scatter from the entry array
+    if (a.num_tiles) { int rc = launch_hash_count_t<uint32_t>(a, ent, a.cb_cursor, a.spill); if (rc) return rc; }
+    hipLaunchKernelGGL(k_cb_scan, dim3(a.num_filters), dim3(256), 0, (hipStream_t)a.stream, a.plans, a.cb_cursor,
+                       a.cb_count, a.cb_start, a.cb_cursor, a.spill);
+    CHECK_LAUNCH();
+    REC(EV_B_SCAN);
+    if (int rc = launch_scatter_t<uint32_t>(a, ent, part, a.spill)) return rc;
+    REC(EV_B_SCATTER);
+    if (int rc = launch_sort_t<uint32_t>(a, ent, part, a.spill)) return rc;
   }
-  REC(EV_B_HASH);
-  hipLaunchKernelGGL(k_cb_scan, dim3(a.num_filters), dim3(256), 0, (hipStream_t)a.stream, a.plans, a.cb_count,
-                     a.cb_start, a.cb_cursor);
-  CHECK_LAUNCH();
-  REC(EV_B_SCAN);
-  int rc = a.wide ? launch_rest_t<uint64_t>(a, (uint64_t*)a.ent, (uint64_t*)a.part)
-                  : launch_rest_t<uint32_t>(a, (uint32_t*)a.ent, (uint32_t*)a.part);
-  if (rc) return rc;
   hipLaunchKernelGGL(k_layout, dim3(a.num_filters), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, a.plans, a.idx_cnt,
                      a.idx_start, a.sorted32, a.first_old, a.has_old, a.pplans_mut, a.slots, a.page_first, a.outs, a.lis, a.page_size);
   CHECK_LAUNCH();
@@ -1378,8 +1513,9 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
     else if (o == 4) PK(IN_KEYS24, 38 * 1024); else if (o == 3) PK(IN_KEYS24, 50 * 1024);
     else PK(IN_KEYS24, 70 * 1024);
   } else {
-    // production: 24 KiB LDS pad = 6 workgroups (6 waves/SIMD) per CU; 8 waves measured
-    // 4 % slower (more outstanding random fetches thrash the XCD L2), 5 equal, 4 slower
+    // production: no LDS pad (8 waves/SIMD). The line probe is bound by outstanding random
+    // line fetches (latency x concurrency): 8 waves 1.14 ms, 6 waves 1.20, 5 1.27, 4 1.41
+    // at C2 (tools/line_sigma.py). The record-era probe preferred 6 (L2 thrash).
     switch (kind) {
       case IN_KEYS24: PK(IN_KEYS24, PROBE_LDS_PAD); break;
       case IN_KEYS_W: PK(IN_KEYS_W, PROBE_LDS_PAD); break;

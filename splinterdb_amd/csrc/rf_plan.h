@@ -82,6 +82,7 @@ struct LaunchArgs {
   const uint32_t* cb_filter;
   uint32_t num_cb;
   uint32_t* overflow;
+  uint32_t* spill;  // fused build: a coarse bucket exceeded its SORT_CAP region
   uint32_t* idx_cnt;
   uint32_t* idx_start;
   uint32_t* first_old;  // wide mode: per index, smallest old entry (valid if has_old)

@@ -1,4 +1,4 @@
-"""Diagnostic: time k_probe truncated after each step (hash / slot / block head / full),
+"""Diagnostic: time k_probe truncated after each step (hash / + probe-line load / full),
 interleaved rounds in one process (cdna_hip_programming.md rule 24). C2 shape."""
 import json
 import os
@@ -31,6 +31,6 @@ for rnd in range(6):
         torch.cuda.synchronize()
         res[m].append(b.timings()["probe"])
 L.rf_amd_debug_probe_ablate(0)
-out = {("hash", "record", "full")[i]: round(float(np.median(res[m][1:])), 4)
+out = {("hash", "line", "full")[i]: round(float(np.median(res[m][1:])), 4)
        for i, m in enumerate((1, 2, 0))}
 print(json.dumps(out))
