@@ -451,7 +451,8 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   (void)hipGetLastError();
   LaunchArgs a = make_args(b, st);
   a.ablate = g_probe_ablate & 0xff;
-  a.occ = g_probe_ablate >> 8;
+  a.occ = (g_probe_ablate >> 8) & 0xff;
+  a.ppl = (g_probe_ablate >> 16) & 0xff;
   int rc = rf_launch_probe(&a, kind, in0, offs, key_len, fid, n, found);
   if (rc) return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
   return 0;

@@ -213,11 +213,12 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
   EntT v[PER];
   uint32_t cbv[PER], rank[PER];
 #pragma unroll
+  for (int k = 0; k < PER; k++) v[k] = ent[base + min(threadIdx.x + k * SCAT_NT, count - 1)];
+#pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = threadIdx.x + k * SCAT_NT;
     cbv[k] = ~0u;
     if (j < count) {
-      v[k] = ent[base + j];
       bool valid = true;
       if constexpr (sizeof(EntT) == 8) valid = v[k] != ~0ull;
       if (valid) {
@@ -300,14 +301,29 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   const uint32_t esh = fp_size + P.vs - P.cbits;  // entry >> esh = coarse bucket
   auto cb_of = [&](uint32_t e) -> uint32_t { return P.cbits ? (e >> esh) : 0u; };
   uint32_t v[PER], rank[PER];
+  // all key loads first (clamped index: no branch, every load in flight at once), then the
+  // LDS ranking -- interleaving them serialises one HBM round trip per key
+  // in chunks of HASH_CHUNK keys: a chunk's loads are all in flight together; the next
+  // chunk's addresses take an opaque zero computed from this chunk's last hash, so the
+  // compiler cannot hoist every key of the tile into registers (236 VGPRs, 2 waves/SIMD)
+  constexpr int HASH_CHUNK = 8;
+  uint32_t dep = 0;
 #pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x + k * SCAT_NT;
-    if (j < count) {
+  for (int k0 = 0; k0 < PER; k0 += HASH_CHUNK) {
+#pragma unroll
+    for (int k = k0; k < k0 + HASH_CHUNK; k++) {
+      const uint32_t j = min(threadIdx.x + k * SCAT_NT, count - 1) + dep;
       const uint32_t h = hash_key<KIND>(in0, offs, key_len, seed, P.key_first + start + j);
       v[k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
-      rank[k] = atomicAdd(&s_off[cb_of(v[k])], 1u);
     }
+    static_assert(HASH_CHUNK == 8, "opaque dependency below takes 8 hashes");
+    asm volatile("v_mov_b32 %0, 0" : "=v"(dep)
+                 : "v"(v[k0]), "v"(v[k0 + 1]), "v"(v[k0 + 2]), "v"(v[k0 + 3]), "v"(v[k0 + 4]),
+                   "v"(v[k0 + 5]), "v"(v[k0 + 6]), "v"(v[k0 + 7]));
+  }
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    if (threadIdx.x + k * SCAT_NT < count) rank[k] = atomicAdd(&s_off[cb_of(v[k])], 1u);
   }
   __syncthreads();
   uint32_t cnt[BPT], sum = 0;
@@ -461,11 +477,13 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
   EntT v[PER];
   uint32_t r[PER];
   const EntT* src = part + P.e_first + c.cb_rel;
+  // loads first (clamped, branch-free), then the LDS ranking (see k_hash_scatter)
+  const uint32_t nm1 = n ? n - 1 : 0u;
+#pragma unroll
+  for (int k = 0; k < PER; k++) v[k] = src[min(threadIdx.x + k * SORT_NT, nm1)];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t i = threadIdx.x + k * SORT_NT;
-    if (i < n) {
-      v[k] = src[i];
+    if (threadIdx.x + k * SORT_NT < n) {
       const uint32_t e = ent_e(v[k]);
       const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
       r[k] = atomicAdd(&s_bin[b], 1u);
@@ -1214,19 +1232,15 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
   }
 }
 
-// Line probe: bucket j of the line's group; returns false on an overflowed line.
-__device__ __forceinline__ bool probe_line(const uint4* __restrict__ lines, uint64_t line, uint32_t j,
-                                           uint32_t G, uint32_t remainder, uint32_t vs, uint32_t rvs,
-                                           uint64_t& found) {
+// Line probe, decode half: bucket j of the line's group (line bytes in Q); returns false
+// on an overflowed line.
+__device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint32_t G, uint32_t remainder,
+                                            uint32_t vs, uint32_t rvs, uint64_t& found) {
   uint64_t W[8];
-  {
-    const v4u* q = reinterpret_cast<const v4u*>(lines + line * 4);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const v4u v = q[k];
-      W[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-      W[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
-    }
+  for (int k = 0; k < 4; k++) {
+    W[2 * k] = (uint64_t)Q[k].x | ((uint64_t)Q[k].y << 32);
+    W[2 * k + 1] = (uint64_t)Q[k].z | ((uint64_t)Q[k].w << 32);
   }
   const uint32_t hdr = (uint32_t)W[0] & 0xffffu;
   if (hdr & 0x8000u) return false;
@@ -1296,12 +1310,15 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
 
 constexpr int PROBE_NT = 256;
 constexpr int PROBE_LDS_PAD = 0;
+constexpr int PROBE_PPL = 1;  // probes per lane (production)
 
 // One lane per probe. (A cooperative variant that staged 128-byte block heads through LDS,
 // 8 lanes per block, measured slower on MI355X -- 3.09 vs 2.34 ms at C2 -- the kernel is
 // bound by random L2 line fetches, not load-instruction issue; it was removed.)
 // OCC_LDS > 0 pads LDS to cap workgroups per CU (occupancy experiments; 0 = none).
-template <int KIND, int OCC_LDS = 0>
+// A lane handles PPL probes (i, i + PROBE_NT, ...): all their key loads, then all their
+// line loads, then the decodes -- PPL independent random line fetches in flight per lane.
+template <int KIND, int OCC_LDS = 0, int PPL = 1>
 __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
                                                     const FilterPlan* __restrict__ plans,
                                                     const uint8_t* __restrict__ pages,
@@ -1317,44 +1334,62 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     __shared__ uint32_t s_pad[OCC_LDS / 4];
     if (ablate == 0xdead) s_pad[threadIdx.x] = 0;  // keeps the pad allocated
   }
-  const uint64_t i = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  // the key (or hash) and the filter id are independent loads: issue them together
-  const uint32_t fid = __builtin_nontemporal_load(filter_id + i);
-  const uint32_t h = hash_key<KIND, true>(in0, offs, key_len, seed, i);
-  // unknown filter, or one whose build failed (k_layout sets pp.w): nothing found
-  const uint4 pp = fid < num_filters ? pplans[fid] : make_uint4(0, 0, 0, 1);
-  if (pp.w) {
-    __builtin_nontemporal_store((uint64_t)0, found + i);
-    return;
-  }
-  if (ablate == 1) {  // diagnostic: key stream + hash only
-    __builtin_nontemporal_store((uint64_t)h, found + i);
-    return;
-  }
-  const uint32_t vs = pp.x & 0xff, rem = (pp.x >> 8) & 0xff, rvs = (pp.x >> 16) & 0xff, lgl = pp.x >> 24;
-  const uint32_t fp = h >> (32 - fp_size);
-  const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;  // index << lis | bucket in index
-  const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-  uint64_t r = 0;
-  if (lgl) {
-    const uint32_t lgG = lgl - 1;
-    const uint64_t line = (uint64_t)pp.y + (bucket >> lgG);
-    if (ablate == 2) {  // diagnostic: + the line's first 16 bytes
-      __builtin_nontemporal_store((uint64_t)lines[line * 4].x ^ h, found + i);
-      return;
-    }
-    if (probe_line(lines, line, bucket & ((1u << lgG) - 1), 1u << lgG, remainder, vs, rvs, r)) {
-      __builtin_nontemporal_store(r, found + i);
-      return;
+  const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (PROBE_NT * PPL) + threadIdx.x;
+  uint32_t h[PPL], fid[PPL];
+  // the keys (or hashes) and filter ids are independent loads: issue them all together
+#pragma unroll
+  for (int q = 0; q < PPL; q++) {
+    const uint64_t i = i0 + (uint64_t)q * PROBE_NT;
+    fid[q] = 0xffffffffu;
+    h[q] = 0;
+    if (i < n) {
+      fid[q] = __builtin_nontemporal_load(filter_id + i);
+      h[q] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
     }
   }
-  // overflowed line (or no lines): walk the image from the index slot
-  const uint32_t index = bucket >> lis;
-  const uint64_t hdr = slots[pp.z + index];
-  const uint8_t* pg = pages + (uint64_t)plans[fid].page_base * page_size;
-  r = probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, pg, hdr, lis);
-  __builtin_nontemporal_store(r, found + i);
+  uint4 pp[PPL];
+  uint32_t bucket[PPL], remainder[PPL];
+  v4u Q[PPL][4];
+#pragma unroll
+  for (int q = 0; q < PPL; q++) {
+    // unknown filter, or one whose build failed (k_layout sets pp.w): nothing found
+    pp[q] = fid[q] < num_filters ? pplans[fid[q]] : make_uint4(0, 0, 0, 1);
+    const uint32_t rem = (pp[q].x >> 8) & 0xff, lgl = pp[q].x >> 24;
+    const uint32_t fp = h[q] >> (32 - fp_size);
+    bucket[q] = rem >= 32 ? 0u : fp >> rem;  // index << lis | bucket in index
+    remainder[q] = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+    if (!pp[q].w && lgl && ablate != 1) {
+      const v4u* lp = reinterpret_cast<const v4u*>(lines + ((uint64_t)pp[q].y + (bucket[q] >> (lgl - 1))) * 4);
+#pragma unroll
+      for (int k = 0; k < 4; k++) Q[q][k] = lp[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) Q[q][k] = v4u{0x8000u, 0u, 0u, 0u};  // "overflowed": image path
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < PPL; q++) {
+    const uint64_t i = i0 + (uint64_t)q * PROBE_NT;
+    if (i >= n) continue;
+    uint64_t r = 0;
+    if (pp[q].w) {
+      r = 0;
+    } else if (ablate == 1) {  // diagnostic: key stream + hash only
+      r = h[q];
+    } else if (ablate == 2) {  // diagnostic: + the line load
+      r = (uint64_t)Q[q][0].x ^ Q[q][3].w ^ h[q];
+    } else {
+      const uint32_t vs = pp[q].x & 0xff, rvs = (pp[q].x >> 16) & 0xff, lgl = pp[q].x >> 24;
+      const uint32_t G = lgl ? 1u << (lgl - 1) : 1u;
+      if (!lgl || !line_decode(Q[q], bucket[q] & (G - 1), G, remainder[q], vs, rvs, r)) {
+        // overflowed line (or no lines): walk the image from the index slot
+        const uint64_t hdr = slots[pp[q].z + (bucket[q] >> lis)];
+        const uint8_t* pg = pages + (uint64_t)plans[fid[q]].page_base * page_size;
+        r = probe_stream(bucket[q] & ((1u << lis) - 1), remainder[q], vs, rvs, pg, hdr, lis);
+      }
+    }
+    __builtin_nontemporal_store(r, found + i);
+  }
 }
 
 // ======================================================================================
@@ -1504,24 +1539,31 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found) {
   const LaunchArgs& a = *pa;
   if (n == 0) return 0;
-  dim3 g((uint32_t)((n + PROBE_NT - 1) / PROBE_NT)), b(PROBE_NT);
+  const int ppl = a.ppl ? (int)a.ppl : PROBE_PPL;
+  dim3 g((uint32_t)((n + PROBE_NT * ppl - 1) / (PROBE_NT * ppl))), b(PROBE_NT);
   REC(EV_P_START);
-#define PK(K, L) hipLaunchKernelGGL((k_probe<K, L>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
-  if (kind == IN_KEYS24 && a.occ) {  // occupancy experiment variants (waves/SIMD cap)
-    const int o = a.occ;
-    if (o == 8) PK(IN_KEYS24, 0); else if (o == 6) PK(IN_KEYS24, 24 * 1024); else if (o == 5) PK(IN_KEYS24, 30 * 1024);
-    else if (o == 4) PK(IN_KEYS24, 38 * 1024); else if (o == 3) PK(IN_KEYS24, 50 * 1024);
-    else PK(IN_KEYS24, 70 * 1024);
+#define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
+  if (kind == IN_KEYS24 && (a.occ || a.ppl)) {  // experiment variants: waves/SIMD cap, probes per lane
+    const int o = a.occ ? (int)a.occ : 8;
+    if (ppl == 2) {
+      if (o == 8) PK(IN_KEYS24, 0, 2); else if (o == 6) PK(IN_KEYS24, 24 * 1024, 2); else PK(IN_KEYS24, 30 * 1024, 2);
+    } else if (ppl == 3) {
+      PK(IN_KEYS24, 0, 3);
+    } else {
+      if (o == 8) PK(IN_KEYS24, 0, 1); else if (o == 6) PK(IN_KEYS24, 24 * 1024, 1); else if (o == 5) PK(IN_KEYS24, 30 * 1024, 1);
+      else if (o == 4) PK(IN_KEYS24, 38 * 1024, 1); else if (o == 3) PK(IN_KEYS24, 50 * 1024, 1);
+      else PK(IN_KEYS24, 70 * 1024, 1);
+    }
   } else {
     // production: no LDS pad (8 waves/SIMD). The line probe is bound by outstanding random
     // line fetches (latency x concurrency): 8 waves 1.14 ms, 6 waves 1.20, 5 1.27, 4 1.41
     // at C2 (tools/line_sigma.py). The record-era probe preferred 6 (L2 thrash).
     switch (kind) {
-      case IN_KEYS24: PK(IN_KEYS24, PROBE_LDS_PAD); break;
-      case IN_KEYS_W: PK(IN_KEYS_W, PROBE_LDS_PAD); break;
-      case IN_KEYS_B: PK(IN_KEYS_B, PROBE_LDS_PAD); break;
-      case IN_VAR: PK(IN_VAR, PROBE_LDS_PAD); break;
-      default: PK(IN_HASH, PROBE_LDS_PAD); break;
+      case IN_KEYS24: PK(IN_KEYS24, PROBE_LDS_PAD, PROBE_PPL); break;
+      case IN_KEYS_W: PK(IN_KEYS_W, PROBE_LDS_PAD, PROBE_PPL); break;
+      case IN_KEYS_B: PK(IN_KEYS_B, PROBE_LDS_PAD, PROBE_PPL); break;
+      case IN_VAR: PK(IN_VAR, PROBE_LDS_PAD, PROBE_PPL); break;
+      default: PK(IN_HASH, PROBE_LDS_PAD, PROBE_PPL); break;
     }
   }
 #undef PK

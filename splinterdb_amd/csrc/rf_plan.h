@@ -99,6 +99,7 @@ struct LaunchArgs {
   FilterOut* outs;
   uint32_t ablate;  // probe diagnostics (0 = normal)
   uint32_t occ;     // probe occupancy experiment (0 = normal)
+  uint32_t ppl;     // probe probes-per-lane experiment (0 = production)
   void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)
 };
 
