@@ -310,11 +310,38 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   uint32_t dep = 0;
 #pragma unroll
   for (int k0 = 0; k0 < PER; k0 += HASH_CHUNK) {
+    if constexpr (KIND == IN_KEYS24) {
+      // 24-byte keys: issue all of the chunk's loads, then hash (z depends on every loaded
+      // word, so no hash starts before the last load is issued)
+      v2u ka[HASH_CHUNK], kb[HASH_CHUNK], kc[HASH_CHUNK];
 #pragma unroll
-    for (int k = k0; k < k0 + HASH_CHUNK; k++) {
-      const uint32_t j = min(threadIdx.x + k * SCAT_NT, count - 1) + dep;
-      const uint32_t h = hash_key<KIND>(in0, offs, key_len, seed, P.key_first + start + j);
-      v[k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+      for (int k = 0; k < HASH_CHUNK; k++) {
+        const uint32_t j = min(threadIdx.x + (k0 + k) * SCAT_NT, count - 1) + dep;
+        const v2u* kp = reinterpret_cast<const v2u*>(static_cast<const uint8_t*>(in0) +
+                                                     (P.key_first + start + j) * 24);
+        ka[k] = kp[0];
+        kb[k] = kp[1];
+        kc[k] = kp[2];
+      }
+      uint32_t z;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z)
+                   : "v"(ka[0].x), "v"(ka[1].x), "v"(ka[2].x), "v"(ka[3].x), "v"(ka[4].x), "v"(ka[5].x),
+                     "v"(ka[6].x), "v"(ka[7].x), "v"(kb[0].x), "v"(kb[1].x), "v"(kb[2].x), "v"(kb[3].x),
+                     "v"(kb[4].x), "v"(kb[5].x), "v"(kb[6].x), "v"(kb[7].x), "v"(kc[0].x), "v"(kc[1].x),
+                     "v"(kc[2].x), "v"(kc[3].x), "v"(kc[4].x), "v"(kc[5].x), "v"(kc[6].x), "v"(kc[7].x));
+#pragma unroll
+      for (int k = 0; k < HASH_CHUNK; k++) {
+        uint32_t w[6] = {ka[k].x + z, ka[k].y, kb[k].x, kb[k].y, kc[k].x, kc[k].y};
+        const uint32_t h = xxh32_24(w, seed);
+        v[k0 + k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+      }
+    } else {
+#pragma unroll
+      for (int k = k0; k < k0 + HASH_CHUNK; k++) {
+        const uint32_t j = min(threadIdx.x + k * SCAT_NT, count - 1) + dep;
+        const uint32_t h = hash_key<KIND>(in0, offs, key_len, seed, P.key_first + start + j);
+        v[k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+      }
     }
     static_assert(HASH_CHUNK == 8, "opaque dependency below takes 8 hashes");
     asm volatile("v_mov_b32 %0, 0" : "=v"(dep)
