@@ -119,6 +119,12 @@ int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
  * (results are then NOT found_values); 0 restores normal probes. Bits 8+: cap the probe
  * kernel at that many waves per SIMD (occupancy experiments). */
 void rf_amd_debug_probe_ablate(uint32_t mode);
+/* diagnostics: the batch's device-only probe lines (64 B each). read_lines copies them to
+ * host (h_lines == NULL: only *num_lines is set); rebuild_lines re-cuts them from the
+ * filter images with the image-upload kernel (k_plines), so a test can check that the
+ * build's lines and the image's lines are byte-identical. */
+int rf_amd_debug_read_lines(rf_amd_batch *b, uint8_t *h_lines, uint64_t bytes, uint64_t *num_lines);
+int rf_amd_debug_rebuild_lines(rf_amd_batch *b);
 int rf_amd_batch_timings(rf_amd_batch *b, float *ms, uint32_t n);
 
 /* ---- drop-in single-filter calls on HOST buffers ------------------------------------

@@ -477,6 +477,28 @@ extern "C" int rf_amd_batch_probe_hashes(rf_amd_batch* b, const uint32_t* d_hash
 // the probe kernel at that many waves per SIMD via LDS padding (occupancy experiments).
 extern "C" void rf_amd_debug_probe_ablate(uint32_t mode) { g_probe_ablate = mode; }
 
+extern "C" int rf_amd_debug_read_lines(rf_amd_batch* b, uint8_t* h_lines, uint64_t bytes, uint64_t* num_lines) {
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "unbuilt batch");
+  if (num_lines) *num_lines = b->NL;
+  if (!h_lines) return 0;
+  if (bytes < 64ull * b->NL) return fail(RF_AMD_EINVAL, "lines buffer too small");
+  HIPCHK(hipSetDevice(b->eng->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(h_lines, b->d_lines.p, 64ull * b->NL, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int rf_amd_debug_rebuild_lines(rf_amd_batch* b) {
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "unbuilt batch");
+  HIPCHK(hipSetDevice(b->eng->device));
+  HIPCHK(hipDeviceSynchronize());
+  (void)hipGetLastError();
+  LaunchArgs a = make_args(b, b->eng->stream);
+  if (int rc = rf_launch_plines(&a)) return fail(RF_AMD_EINVAL, std::string("probe-line launch: ") + hipGetErrorString((hipError_t)rc));
+  HIPCHK(hipStreamSynchronize(b->eng->stream));
+  return 0;
+}
+
 extern "C" int rf_amd_batch_set_timing(rf_amd_batch* b, int enable) {
   if (!b) return fail(RF_AMD_EINVAL, "null batch");
   HIPCHK(hipSetDevice(b->eng->device));

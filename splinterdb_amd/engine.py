@@ -34,6 +34,7 @@ EXPORTED = [
     "rf_amd_batch_probe_var_keys", "rf_amd_batch_probe_hashes", "rf_amd_batch_info",
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
     "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_debug_probe_ablate",
+    "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines",
     "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",
     "rf_amd_image_free",
     "rf_amd_max_fingerprints", "rf_amd_estimate_unique_keys_from_count",
@@ -100,6 +101,8 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_set_timing.argtypes = [vp, i32]
     L.rf_amd_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), u32]
     L.rf_amd_debug_probe_ablate.argtypes = [u32]
+    L.rf_amd_debug_read_lines.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
+    L.rf_amd_debug_rebuild_lines.argtypes = [vp]
     L.rf_amd_debug_probe_ablate.restype = None
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
@@ -391,6 +394,18 @@ class FilterBatch:
 
     def set_timing(self, enable=True):
         _check(load_library().rf_amd_batch_set_timing(self.h, 1 if enable else 0))
+
+    def debug_lines(self) -> np.ndarray:
+        """The batch's device-only probe lines (diagnostics), as an (N, 64) uint8 array."""
+        L, n = load_library(), ctypes.c_uint64(0)
+        _check(L.rf_amd_debug_read_lines(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros((n.value, 64), dtype=np.uint8)
+        _check(L.rf_amd_debug_read_lines(self.h, out.ctypes.data, out.nbytes, ctypes.byref(n)))
+        return out
+
+    def debug_rebuild_lines(self):
+        """Re-cut the probe lines from the images with the image-upload kernel (diagnostics)."""
+        _check(load_library().rf_amd_debug_rebuild_lines(self.h))
 
     def timings(self):
         """Per-stage milliseconds of the last build / probe (HIP events on the launch stream)."""

@@ -315,6 +315,86 @@ def test_probe_line_overflow_falls_back_to_image(oracle):
         assert (got[: P // 3] >> np.uint64(value) & np.uint64(1)).all()
 
 
+def expected_probe_lines(pages, slots, num_indices, IS, G, rvs):
+    """numpy restatement of the device-only probe-line format (rf_kernels.hip, "probe
+    lines"), cut from a filter image: per group of G buckets, a 16-bit header (entry count,
+    or 0x8000 = overflow), the group's slice of the unary encoding, its packed remainders."""
+    bits = np.unpackbits(pages, bitorder="little")
+    L = IS // G
+    out = np.zeros((num_indices * L, 64), dtype=np.uint8)
+    for i in range(num_indices):
+        h = int(slots[i])
+        c = int(pages[h]) | (int(pages[h + 1]) << 8)
+        e0 = (h + 2) * 8
+        enc = bits[e0: e0 + c + IS]
+        ones = np.flatnonzero(enc)
+        r0 = (h + 2 + (c + IS - 1) // 8 + 4) * 8
+        for g in range(L):
+            a = 0 if g == 0 else int(ones[g * G - 1]) + 1
+            end = int(ones[g * G + G - 1]) + 1
+            ne = end - a
+            n, E = ne - G, a - g * G
+            tot = 16 + ne + n * rvs
+            line = np.zeros(512, dtype=np.uint8)
+            hdr = 0x8000 if tot > 512 else n
+            if tot <= 512:
+                line[16:16 + ne] = enc[a:end]
+                line[16 + ne:tot] = bits[r0 + E * rvs: r0 + (E + n) * rvs]
+            line[:16] = [(hdr >> k) & 1 for k in range(16)]
+            out[i * L + g] = np.packbits(line, bitorder="little")
+    return out
+
+
+def _check_lines(b, img, cfg_kw, value):
+    lines = b.debug_lines()
+    lis = cfg_kw.get("log_index_size", 8)
+    fps = cfg_kw.get("fingerprint_size", 26)
+    IS = 1 << lis
+    lnb = max(int(img.num_fingerprints).bit_length() - 1, lis)
+    rvs = fps - lnb + int(value).bit_length()
+    G = img.num_indices * IS // lines.shape[0]
+    assert G * lines.shape[0] == img.num_indices * IS and G & (G - 1) == 0
+    want = expected_probe_lines(img.pages, img.slots, img.num_indices, IS, G, rvs)
+    bad = np.nonzero((lines != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} of {lines.shape[0]} lines differ, first {bad[:5]}"
+    b.debug_rebuild_lines()  # the image-upload path re-cuts the same lines
+    assert (b.debug_lines() == want).all()
+    hdr = want[:, 0].astype(np.uint32) | (want[:, 1].astype(np.uint32) << 8)
+    return G, float(((hdr & 0x8000) != 0).mean())
+
+
+def test_probe_lines_match_numpy_restatement(oracle):
+    """The device-only probe lines, byte for byte, against a numpy restatement cut from the
+    (oracle-verified) image: fresh build, spill fallback + big buckets, clustered
+    fingerprints (overflowed lines), incremental merge (64-bit entries)."""
+    kw = {}
+    b = E.FilterBatch(E.routing_config_init(), [300_000], [0])
+    b.build_keys(dev(K.random_keys(300_000, seed=3)), 24)
+    G, ovf = _check_lines(b, b.image(0), kw, 0)
+    assert G >= 8 and ovf < 1e-3
+    keys = K.ids_keys(np.arange(200_000, dtype=np.uint64) % 3)  # spill -> k_cb_sort_big
+    b = E.FilterBatch(E.routing_config_init(), [200_000], [3])
+    b.build_keys(dev(keys), 24)
+    _check_lines(b, b.image(0), kw, 3)
+    # clustered fingerprints: 150 in 4 adjacent buckets overflow their line
+    rng = np.random.default_rng(2)
+    n, rem, sh = 100_000, 26 - 16, 6
+    h = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    for j in range(150):
+        h[j] = np.uint32((((777 + j % 4) << rem) | (j * 7919 % (1 << rem))) << sh)
+    b = E.FilterBatch(E.routing_config_init(), [n], [0])
+    b.build_hashes(dev(h))
+    _, ovf = _check_lines(b, b.image(0), kw, 0)
+    assert ovf > 0
+    kw9 = dict(log_index_size=9, fingerprint_size=28)
+    cfg9 = E.routing_config_init(**kw9)
+    b0 = E.FilterBatch(cfg9, [150_000], [1])
+    b0.build_keys(dev(K.random_keys(150_000, seed=4)), 24)
+    b1 = E.FilterBatch(cfg9, [200_000], [6], old=[(b0, 0)])
+    b1.build_keys(dev(K.random_keys(200_000, seed=5)), 24)
+    _check_lines(b1, b1.image(0), kw9, 6)
+
+
 def test_errors_match_reference_contract():
     cfg = E.routing_config_init()
     with pytest.raises(E.PlatformStatusError) as ei:
