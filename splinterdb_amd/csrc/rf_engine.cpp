@@ -7,6 +7,7 @@
 // device is present.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -125,12 +126,11 @@ static int check_cfg(const rf_amd_config* cfg) {
 static uint32_t vsize_of(uint32_t value) { return value == 0 ? 0 : 32 - __builtin_clz(value); }
 
 // Probe-line group size (k_plines): the largest G = 2^g <= min(IS, 64) whose 64-byte line
-// (16-bit header + n + G encoding bits + n*rvs remainder bits) holds mean + SIGMA sd + 2
+// (128 encoding bits for n + G, 384 remainder bits for n * rvs) holds mean + SIGMA sd + 2
 // entries, n ~ Poisson(lam*G) with lam = fingerprints per bucket (< 2 by the choice of
-// log_num_buckets). Larger G = smaller line table (L2-resident sooner) but more overflowed
-// lines (those probes walk the image). SIGMA: RF_AMD_LINE_SIGMA (tuning knob), default 3.5
-// (lam is an upper bound: at C2 the real overflow margin is 4.5 sd; sigma 5 vs 3 measured
-// the same probe time, so the smaller table wins).
+// log_num_buckets). Larger G = smaller line table but more overflowed lines (those probes
+// walk the image). SIGMA: RF_AMD_LINE_SIGMA (tuning knob), default 3.5 (lam is an upper
+// bound; table size measured not to matter for the probe, overflow rate does).
 // Returns g + 1, or 0 = no lines (rvs > 32: probes walk the image).
 static double line_sigma() {
   const char* e = getenv("RF_AMD_LINE_SIGMA");
@@ -142,7 +142,8 @@ static uint32_t line_log_group(uint32_t lis, uint32_t rvs, double lam) {
   const double sg = line_sigma();
   for (int g = (int)(lis < 6 ? lis : 6); g >= 0; g--) {
     const double G = (double)(1u << g), mean = lam * G;
-    if (mean + sg * sqrt(mean) + 2.0 <= (512.0 - 16.0 - G) / (rvs + 1.0)) return (uint32_t)g + 1;
+    const double cap = rvs ? std::min(128.0 - G, 384.0 / rvs) : 128.0 - G;
+    if (mean + sg * sqrt(mean) + 2.0 <= cap) return (uint32_t)g + 1;
   }
   return 0;
 }

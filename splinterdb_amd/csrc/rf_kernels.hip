@@ -1339,13 +1339,15 @@ __device__ __forceinline__ uint64_t probe_stream(uint32_t bo, uint32_t remainder
 // Device-only, not part of the on-disk image. An index's block is cut into groups of
 // G = 2^(lg_line-1) consecutive buckets; group k of the filter (buckets [kG, kG+G)) gets a
 // 64-byte line at line_base + k:
-//   bits [0,16)        n = entries in the group, or 0x8000 = overflow (use the image)
-//   bits [16,16+n+G)   the group's slice of the unary encoding (0 = entry, 1 = bucket end)
-//   then n x rvs bits  the group's packed remainder|value entries (LSB-first)
+//   bits [0,128)    the group's slice of the unary encoding (0 = entry, 1 = bucket end),
+//                   n + G bits, zero padded; all ones = overflow (probes use the image)
+//   bits [128,512)  the group's n packed remainder|value entries, rvs bits each (LSB-first)
 // Both slices are contiguous bit ranges of the reference block (layout written at
-// src/routing_filter.c:622-633), so a probe touches ONE random 64-byte line instead of the index slot,
-// header, encoding window and remainder run. G is chosen on the host so that overflow is a
-// > 5-sigma event for random fingerprints (engine: line_log_group).
+// src/routing_filter.c:622-633), so a probe touches ONE random 64-byte line instead of the
+// index slot, header, encoding window and remainder run; and because the encoding and the
+// remainders start at fixed offsets, decoding is one 128-bit select, one count of
+// trailing zeros and one 96-bit window. G is chosen on the host so that n + G <= 128 and
+// n * rvs <= 384 hold with margin for random fingerprints (engine: line_log_group).
 __device__ __forceinline__ uint64_t bits64_at(const uint8_t* pg, uint64_t bitpos) {
   const uint64_t by = bitpos >> 3;
   const uint32_t sh = (uint32_t)(bitpos & 7);
@@ -1412,20 +1414,20 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
     const uint32_t gl = u >> 2, qq = u & 3;
     const uint32_t a = s_a[gl], ne = s_a[gl + 1] - a;  // encoding bits of the group = n + G
     const uint32_t n = ne - G, E = a - gl * G;         // entries, first entry of the group
-    const uint32_t R0 = 16 + ne, tot = R0 + n * rvs;
-    const bool ovf = tot > 512;
+    const bool ovf = ne > 128 || (uint64_t)n * rvs > 384;
     uint64_t w[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint32_t o = qq * 128 + h * 64;
-      uint64_t x = (o == 0) ? (ovf ? 0x8000ull : (uint64_t)n) : 0ull;
-      if (!ovf) {
-        uint32_t lo = max(o, 16u), hi = min(o + 64, R0);
-        if (lo < hi) x |= (bits64_at(pg, ebit + a + (lo - 16)) & lowmask64(hi - lo)) << (lo - o);
-        lo = max(o, R0);
-        hi = min(o + 64, tot);
-        if (lo < hi)
-          x |= (bits64_at(pg, rbit0 + (uint64_t)E * rvs + (lo - R0)) & lowmask64(hi - lo)) << (lo - o);
+      uint64_t x = 0;
+      if (ovf) {
+        x = o < 128 ? ~0ull : 0ull;
+      } else if (o < 128) {
+        const uint32_t hi = min(o + 64, ne);
+        if (o < hi) x = bits64_at(pg, ebit + a + o) & lowmask64(hi - o);
+      } else {
+        const uint32_t ro = o - 128, hi = min(ro + 64, n * rvs);
+        if (ro < hi) x = bits64_at(pg, rbit0 + (uint64_t)E * rvs + ro) & lowmask64(hi - ro);
       }
       w[h] = x;
     }
@@ -1434,65 +1436,68 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
   }
 }
 
-// Line probe, decode half: bucket j of the line's group (line bytes in Q); returns false
-// on an overflowed line.
-__device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint32_t G, uint32_t remainder,
-                                            uint32_t vs, uint32_t rvs, uint64_t& found) {
-  uint64_t W[8];
+// position of the r-th (0-based) set bit of x (exists)
+__device__ __forceinline__ uint32_t select32(uint32_t x, uint32_t r) {
+  uint32_t pos = 0;
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    W[2 * k] = (uint64_t)Q[k].x | ((uint64_t)Q[k].y << 32);
-    W[2 * k + 1] = (uint64_t)Q[k].z | ((uint64_t)Q[k].w << 32);
+  for (uint32_t w = 16; w >= 1; w >>= 1) {
+    const uint32_t c = __popc(x & ((1u << w) - 1));
+    const bool up = r >= c;
+    r = up ? r - c : r;
+    x = up ? x >> w : x;
+    pos = up ? pos + w : pos;
   }
-  const uint32_t hdr = (uint32_t)W[0] & 0xffffu;
-  if (hdr & 0x8000u) return false;
-  const uint32_t n = hdr;
-  W[0] &= ~0xffffull;
-  // line positions of bucket terminators #(j-1) and #j (ranks among the line's 1-bits; the
-  // first G of them are the group's terminators, so remainder bits never interfere)
-  const uint32_t r2 = j, r1 = j ? j - 1 : 0;
-  uint32_t j1 = 8, j2 = 8, c1 = 0, cum = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t pc = __popcll(W[k]);
-    const bool h1 = (j1 == 8) && (cum + pc > r1);
-    const bool h2 = (j2 == 8) && (cum + pc > r2);
-    c1 = h1 ? cum : c1;
-    j1 = h1 ? (uint32_t)k : j1;
-    j2 = h2 ? (uint32_t)k : j2;
-    cum += pc;
+  return pos;
+}
+
+// Line probe, decode half (format above): bucket j of the line's group, line bytes in Q.
+// Returns false when the image must be walked instead (overflowed line, or a bucket too
+// large for the 96-bit remainder window).
+__device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint32_t remainder, uint32_t vs,
+                                            uint32_t rvs, uint64_t& found) {
+  const uint32_t d0 = Q[0].x, d1 = Q[0].y, d2 = Q[0].z, d3 = Q[0].w;
+  if ((d0 & d1 & d2 & d3) == 0xffffffffu) return false;  // overflow marker
+  // p1 = first bit after terminator j-1 (0 for bucket 0); entries before bucket j = p1 - j
+  uint32_t p1 = 0;
+  if (j) {
+    const uint32_t r = j - 1, c0 = __popc(d0), c1 = c0 + __popc(d1), c2 = c1 + __popc(d2);
+    const uint32_t x = r >= c2 ? d3 : (r >= c1 ? d2 : (r >= c0 ? d1 : d0));
+    const uint32_t base = r >= c2 ? 96u : (r >= c1 ? 64u : (r >= c0 ? 32u : 0u));
+    const uint32_t rr = r - (r >= c2 ? c2 : (r >= c1 ? c1 : (r >= c0 ? c0 : 0u)));
+    p1 = base + select32(x, rr) + 1;
   }
-  auto pick8 = [&](uint32_t i) {
-    uint64_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) r |= W[k] & (0ull - (uint64_t)(i == (uint32_t)k));
-    return r;
-  };
+  const uint32_t s = p1 - j;
+  // c = entries of bucket j = zeros from p1 up to terminator j
+  const uint32_t q = p1 >> 5, sh = p1 & 31;
+  const uint64_t lo = q == 0 ? ((uint64_t)d1 << 32 | d0)
+                             : (q == 1 ? ((uint64_t)d2 << 32 | d1) : (q == 2 ? ((uint64_t)d3 << 32 | d2) : d3));
+  const uint32_t hi = q == 0 ? d2 : (q == 1 ? d3 : 0u);
+  const uint64_t y = (lo >> sh) | (sh ? (uint64_t)hi << (64 - sh) : 0ull);
+  if (y == 0) return false;
+  const uint32_t c = (uint32_t)__builtin_ctzll(y);
   found = 0;
-  if (j2 == 8) return true;  // corrupt line: never read out of range
-  const uint64_t x1 = pick8(j1);
-  const uint32_t q1 = 64u * j1 + select64_fast(x1, r1 - c1);
-  uint32_t q2;
-  if (r2 == 0) {
-    q2 = q1;
-  } else if (j2 == j1) {
-    const uint32_t b1 = q1 & 63;
-    const uint64_t rest = b1 == 63 ? 0ull : (x1 & (~0ull << (b1 + 1)));
-    q2 = 64u * j1 + (uint32_t)__builtin_ctzll(rest);
-  } else {
-    q2 = 64u * j2 + (uint32_t)__builtin_ctzll(pick8(j2));
+  if (c == 0 || rvs == 0) {
+    if (c && remainder == 0) found = 1;  // rvs == 0: every entry matches, value 0
+    return true;
   }
-  const uint32_t start = j ? q1 - 15 - j : 0u;  // zeros before terminator j-1
-  const uint32_t end = q2 - 16 - j;             // zeros before terminator j
-  const uint32_t R0 = 16 + n + G;
+  // the bucket's remainders: bits [s*rvs, (s+c)*rvs) of the 384-bit remainder area
+  const uint32_t b = s * rvs, wi = b >> 5, off = b & 31;
+  if (off + c * rvs > 96 || b + c * rvs > 384) return false;
+  const uint32_t R[12] = {Q[1].x, Q[1].y, Q[1].z, Q[1].w, Q[2].x, Q[2].y,
+                          Q[2].z, Q[2].w, Q[3].x, Q[3].y, Q[3].z, Q[3].w};
+  uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 12; k++) {  // 96-bit window at dword wi (branch-free picks)
+    w0 = wi == k ? R[k] : w0;
+    w1 = wi + 1 == k ? R[k] : w1;
+    w2 = wi + 2 == k ? R[k] : w2;
+  }
+  const uint64_t wl = (uint64_t)w1 << 32 | w0;
   const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
   const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
-  for (uint32_t pos = start; pos < end; pos++) {
-    const uint32_t bb = R0 + pos * rvs;
-    if (bb + rvs > 512) break;  // corrupt line
-    const uint32_t wi = bb >> 6, sh = bb & 63;
-    uint64_t v = pick8(wi) >> sh;
-    if (sh + rvs > 64) v |= pick8(wi + 1) << (64 - sh);
+  for (uint32_t k = 0; k < c; k++) {
+    const uint32_t qb = off + k * rvs;  // < 96
+    const uint64_t v = qb < 64 ? ((wl >> qb) | (qb ? (uint64_t)w2 << (64 - qb) : 0ull)) : (uint64_t)(w2 >> (qb - 64));
     const uint32_t rv = (uint32_t)v & rvmask;
     if ((rv >> vs) == remainder) {
       const uint32_t val = rv & vmask;
@@ -1566,7 +1571,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
       for (int k = 0; k < 4; k++) Q[q][k] = lp[k];
     } else {
 #pragma unroll
-      for (int k = 0; k < 4; k++) Q[q][k] = v4u{0x8000u, 0u, 0u, 0u};  // "overflowed": image path
+      for (int k = 0; k < 4; k++) Q[q][k] = v4u{~0u, ~0u, ~0u, ~0u};  // "overflowed": image path
     }
   }
 #pragma unroll
@@ -1583,7 +1588,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     } else {
       const uint32_t vs = pp[q].x & 0xff, rvs = (pp[q].x >> 16) & 0xff, lgl = pp[q].x >> 24;
       const uint32_t G = lgl ? 1u << (lgl - 1) : 1u;
-      if (!lgl || !line_decode(Q[q], bucket[q] & (G - 1), G, remainder[q], vs, rvs, r)) {
+      if (!lgl || !line_decode(Q[q], bucket[q] & (G - 1), remainder[q], vs, rvs, r)) {
         // overflowed line (or no lines): walk the image from the index slot
         const uint64_t hdr = slots[pp[q].z + (bucket[q] >> lis)];
         const uint8_t* pg = pages + (uint64_t)plans[fid[q]].page_base * page_size;

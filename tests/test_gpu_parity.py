@@ -317,8 +317,9 @@ def test_probe_line_overflow_falls_back_to_image(oracle):
 
 def expected_probe_lines(pages, slots, num_indices, IS, G, rvs):
     """numpy restatement of the device-only probe-line format (rf_kernels.hip, "probe
-    lines"), cut from a filter image: per group of G buckets, a 16-bit header (entry count,
-    or 0x8000 = overflow), the group's slice of the unary encoding, its packed remainders."""
+    lines"), cut from a filter image: per group of G buckets, bits [0,128) the group's slice
+    of the unary encoding (zero padded; all ones = overflow), bits [128,512) its packed
+    remainders."""
     bits = np.unpackbits(pages, bitorder="little")
     L = IS // G
     out = np.zeros((num_indices * L, 64), dtype=np.uint8)
@@ -334,13 +335,12 @@ def expected_probe_lines(pages, slots, num_indices, IS, G, rvs):
             end = int(ones[g * G + G - 1]) + 1
             ne = end - a
             n, E = ne - G, a - g * G
-            tot = 16 + ne + n * rvs
             line = np.zeros(512, dtype=np.uint8)
-            hdr = 0x8000 if tot > 512 else n
-            if tot <= 512:
-                line[16:16 + ne] = enc[a:end]
-                line[16 + ne:tot] = bits[r0 + E * rvs: r0 + (E + n) * rvs]
-            line[:16] = [(hdr >> k) & 1 for k in range(16)]
+            if ne > 128 or n * rvs > 384:
+                line[:128] = 1
+            else:
+                line[:ne] = enc[a:end]
+                line[128:128 + n * rvs] = bits[r0 + E * rvs: r0 + (E + n) * rvs]
             out[i * L + g] = np.packbits(line, bitorder="little")
     return out
 
@@ -359,8 +359,7 @@ def _check_lines(b, img, cfg_kw, value):
     assert bad.size == 0, f"{bad.size} of {lines.shape[0]} lines differ, first {bad[:5]}"
     b.debug_rebuild_lines()  # the image-upload path re-cuts the same lines
     assert (b.debug_lines() == want).all()
-    hdr = want[:, 0].astype(np.uint32) | (want[:, 1].astype(np.uint32) << 8)
-    return G, float(((hdr & 0x8000) != 0).mean())
+    return G, float((want[:, :16] == 0xFF).all(axis=1).mean())
 
 
 def test_probe_lines_match_numpy_restatement(oracle):
