@@ -75,6 +75,7 @@ struct rf_amd_batch {
   uint64_t E = 0, keys_total = 0;
   uint32_t CB = 0, I = 0, PS = 0, PF = 0;
   uint64_t NL = 0;         // probe lines (64 B each)
+  bool plines_needed = false;  // some filter's lines come from k_plines
   uint32_t line_lmax = 0;  // max probe lines per index
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
@@ -132,6 +133,15 @@ static uint32_t vsize_of(uint32_t value) { return value == 0 ? 0 : 32 - __builti
 // walk the image). SIGMA: RF_AMD_LINE_SIGMA (tuning knob), default 3.5 (lam is an upper
 // bound; table size measured not to matter for the probe, overflow rate does).
 // Returns g + 1, or 0 = no lines (rvs > 32: probes walk the image).
+// K6 cuts a filter's probe lines from its LDS page images when the per-page group table
+// fits (blocks per page <= page_size / smallest block, each with IS/G + 1 entries).
+static bool lines_in_assembly(uint32_t lis, uint32_t lg_line, uint32_t page_size) {
+  const uint32_t IS = 1u << lis, L = IS >> (lg_line - 1);
+  const uint32_t min_block = 2 + (IS - 1) / 8 + 4 + 3;
+  const uint32_t maxb = page_size / min_block + 1;
+  return maxb <= ASM_MAXB_HOST && (uint64_t)maxb * (L + 1) <= ASM_GT_HOST;
+}
+
 static double line_sigma() {
   const char* e = getenv("RF_AMD_LINE_SIGMA");
   const double v = e ? atof(e) : 0.0;
@@ -221,6 +231,8 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     p.pf_base = pf_base;
     p.lg_line = line_log_group(lis, p.rvs, (double)nfp / (double)(1ull << lnb));
     p.line_base = (uint32_t)line_base;
+    p.lines_asm = p.lg_line && lines_in_assembly(lis, p.lg_line, P);
+    if (p.lg_line && !p.lines_asm) b->plines_needed = true;
     if (p.lg_line) {
       line_base += (uint64_t)p.num_indices << (lis - (p.lg_line - 1));
       b->line_lmax = std::max(b->line_lmax, IS >> (p.lg_line - 1));
@@ -377,6 +389,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.slots = b->d_slots.as<uint64_t>();
   a.lines = b->d_lines.as<uint4>();
   a.line_lmax = b->line_lmax;
+  a.plines_needed = b->plines_needed ? 1u : 0u;
   a.idx_filter = b->d_idx_filter.as<uint32_t>();
   a.num_idx = b->I;
   a.page_first = b->d_page_first.as<uint32_t>();
@@ -495,6 +508,7 @@ extern "C" int rf_amd_debug_rebuild_lines(rf_amd_batch* b) {
   HIPCHK(hipDeviceSynchronize());
   (void)hipGetLastError();
   LaunchArgs a = make_args(b, b->eng->stream);
+  a.plines_force = 1;  // every filter, also those whose lines K6 cut
   if (int rc = rf_launch_plines(&a)) return fail(RF_AMD_EINVAL, std::string("probe-line launch: ") + hipGetErrorString((hipError_t)rc));
   HIPCHK(hipStreamSynchronize(b->eng->stream));
   return 0;
@@ -626,6 +640,7 @@ static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf
   if (p.lg_line) {
     b->NL = (uint64_t)p.num_indices << (lis - (p.lg_line - 1));
     b->line_lmax = (1u << lis) >> (p.lg_line - 1);
+    b->plines_needed = true;  // uploaded image: lines are cut by k_plines
   }
   int rc = b->d_plans.alloc(sizeof(FilterPlan));
   rc |= b->d_pplans.alloc(16);

@@ -69,6 +69,18 @@ __device__ __forceinline__ uint32_t hash_key(const void* __restrict__ in0, const
   }
 }
 
+// position of the r-th (0-based) set bit of x (exists)
+__device__ __forceinline__ uint32_t select64_fast(uint64_t x, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = __popcll(x & ((1ull << w) - 1));
+    if (r >= c) { r -= c; x >>= w; pos += w; }
+  }
+  return pos;
+}
+__device__ __forceinline__ uint64_t lowmask64(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
+
 // ======================================================================================
 // K1: hash + coarse-bucket histogram
 // ======================================================================================
@@ -922,7 +934,8 @@ __device__ __forceinline__ void lds_or_bits(uint32_t* s, uint64_t bitpos, uint32
 }
 
 // Fallback for pages with more blocks / entries than the word-parallel path stages in LDS
-// (tiny index_size or rvs): bits OR-ed into an LDS page image with atomics.
+// (tiny index_size or rvs): bits OR-ed into the LDS page image s_pg with atomics (the
+// caller stores it).
 __device__ __forceinline__ void assemble_atomic(const FilterPlan& P, uint32_t p, uint32_t slot, uint32_t b0,
                                                 uint32_t b1, const uint32_t* __restrict__ idx_cnt,
                                                 const uint32_t* __restrict__ idx_start,
@@ -968,15 +981,19 @@ __device__ __forceinline__ void assemble_atomic(const FilterPlan& P, uint32_t p,
       lds_or_bits(s_pg, rbit + (uint64_t)k * P.rvs, rv, P.rvs);
     }
   }
-  __syncthreads();
-  uint4* dst = reinterpret_cast<uint4*>(pages + (uint64_t)slot * page_size);
-  const uint4* src = reinterpret_cast<const uint4*>(s_pg);
-  for (uint32_t i = threadIdx.x; i < page_size / 16; i += ASM_NT) dst[i] = src[i];
 }
 
 constexpr uint32_t ASM_MAXB = 512;  // blocks per page held in LDS (more: assemble_atomic)
 constexpr uint32_t ASM_RUN = 16;    // entries per thread-run in phase C
 constexpr uint32_t ASM_MAXE = 16384;  // entries per page covered by the run table
+constexpr uint32_t ASM_GT = 4096;     // group-start table entries per page (lines_asm bound)
+
+// 64 bits of the LDS page image from bit `bitpos` (the image has 4 words of tail padding)
+__device__ __forceinline__ uint64_t lds_bits64(const uint32_t* s_pg, uint32_t bitpos) {
+  const uint32_t w = bitpos >> 5, sh = bitpos & 31;
+  const uint64_t lo = ((uint64_t)s_pg[w + 1] << 32) | s_pg[w];
+  return (lo >> sh) | (sh ? (uint64_t)s_pg[w + 2] << (64 - sh) : 0ull);
+}
 
 // One workgroup per page. (A) block metadata in LDS. (B) word-parallel fill of the LDS page
 // image: header counts, 0xFF encodings, zeros -- plain stores. (C) entry runs: a thread
@@ -994,9 +1011,11 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
                                                      const uint64_t* __restrict__ slots,
                                                      const uint32_t* __restrict__ page_first,
                                                      const FilterOut* __restrict__ outs,
-                                                     uint8_t* __restrict__ pages, uint32_t lis,
-                                                     uint32_t page_size) {
+                                                     uint8_t* __restrict__ pages, uint4* __restrict__ lines,
+                                                     uint32_t lis, uint32_t page_size) {
   __shared__ __attribute__((aligned(16))) uint32_t s_pg[MAX_PAGE / 4 + 4];
+  __shared__ uint16_t s_gs[ASM_GT];  // per block: bit after each line group's last terminator
+  __shared__ uint32_t s_wpre[ASM_MAXB];
   __shared__ uint32_t s_off[ASM_MAXB + 1];
   __shared__ uint32_t s_c[ASM_MAXB];
   __shared__ uint32_t s_est[ASM_MAXB + 1];
@@ -1010,8 +1029,11 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   if (outs[f].error || p >= outs[f].num_pages) return;
   const uint32_t* pf = page_first + P.pf_base;
   const uint32_t b0 = pf[p], b1 = pf[p + 1], nb = b1 - b0;
-  if (nb > ASM_MAXB) {
+  uint4* dst = reinterpret_cast<uint4*>(pages + (uint64_t)slot * page_size);
+  if (nb > ASM_MAXB) {  // (never with lines_asm: the host bounds blocks per page for it)
     assemble_atomic(P, p, slot, b0, b1, idx_cnt, idx_start, sorted32, slots, pages, lis, page_size, s_pg);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < page_size / 16; i += ASM_NT) dst[i] = reinterpret_cast<const uint4*>(s_pg)[i];
     return;
   }
   const uint32_t IS = 1u << lis, rvs = P.rvs;
@@ -1042,8 +1064,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   if (ne > ASM_MAXE) {  // uniform (scan total)
     __syncthreads();
     assemble_atomic(P, p, slot, b0, b1, idx_cnt, idx_start, sorted32, slots, pages, lis, page_size, s_pg);
-    return;
-  }
+  } else {
   __syncthreads();
   // run table: block of each run's first entry
 #pragma unroll
@@ -1153,11 +1174,95 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
     flush_e();
     flush_r();
   }
+  }  // word-parallel path
   __syncthreads();
   // (D) store
-  uint4* dst = reinterpret_cast<uint4*>(pages + (uint64_t)slot * page_size);
   const uint4* srcp = reinterpret_cast<const uint4*>(s_pg);
   for (uint32_t i = threadIdx.x; i < page_size / 16; i += ASM_NT) dst[i] = srcp[i];
+  if (!P.lines_asm) return;
+  // (E) probe lines of the page's blocks, cut from the LDS image (format: "probe lines").
+  // E1: popcount scan over the blocks' encoding words -> group boundaries in s_gs.
+  const uint32_t lgG = P.lg_line - 1, G = 1u << lgG, L = IS >> lgG;
+  uint32_t wc[2], wsum = 0;  // encoding words per block (2 blocks per thread)
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint32_t j = threadIdx.x * 2 + q;
+    wc[q] = j < nb ? (s_c[j] + IS + 63) / 64 : 0u;
+    wsum += wc[q];
+  }
+  uint32_t nw;
+  uint32_t wrun = block_excl_scan<ASM_NT>(wsum, s_tmp, &nw);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint32_t j = threadIdx.x * 2 + q;
+    if (j < nb) {
+      s_est[j] = wrun;  // reused: first encoding word item of block j
+      s_gs[j * (L + 1)] = 0;
+      s_gs[j * (L + 1) + L] = (uint16_t)(s_c[j] + IS);
+    }
+    wrun += wc[q];
+  }
+  if (threadIdx.x == 0) s_est[nb] = nw;
+  __syncthreads();
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < nw; base += ASM_NT) {
+    const uint32_t it = base + threadIdx.x;
+    uint32_t j = 0, w = 0, ones = 0;
+    uint64_t x = 0;
+    if (it < nw) {
+      uint32_t lo = 0, hi = nb;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_est[mid] <= it) lo = mid; else hi = mid;
+      }
+      j = lo;
+      w = it - s_est[j];
+      const uint32_t nbits = s_c[j] + IS, b = w * 64;
+      x = lds_bits64(s_pg, (s_off[j] + 2) * 8 + b);
+      if (nbits - b < 64) x &= (1ull << (nbits - b)) - 1;
+      ones = __popcll(x);
+    }
+    uint32_t tot;
+    const uint32_t ex_all = block_excl_scan<ASM_NT>(ones, s_tmp, &tot) + carry;
+    carry += tot;
+    // prefix inside block j = ex_all - ex_all of the block's first word (this pass or earlier)
+    if (it < nw && w == 0) s_wpre[j] = ex_all;
+    __syncthreads();
+    if (it < nw) {
+      const uint32_t ex = ex_all - s_wpre[j];
+      for (uint32_t k = (ex + G) >> lgG; k < L && k * G - 1 < ex + ones; k++)
+        s_gs[j * (L + 1) + k] = (uint16_t)(w * 64 + select64_fast(x, k * G - 1 - ex) + 1);
+    }
+    __syncthreads();
+  }
+  // E2: 4 lanes per line, 16 bytes each
+  const uint32_t nt = nb * L * 4;
+  for (uint32_t u = threadIdx.x; u < nt; u += ASM_NT) {
+    const uint32_t j = u / (L * 4), rest = u - j * (L * 4), gl = rest >> 2, qq = rest & 3;
+    const uint32_t c = s_c[j];
+    const uint32_t ebit = (s_off[j] + 2) * 8, rbit = (s_off[j] + 2 + (c + IS - 1) / 8 + 4) * 8;
+    const uint32_t a = s_gs[j * (L + 1) + gl], ne2 = s_gs[j * (L + 1) + gl + 1] - a;
+    const uint32_t n = ne2 - G, E = a - gl * G;
+    const bool ovf = ne2 > 128 || n * rvs > 384;
+    uint64_t wv[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t o = qq * 128 + h * 64;
+      uint64_t x = 0;
+      if (ovf) {
+        x = o < 128 ? ~0ull : 0ull;
+      } else if (o < 128) {
+        const uint32_t hi = min(o + 64, ne2);
+        if (o < hi) x = lds_bits64(s_pg, ebit + a + o) & lowmask64(hi - o);
+      } else {
+        const uint32_t ro = o - 128, hi = min(ro + 64, n * rvs);
+        if (ro < hi) x = lds_bits64(s_pg, rbit + E * rvs + ro) & lowmask64(hi - ro);
+      }
+      wv[h] = x;
+    }
+    const uint64_t line = (uint64_t)P.line_base + (uint64_t)(b0 + j) * L + gl;
+    lines[line * 4 + qq] = make_uint4((uint32_t)wv[0], (uint32_t)(wv[0] >> 32), (uint32_t)wv[1], (uint32_t)(wv[1] >> 32));
+  }
 }
 
 // ======================================================================================
@@ -1259,16 +1364,7 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
 // ======================================================================================
 // Probe: routing_filter_lookup (src/routing_filter.c:985-1073), one lane per probe
 // ======================================================================================
-// select: position of the r-th (0-based) set bit of x, by popcount bisection
-__device__ __forceinline__ uint32_t select64_fast(uint64_t x, uint32_t r) {
-  uint32_t pos = 0;
-#pragma unroll
-  for (uint32_t w = 32; w >= 1; w >>= 1) {
-    const uint32_t c = __popcll(x & ((1ull << w) - 1));
-    if (r >= c) { r -= c; x >>= w; pos += w; }
-  }
-  return pos;
-}
+// position of the r-th (0-based) set bit of the 128-bit value hi:lo
 __device__ __forceinline__ uint32_t select128(uint64_t lo, uint64_t hi, uint32_t r) {
   const uint32_t c = __popcll(lo);
   return r < c ? select64_fast(lo, r) : 64 + select64_fast(hi, r - c);
@@ -1355,7 +1451,6 @@ __device__ __forceinline__ uint64_t bits64_at(const uint8_t* pg, uint64_t bitpos
   if (sh) x |= (uint64_t)pg[by + 8] << (64 - sh);
   return x;
 }
-__device__ __forceinline__ uint64_t lowmask64(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
 
 // One wave per index (4 per workgroup). Phase 1: popcount-prefix over the encoding, the
 // position after each group's last bucket terminator -> LDS. Phase 2: 4 lanes per line,
@@ -1366,14 +1461,15 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
                                                 const uint8_t* __restrict__ pages,
                                                 const FilterOut* __restrict__ outs,
                                                 uint4* __restrict__ lines, uint32_t num_idx,
-                                                uint32_t lmax, uint32_t lis, uint32_t page_size) {
+                                                uint32_t lmax, uint32_t lis, uint32_t page_size,
+                                                uint32_t force) {
   extern __shared__ uint32_t s_dyn[];
   const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   const uint32_t g = blockIdx.x * (blockDim.x / WAVE) + wv;
   uint32_t* s_a = s_dyn + wv * (lmax + 1);
   const uint32_t f = g < num_idx ? idx_filter[g] : 0u;
   const FilterPlan& P = plans[f];
-  const bool active = g < num_idx && P.lg_line != 0 && !(outs && outs[f].error) &&
+  const bool active = g < num_idx && P.lg_line != 0 && (force || !P.lines_asm) && !(outs && outs[f].error) &&
                       g - P.idx_base < P.num_indices;
   const uint32_t IS = 1u << lis;
   const uint32_t lgG = active ? P.lg_line - 1 : 0u, G = 1u << lgG, L = IS >> lgG;
@@ -1708,10 +1804,11 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
   CHECK_LAUNCH();
   REC(EV_B_LAYOUT);
   hipLaunchKernelGGL(k_assemble, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans, a.pg_filter,
-                     a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages, a.lis,
-                     a.page_size);
+                     a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages, a.lines,
+                     a.lis, a.page_size);
   CHECK_LAUNCH();
-  if (int rc = rf_launch_plines(&a)) return rc;
+  if (a.plines_needed)
+    if (int rc = rf_launch_plines(&a)) return rc;
   REC(EV_B_ASSEMBLE);
   return 0;
 }
@@ -1722,7 +1819,7 @@ extern "C" int rf_launch_plines(const LaunchArgs* pa) {
   const size_t lds = 4ull * (256 / WAVE) * (a.line_lmax + 1);
   hipLaunchKernelGGL(k_plines, dim3((a.num_idx + 3) / 4), dim3(256), lds, (hipStream_t)a.stream, a.plans,
                      a.idx_filter, a.slots, a.pages, a.outs, a.lines, a.num_idx, a.line_lmax, a.lis,
-                     a.page_size);
+                     a.page_size, a.plines_force);
   CHECK_LAUNCH();
   return 0;
 }

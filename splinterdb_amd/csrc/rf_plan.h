@@ -24,6 +24,8 @@ constexpr int BIG_NT = 1024;
 constexpr int BIG_GRID = 64;
 constexpr int LAYOUT_NT = 1024;
 constexpr int ASM_NT = 256;
+constexpr uint32_t ASM_MAXB_HOST = 512;  // = ASM_MAXB in rf_kernels.hip (blocks per page in LDS)
+constexpr uint32_t ASM_GT_HOST = 4096;   // = ASM_GT (group-start table entries per page)
 
 enum InputKind { IN_KEYS24 = 0, IN_KEYS_W = 1, IN_KEYS_B = 2, IN_VAR = 3, IN_HASH = 4 };
 
@@ -43,6 +45,7 @@ struct FilterPlan {
   uint32_t cb_base, idx_base, page_base, page_cap, pf_base;
   // probe lines (device-only, 64 B per group of 2^(lg_line-1) buckets; lg_line 0 = none)
   uint32_t lg_line, line_base;
+  uint32_t lines_asm;  // 1: K6 cuts this filter's lines from its LDS page images; 0: k_plines
   // old filter (incremental add)
   uint32_t old_num_indices, old_vs, old_rvs, npo;  // npo = new indices per old index
   const uint8_t* old_pages;
@@ -90,6 +93,8 @@ struct LaunchArgs {
   uint64_t* slots;
   uint4* lines;             // device-only probe lines (64 B = 4 x uint4 each)
   uint32_t line_lmax;       // max lines per index over the batch (k_plines LDS sizing)
+  uint32_t plines_needed;   // some filter's lines come from k_plines
+  uint32_t plines_force;    // k_plines over every filter (diagnostics)
   const uint32_t* idx_filter;
   uint32_t num_idx;
   uint32_t* page_first;
