@@ -67,8 +67,7 @@ def parse():
 def stage_bytes(stage, N, P, image_bytes, slot_bytes, unique):
     """Algorithmic bytes per launch of each stage (DESIGN.md 'Roofline')."""
     return {
-        "hash_count": N * 24 + N * 4,          # read keys, write entries
-        "scatter": N * 8,                      # read + write entries
+        "partition": N * 24 + N * 4,           # fused K1+K3: read keys, write bucketed entries
         "cb_sort": N * 4 + unique * 4,         # read bucketed entries, write sorted unique
         "assemble": unique * 4 + image_bytes,  # read sorted entries, write pages
         "probe": P * 24 + P * 8 + image_bytes + slot_bytes,  # SURVEY.md §8(d) probe figure
@@ -212,13 +211,13 @@ def main():
 
     ms = {k: float(np.mean(v)) for k, v in stages.items()}
     kern = {}
-    for k in ("hash_count", "scatter", "cb_sort", "cb_sort_big", "layout", "assemble", "cb_scan", "probe"):
+    for k in ("partition", "count_scan", "scatter", "cb_sort", "cb_sort_big", "layout", "assemble", "probe"):
         b = stage_bytes(k, N, N, image_bytes, slot_bytes, unique)
         kern[k] = {"ms": round(ms[k], 4)}
         if b:
             kern[k]["alg_bytes"] = int(b)
             kern[k]["gbs"] = round(b / (ms[k] * 1e-3) / 1e9, 1) if ms[k] > 0 else None
-    dom = max(("hash_count", "scatter", "cb_sort", "assemble", "probe"), key=lambda k: ms[k])
+    dom = max(("partition", "cb_sort", "assemble", "probe"), key=lambda k: ms[k])
     achieved = kern[dom]["gbs"]
     traffic = None
     if os.path.exists(args.pmc):

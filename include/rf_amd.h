@@ -110,8 +110,10 @@ int rf_amd_batch_image_ptrs(rf_amd_batch *b, uint32_t f, void **d_pages, void **
 uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
 
 /* per-stage timing with HIP events recorded on the launch stream. Stages of the last
- * build: 0 hash+histogram, 1 bucket scan, 2 scatter, 3 bucket sort, 4 big-bucket sort,
- * 5 layout, 6 page assembly + probe lines, 7 whole build; 8 = last probe kernel.
+ * build: 0 partition (fresh builds: fused hash + coarse-bucket partition; incremental: hash
+ * + histogram), 1 count/scan (fresh: spill fallback only), 2 scatter (fresh: spill fallback
+ * only), 3 bucket sort, 4 big-bucket sort, 5 layout, 6 page assembly + probe lines, 7 whole
+ * build; 8 = last probe kernel.
  * Milliseconds, -1 if a stage did not run. */
 #define RF_AMD_NUM_TIMINGS 9
 int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);

@@ -15,9 +15,9 @@ import csv
 import json
 import sys
 
-SHORT = {"k_hash_count": "hash_count", "k_scatter": "scatter", "k_cb_sort<": "cb_sort",
-         "k_cb_sort_big": "cb_sort_big", "k_layout": "layout", "k_assemble": "assemble",
-         "k_probe": "probe", "k_cb_scan": "cb_scan"}
+SHORT = {"k_hash_scatter": "partition", "k_hash_count": "count_fallback", "k_scatter": "scatter_fallback",
+         "k_cb_sort<": "cb_sort", "k_cb_sort_big": "cb_sort_big", "k_layout": "layout",
+         "k_assemble": "assemble", "k_plines": "plines", "k_probe": "probe", "k_cb_scan": "count_scan"}
 
 
 def short(name):

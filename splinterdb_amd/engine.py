@@ -389,7 +389,11 @@ class FilterBatch:
         _check(load_library().rf_amd_batch_probe_hashes(self.h, _dptr(d_hashes), _dptr(d_filter_id),
                                                         n, _dptr(d_found), _stream(stream)))
 
-    STAGES = ["hash_count", "cb_scan", "scatter", "cb_sort", "cb_sort_big", "layout",
+    # fresh builds: partition = fused hash + coarse-bucket partition (K1+K3); count_scan and
+    # scatter = the spill fallback (near zero unless a coarse bucket overflowed); incremental
+    # builds: partition = K1 count, count_scan = K2, scatter = K3. assemble includes the
+    # probe lines.
+    STAGES = ["partition", "count_scan", "scatter", "cb_sort", "cb_sort_big", "layout",
               "assemble", "build_total", "probe"]
 
     def set_timing(self, enable=True):
