@@ -156,6 +156,53 @@ int  rf_amd_filter_lookup_keys(rf_amd_engine *e, const rf_amd_config *cfg,
                                uint64_t n, uint64_t *found_values);
 void rf_amd_image_free(rf_amd_image *img);
 
+/* ---- routing_filter_estimate_unique_fp (src/routing_filter.h:169-175, .c:702-848) ------
+ * Distinct fingerprints among the first 1/16 of the indices of up to 32 filters, times 16
+ * (leaf-split sizing, src/trunk.c:4506). Filters with pages == NULL (filter.addr == 0) or
+ * fewer than 16 indices contribute nothing, as in the reference. EINVAL: NULL out-param
+ * (STATUS_BAD_PARAM, :710-714), more than MAX_FILTERS = 32 filters, or more decoded entries
+ * than num_fingerprints / 12 (the reference asserts, :776-780). */
+int rf_amd_estimate_unique_fp(rf_amd_engine *e, const rf_amd_config *cfg, const rf_amd_image *filters,
+                              uint64_t num_filters, uint32_t *num_unique_fp);
+/* same over device-resident filters: filter i = (batches[i], filter_index[i]); a NULL
+ * batches[i] is NULL_ROUTING_FILTER. All batches share one engine and routing config. */
+int rf_amd_batch_estimate_unique_fp(rf_amd_batch *const *batches, const uint32_t *filter_index,
+                                    uint64_t num_filters, uint32_t *num_unique_fp);
+/* routing_filter_estimate_unique_keys (src/routing_filter.h:165-167, .c:1141-1146) */
+uint32_t rf_amd_estimate_unique_keys(const rf_amd_filter_info *filter, const rf_amd_config *cfg);
+
+/* ---- asynchronous lookups (routing_filter_lookup_async, src/routing_filter.h:130-155,
+ * .c:895-972) ---------------------------------------------------------------------------
+ * The reference's lookup coroutine returns ASYNC_STATUS_RUNNING while it waits for a page
+ * and calls callback(callback_arg) when it can be resumed. Here one call starts a whole
+ * batch of lookups against a built (device-resident) batch: host keys are staged through
+ * pinned memory to HBM, probed, and the found_values bit-vectors copied back into h_found,
+ * all on `stream` (NULL = the engine's). When h_found is complete, callback(callback_arg)
+ * runs on a HIP runtime thread (it must not call HIP). h_filter_id == NULL probes filter 0.
+ * poll returns RF_AMD_ASYNC_RUNNING / RF_AMD_ASYNC_DONE (async_status order); free waits for
+ * completion first. The keys buffer may be reused as soon as rf_amd_lookup_async returns. */
+#define RF_AMD_ASYNC_RUNNING 0
+#define RF_AMD_ASYNC_DONE    1
+typedef void (*rf_amd_callback_fn)(void *arg);
+typedef struct rf_amd_lookup_async_state rf_amd_lookup_async_state;
+int  rf_amd_lookup_async(rf_amd_batch *b, const void *h_keys, uint32_t key_len,
+                         const uint32_t *h_filter_id, uint64_t n, uint64_t *h_found,
+                         rf_amd_callback_fn callback, void *callback_arg, void *stream,
+                         rf_amd_lookup_async_state **state);
+int  rf_amd_lookup_async_poll(rf_amd_lookup_async_state *state);
+int  rf_amd_lookup_async_wait(rf_amd_lookup_async_state *state);
+void rf_amd_lookup_async_free(rf_amd_lookup_async_state *state);
+
+/* ---- debug functions (src/routing_filter.h:185-192) ------------------------------------
+ * rf_amd_filter_verify replaces routing_filter_verify (.c:1163-1183): every key must find
+ * `value`; returns EINVAL (the reference asserts) with *num_missing keys that did not.
+ * rf_amd_filter_print replaces routing_filter_print (.c:1260-1286), same text (slots are
+ * relocatable), to out_file (a FILE *, NULL = stdout). */
+int rf_amd_filter_verify(rf_amd_engine *e, const rf_amd_config *cfg, const rf_amd_image *filter,
+                         const void *keys, uint32_t key_len, uint64_t n, uint16_t value,
+                         uint64_t *num_missing);
+int rf_amd_filter_print(const rf_amd_config *cfg, const rf_amd_image *filter, void *out_file);
+
 /* host-side helpers mirroring routing_filter.h (no GPU work) */
 uint64_t rf_amd_max_fingerprints(const rf_amd_config *cfg);              /* .h:120-127  */
 uint32_t rf_amd_estimate_unique_keys_from_count(const rf_amd_config *cfg,

@@ -189,7 +189,8 @@ def filter_add(cfg, hashes: np.ndarray, value=0, old: OracleFilter = None):
 
 
 def estimate_unique_fp(cfg, filters):
-    arr = (Filter * len(filters))(*[f.f for f in filters])
+    """None entries are NULL_ROUTING_FILTER (addr 0: skipped, :739-742)."""
+    arr = (Filter * max(1, len(filters)))(*[(f.f if f is not None else Filter()) for f in filters])
     out = ctypes.c_uint32(0)
     rc = lib().rfo_estimate_unique_fp(ctypes.byref(cfg), arr, len(filters), ctypes.byref(out))
     if rc:

@@ -794,3 +794,328 @@ extern "C" uint64_t rf_amd_space_use_bytes(const rf_amd_config* cfg, uint32_t nu
   const uint64_t extent = (uint64_t)cfg->page_size * cfg->pages_per_extent;
   return cfg->page_size + extent * (1 + (num_pages + cfg->pages_per_extent - 1) / cfg->pages_per_extent);
 }
+
+// ---- routing_filter_estimate_unique_fp (src/routing_filter.c:702-848) --------------------
+extern "C" int rf_launch_estimate(void* stream, const EstFilter* fl, uint32_t num_filters, uint32_t total_idx,
+                                  uint32_t lis, uint32_t* bitmap, uint64_t bitmap_words, uint32_t* counters);
+constexpr uint64_t EST_MAX_FILTERS = 32;  // MAX_FILTERS, src/routing_filter.h:25
+
+// fl: the filters to decode (pages/slots already device pointers, idx_first unset);
+// total_num_fp: the reference's uint32 sum of num_fingerprints over ALL filters (:719-722)
+static int estimate_run(rf_amd_engine* e, hipStream_t st, const rf_amd_config* cfg, std::vector<EstFilter>& fl,
+                        uint32_t total_num_fp, uint32_t* num_unique_fp) {
+  uint32_t total_idx = 0;
+  for (auto& f : fl) {
+    f.idx_first = total_idx;
+    total_idx += f.num_idx;
+  }
+  const uint32_t ubits = cfg->fingerprint_size > 4 ? cfg->fingerprint_size - 4 : 0;  // fps < 2^(fp_size-4)
+  uint64_t words = ((1ull << ubits) + 31) / 32;
+  words = (words + 3) & ~3ull;
+  DevBuf d_fl, d_bm, d_cnt;
+  if (d_fl.alloc(sizeof(EstFilter) * (fl.size() + 1)) || d_bm.alloc(4 * words) || d_cnt.alloc(16))
+    return fail(RF_AMD_ENOMEM, "device allocation failed");
+  if (!fl.empty())
+    HIPCHK(hipMemcpyAsync(d_fl.p, fl.data(), sizeof(EstFilter) * fl.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(d_bm.p, 0, 4 * words, st));
+  HIPCHK(hipMemsetAsync(d_cnt.p, 0, 16, st));
+  if (rf_launch_estimate(st, d_fl.as<EstFilter>(), (uint32_t)fl.size(), total_idx, cfg->log_index_size,
+                         d_bm.as<uint32_t>(), words, d_cnt.as<uint32_t>()))
+    return fail(RF_AMD_EINVAL, "estimate kernel launch failed");
+  uint32_t cnt[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(cnt, d_cnt.p, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  (void)e;
+  // the reference unpacks every decoded entry into a total_num_fp / 12 buffer and asserts
+  // it fits (:776-780); the running count only grows, so this is the same condition
+  if (cnt[0] > total_num_fp / 12)
+    return fail(RF_AMD_EINVAL, "decoded fingerprints exceed num_fingerprints / 12 (reference asserts, :776)");
+  *num_unique_fp = cnt[1] * 16;
+  return 0;
+}
+
+static uint32_t est_lnb(const rf_amd_config* cfg, uint32_t num_fp) {
+  uint32_t lnb = num_fp ? 31 - __builtin_clz(num_fp) : 0;
+  return lnb < cfg->log_index_size ? cfg->log_index_size : lnb;
+}
+
+extern "C" int rf_amd_estimate_unique_fp(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* filters,
+                                         uint64_t num_filters, uint32_t* num_unique_fp) {
+  if (!num_unique_fp) return fail(RF_AMD_EINVAL, "num_unique_fp must not be NULL");  // :710-714
+  *num_unique_fp = 0;
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (int rc = check_cfg(cfg)) return rc;
+  if (num_filters > EST_MAX_FILTERS) return fail(RF_AMD_EINVAL, "more than MAX_FILTERS filters (:717)");
+  if (num_filters && !filters) return fail(RF_AMD_EINVAL, "null filters");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = e->stream;
+  uint32_t total_num_fp = 0;
+  std::vector<EstFilter> fl;
+  std::vector<DevBuf> bufs(2 * num_filters);
+  for (uint64_t i = 0; i < num_filters; i++) {
+    const rf_amd_image& im = filters[i];
+    total_num_fp += im.info.num_fingerprints;
+    if (!im.pages || !im.slots) continue;  // filter.addr == 0 (:739-742)
+    const uint32_t lnb = est_lnb(cfg, im.info.num_fingerprints);
+    if (lnb > cfg->fingerprint_size || lnb - cfg->log_index_size > 14)
+      return fail(RF_AMD_EINVAL, "image geometry out of range");
+    const uint32_t num_indices = 1u << (lnb - cfg->log_index_size);
+    if (num_indices < 16) continue;  // "the filter is too small forget it" (:755)
+    if (cfg->fingerprint_size + im.info.value_size > 32) return fail(RF_AMD_EINVAL, "fp_size + value_size > 32");
+    const uint32_t nidx = num_indices / 16;
+    uint64_t last_page = 0;  // upload only the pages the decoded indices live on
+    for (uint32_t k = 0; k < nidx; k++) last_page = std::max<uint64_t>(last_page, im.slots[k] / cfg->page_size);
+    if (last_page >= im.info.num_pages) return fail(RF_AMD_EINVAL, "index slot outside the image");
+    const uint64_t pbytes = (last_page + 1) * cfg->page_size;
+    DevBuf& dp = bufs[2 * i];
+    DevBuf& ds = bufs[2 * i + 1];
+    if (dp.alloc(pbytes + 256) || ds.alloc(8ull * nidx)) return fail(RF_AMD_ENOMEM, "device allocation failed");
+    HIPCHK(hipMemsetAsync(dp.as<uint8_t>() + pbytes, 0, 256, st));
+    HIPCHK(hipMemcpyAsync(dp.p, im.pages, pbytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(ds.p, im.slots, 8ull * nidx, hipMemcpyHostToDevice, st));
+    const uint32_t rem = cfg->fingerprint_size - lnb;
+    fl.push_back(EstFilter{dp.as<uint8_t>(), ds.as<uint64_t>(), im.info.value_size, rem + im.info.value_size, nidx, 0});
+  }
+  return estimate_run(e, st, cfg, fl, total_num_fp, num_unique_fp);
+}
+
+extern "C" int rf_amd_batch_estimate_unique_fp(rf_amd_batch* const* batches, const uint32_t* filter_index,
+                                               uint64_t num_filters, uint32_t* num_unique_fp) {
+  if (!num_unique_fp) return fail(RF_AMD_EINVAL, "num_unique_fp must not be NULL");
+  *num_unique_fp = 0;
+  if (num_filters > EST_MAX_FILTERS) return fail(RF_AMD_EINVAL, "more than MAX_FILTERS filters (:717)");
+  if (num_filters == 0) return 0;
+  if (!batches || !filter_index) return fail(RF_AMD_EINVAL, "null batch list");
+  rf_amd_engine* e = nullptr;
+  const rf_amd_config* cfg = nullptr;
+  uint32_t total_num_fp = 0;
+  std::vector<EstFilter> fl;
+  for (uint64_t i = 0; i < num_filters; i++) {
+    rf_amd_batch* b = batches[i];
+    if (!b) continue;  // NULL_ROUTING_FILTER
+    const uint32_t f = filter_index[i];
+    if (f >= b->F || !b->built) return fail(RF_AMD_EINVAL, "bad batch/filter (not built)");
+    if (!e) {
+      e = b->eng;
+      cfg = &b->cfg;
+    } else if (b->eng != e || memcmp(&b->cfg, cfg, sizeof(*cfg)) != 0) {
+      return fail(RF_AMD_EINVAL, "filters of one estimate must share an engine and a routing config");
+    }
+    const FilterPlan& p = b->plans[f];
+    total_num_fp += p.num_fp;
+    if (p.num_indices < 16) continue;
+    fl.push_back(EstFilter{b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size,
+                           b->d_slots.as<uint64_t>() + p.idx_base, p.vs, p.rvs, p.num_indices / 16, 0});
+  }
+  if (!e) return 0;
+  HIPCHK(hipSetDevice(e->device));
+  // the images must be complete (and error-free) before they are decoded
+  for (uint64_t i = 0; i < num_filters; i++) {
+    if (!batches[i]) continue;
+    rf_amd_filter_info info;
+    if (int rc = rf_amd_batch_info(batches[i], filter_index[i], &info)) return rc;
+    if (info.error) return fail(RF_AMD_EINVAL, "filter build reported error bits");
+  }
+  return estimate_run(e, e->stream, cfg, fl, total_num_fp, num_unique_fp);
+}
+
+extern "C" uint32_t rf_amd_estimate_unique_keys(const rf_amd_filter_info* filter, const rf_amd_config* cfg) {
+  return rf_amd_estimate_unique_keys_from_count(cfg, filter->num_unique);  // .c:1141-1146
+}
+
+// ---- asynchronous batched lookup (routing_filter_lookup_async, src/routing_filter.h:130-155,
+// .c:895-972) ---------------------------------------------------------------------------
+// The reference's coroutine yields while a filter page is read and calls `callback` when it
+// can be resumed; here one call stages a whole batch of lookups (H2D, probe, D2H) on a
+// stream and the callback fires from a HIP host function once the results are in h_found.
+struct rf_amd_lookup_async_state {
+  rf_amd_batch* b = nullptr;
+  hipStream_t st = nullptr;
+  uint64_t n = 0;
+  uint64_t* h_found = nullptr;
+  void* h_stage = nullptr;  // pinned: keys in, found values out
+  size_t stage_bytes = 0;
+  DevBuf d_keys, d_fid, d_found;
+  hipEvent_t done_ev = nullptr;
+  rf_amd_callback_fn cb = nullptr;
+  void* cb_arg = nullptr;
+  volatile int done = 0;
+  ~rf_amd_lookup_async_state() {
+    if (done_ev) (void)hipEventSynchronize(done_ev);
+    if (done_ev) (void)hipEventDestroy(done_ev);
+    if (h_stage) (void)hipHostFree(h_stage);
+  }
+};
+
+static void lookup_async_finish(void* arg) {  // HIP host function: no HIP calls in here
+  auto* s = static_cast<rf_amd_lookup_async_state*>(arg);
+  memcpy(s->h_found, s->h_stage, 8 * s->n);
+  __atomic_store_n(&s->done, 1, __ATOMIC_RELEASE);
+  if (s->cb) s->cb(s->cb_arg);
+}
+
+extern "C" int rf_amd_lookup_async(rf_amd_batch* b, const void* h_keys, uint32_t key_len,
+                                   const uint32_t* h_filter_id, uint64_t n, uint64_t* h_found,
+                                   rf_amd_callback_fn callback, void* callback_arg, void* stream,
+                                   rf_amd_lookup_async_state** out) {
+  if (!out) return fail(RF_AMD_EINVAL, "null state out-param");
+  *out = nullptr;
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "batch not built");
+  if (n && (!h_keys || !h_found || key_len == 0)) return fail(RF_AMD_EINVAL, "null keys / results");
+  HIPCHK(hipSetDevice(b->eng->device));
+  auto* s = new rf_amd_lookup_async_state();
+  s->b = b;
+  s->st = stream ? (hipStream_t)stream : b->eng->stream;
+  s->n = n;
+  s->h_found = h_found;
+  s->cb = callback;
+  s->cb_arg = callback_arg;
+  const size_t kbytes = (size_t)key_len * n;
+  s->stage_bytes = std::max<size_t>(std::max<size_t>(kbytes, 8 * n), 16);
+  int rc = 0;
+  if (hipHostMalloc(&s->h_stage, s->stage_bytes, hipHostMallocDefault) != hipSuccess) {
+    s->h_stage = nullptr;
+    rc = fail(RF_AMD_ENOMEM, "pinned staging allocation failed");
+  }
+  if (!rc) rc = s->d_keys.alloc(kbytes + 16) | s->d_fid.alloc(4 * n + 16) | s->d_found.alloc(8 * n + 16);
+  if (!rc && hipEventCreateWithFlags(&s->done_ev, hipEventDisableTiming) != hipSuccess)
+    rc = fail(RF_AMD_EINVAL, "event creation failed");
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  if (n) {
+    memcpy(s->h_stage, h_keys, kbytes);
+    if (hipMemcpyAsync(s->d_keys.p, s->h_stage, kbytes, hipMemcpyHostToDevice, s->st) != hipSuccess ||
+        (h_filter_id ? hipMemcpyAsync(s->d_fid.p, h_filter_id, 4 * n, hipMemcpyHostToDevice, s->st)
+                     : hipMemsetAsync(s->d_fid.p, 0, 4 * n, s->st)) != hipSuccess)
+      rc = fail(RF_AMD_EINVAL, "H2D failed");
+    if (!rc) rc = rf_amd_batch_probe_keys(b, s->d_keys.p, key_len, s->d_fid.as<uint32_t>(), n,
+                                          s->d_found.as<uint64_t>(), s->st);
+    // the keys' staging copy has been consumed once the probe ran: reuse it for the results
+    if (!rc && hipMemcpyAsync(s->h_stage, s->d_found.p, 8 * n, hipMemcpyDeviceToHost, s->st) != hipSuccess)
+      rc = fail(RF_AMD_EINVAL, "D2H failed");
+  }
+  if (!rc && hipLaunchHostFunc(s->st, lookup_async_finish, s) != hipSuccess)
+    rc = fail(RF_AMD_EINVAL, "host function launch failed");
+  if (!rc && hipEventRecord(s->done_ev, s->st) != hipSuccess) rc = fail(RF_AMD_EINVAL, "event record failed");
+  if (rc) {
+    (void)hipStreamSynchronize(s->st);
+    delete s;
+    return rc;
+  }
+  *out = s;
+  return 0;
+}
+
+extern "C" int rf_amd_lookup_async_poll(rf_amd_lookup_async_state* s) {
+  if (!s) return RF_AMD_ASYNC_DONE;
+  return __atomic_load_n(&s->done, __ATOMIC_ACQUIRE) ? RF_AMD_ASYNC_DONE : RF_AMD_ASYNC_RUNNING;
+}
+
+extern "C" int rf_amd_lookup_async_wait(rf_amd_lookup_async_state* s) {
+  if (!s) return 0;
+  HIPCHK(hipEventSynchronize(s->done_ev));
+  while (!__atomic_load_n(&s->done, __ATOMIC_ACQUIRE)) {
+  }
+  return 0;
+}
+
+extern "C" void rf_amd_lookup_async_free(rf_amd_lookup_async_state* s) {
+  if (!s) return;
+  (void)rf_amd_lookup_async_wait(s);
+  delete s;
+}
+
+// ---- routing_filter_verify (src/routing_filter.c:1163-1183) ------------------------------
+extern "C" int rf_launch_count_missing(void* stream, const uint64_t* found, uint64_t n, uint32_t value,
+                                       unsigned long long* missing);
+
+extern "C" int rf_amd_filter_verify(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* filter,
+                                    const void* keys, uint32_t key_len, uint64_t n, uint16_t value,
+                                    uint64_t* num_missing) {
+  if (num_missing) *num_missing = 0;
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (value >= 64) return fail(RF_AMD_EINVAL, "value >= 64");
+  if (n == 0) return 0;
+  if (!keys || key_len == 0) return fail(RF_AMD_EINVAL, "null keys");
+  if (!filter || !filter->pages) {  // a NULL filter finds nothing: every key is missing
+    if (num_missing) *num_missing = n;
+    return fail(RF_AMD_EINVAL, "verify: key not found in a NULL filter");
+  }
+  rf_amd_batch* b = nullptr;
+  if (int rc = batch_from_image(e, cfg, filter, &b)) return rc;
+  DevBuf d_k, d_f, d_id, d_m;
+  int rc = d_k.alloc((size_t)key_len * n + 16) | d_f.alloc(8 * n) | d_id.alloc(4 * n) | d_m.alloc(8);
+  unsigned long long missing = 0;
+  if (!rc) {
+    hipStream_t st = e->stream;
+    if (hipMemcpyAsync(d_k.p, keys, (size_t)key_len * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync(d_id.p, 0, 4 * n, st) != hipSuccess || hipMemsetAsync(d_m.p, 0, 8, st) != hipSuccess)
+      rc = fail(RF_AMD_EINVAL, "H2D failed");
+    if (!rc) rc = rf_amd_batch_probe_keys(b, d_k.p, key_len, d_id.as<uint32_t>(), n, d_f.as<uint64_t>(), st);
+    if (!rc && rf_launch_count_missing(st, d_f.as<uint64_t>(), n, value, d_m.as<unsigned long long>()))
+      rc = fail(RF_AMD_EINVAL, "verify kernel launch failed");
+    if (!rc && (hipMemcpyAsync(&missing, d_m.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
+      rc = fail(RF_AMD_EINVAL, "D2H failed");
+  }
+  rf_amd_batch_destroy(b);
+  if (rc) return rc;
+  if (num_missing) *num_missing = missing;
+  // the reference asserts routing_filter_is_value_found for every key (:1177)
+  return missing ? fail(RF_AMD_EINVAL, "verify: " + std::to_string(missing) + " keys not found") : 0;
+}
+
+// ---- routing_filter_print (src/routing_filter.c:1185-1286): debug text, host only ----------
+extern "C" int rf_amd_filter_print(const rf_amd_config* cfg, const rf_amd_image* filter, void* out_file) {
+  if (int rc = check_cfg(cfg)) return rc;
+  if (!filter || !filter->pages || !filter->slots) return fail(RF_AMD_EINVAL, "null filter");
+  FILE* fo = out_file ? (FILE*)out_file : stdout;
+  const uint32_t lis = cfg->log_index_size, index_size = 1u << lis;
+  const uint32_t lnb = est_lnb(cfg, filter->info.num_fingerprints);
+  const uint32_t num_indices = 1u << (lnb - lis);
+  const uint32_t rem = cfg->fingerprint_size - lnb, vs = filter->info.value_size, rvs = rem + vs;
+  const uint8_t* pg = filter->pages;
+  auto bit = [&](uint64_t bp) { return (pg[bp >> 3] >> (bp & 7)) & 1u; };
+  fprintf(fo, "********************************************************************************\n");
+  fprintf(fo, "***   filter INDEX\n");
+  fprintf(fo, "***   filter_addr: %lu\n", (unsigned long)0);
+  fprintf(fo, "--------------------------------------------------------------------------------\n");
+  for (uint32_t i = 0; i < num_indices; i++) fprintf(fo, "index 0x%x: %lu\n", i, (unsigned long)filter->slots[i]);
+  for (uint32_t i = 0; i < num_indices; i++) {
+    const uint64_t h = filter->slots[i];
+    const uint32_t c = (uint32_t)pg[h] | ((uint32_t)pg[h + 1] << 8);
+    fprintf(fo, "----------------------------------------\n");
+    fprintf(fo, "--- Index 0x%x\n", i);
+    fprintf(fo, "--- Encoding: %u\n", c);
+    const uint64_t eb = (h + 2) * 8;
+    for (uint32_t k = 0; k < c + index_size; k++) {
+      if (k != 0 && k % 16 == 0) fprintf(fo, " | ");
+      fputc(bit(eb + k) ? '1' : '0', fo);
+    }
+    fputc('\n', fo);
+    fprintf(fo, "--- Remainders\n");
+    // print_remainders' header_length uses (c + index_size - 1) / 8 + 1 encoding bytes, not
+    // the block's + 4 (:1234-1236 vs :207-211): the reference prints from that offset, so do we
+    const uint64_t hl = (c + index_size - 1) / 8 + 1 + 2;
+    const uint64_t rb = (h + hl) * 8;
+    // bucket bounds by walking the unary encoding (routing_get_bucket_bounds, :230-279)
+    uint32_t pos = 0, start = 0;
+    for (uint32_t bo = 0; bo < index_size; bo++) {
+      uint32_t cnt = 0;
+      while (pos < c + index_size && !bit(eb + pos)) { pos++; cnt++; }
+      pos++;  // the bucket's terminating 1
+      fprintf(fo, "0x%x remainders:", bo);
+      for (uint32_t j = start; j < start + cnt; j++) {
+        uint32_t rv = 0;
+        for (uint32_t t = 0; t < rvs; t++) rv |= bit(rb + (uint64_t)j * rvs + t) << t;
+        fprintf(fo, " 0x%x:%u", vs >= 32 ? 0u : rv >> vs, rv & (uint32_t)((1ull << vs) - 1));
+      }
+      fputc('\n', fo);
+      start += cnt;
+    }
+  }
+  fflush(fo);
+  return 0;
+}

@@ -1362,6 +1362,118 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
 }
 
 // ======================================================================================
+// routing_filter_estimate_unique_fp (src/routing_filter.c:702-848)
+//
+// The reference decodes the first num_indices/16 indices of up to 32 filters (each list
+// sorted, duplicates dropped) and k-way merges them, counting distinct fingerprints; the
+// result is that count * 16. Those indices hold exactly the fingerprints below
+// 2^(fp_size-4), so the distinct count of the union is the population of a bitmap over
+// that range: one wave per decoded index sets its fingerprints' bits (bit-exact with the
+// merge count; no sort, no k-way merge), one pass counts them.
+// ======================================================================================
+__global__ __launch_bounds__(256) void k_est_decode(const EstFilter* __restrict__ fl, uint32_t num_filters,
+                                                    uint32_t total_idx, uint32_t lis,
+                                                    uint32_t* __restrict__ bitmap,
+                                                    uint32_t* __restrict__ num_entries) {
+  const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  if (wid >= total_idx) return;
+  uint32_t f = 0;
+  while (f + 1 < num_filters && fl[f + 1].idx_first <= wid) f++;
+  const EstFilter& F = fl[f];
+  const uint32_t index_no = wid - F.idx_first;
+  const uint32_t index_size = 1u << lis;
+  const uint64_t hdr = F.slots[index_no];
+  const uint8_t* pg = F.pages;
+  const uint32_t c = (uint32_t)pg[hdr] | ((uint32_t)pg[hdr + 1] << 8);
+  if (lane == 0 && c) atomicAdd(num_entries, c);
+  const uint32_t enc = (c + index_size - 1) / 8 + 4;
+  const uint64_t ebit = (hdr + 2) * 8;
+  const uint64_t rbit = (hdr + 2 + enc) * 8;
+  const uint32_t total_bits = c + index_size;
+  uint32_t zeros_before = 0, ones_before = 0;
+  for (uint32_t base = 0; base < total_bits; base += 64 * WAVE) {
+    const uint32_t bit0 = base + lane * 64;
+    uint64_t x = 0;
+    uint32_t nb = 0;
+    if (bit0 < total_bits) {
+      nb = min(64u, total_bits - bit0);
+      const uint64_t bp = ebit + bit0;
+      const uint32_t sh = (uint32_t)(bp & 7);
+      x = ld_u64_unaligned(pg, bp >> 3) >> sh;
+      if (sh) x |= (uint64_t)pg[(bp >> 3) + 8] << (64 - sh);
+      if (nb < 64) x &= (1ull << nb) - 1;
+    }
+    const uint32_t ones = __popcll(x);
+    const uint32_t zer = nb - ones;
+    const uint32_t ones_ex = wave_incl_scan(ones) - ones + ones_before;
+    const uint32_t zer_ex = wave_incl_scan(zer) - zer + zeros_before;
+    uint64_t z = ~x & (nb == 64 ? ~0ull : ((1ull << nb) - 1));
+    uint32_t k = zer_ex;
+    while (z) {  // every 0-bit is an entry; its bucket offset = 1-bits before it
+      const uint32_t b = __builtin_ctzll(z);
+      z &= z - 1;
+      const uint32_t bo = ones_ex + (b - (k - zer_ex));
+      const uint32_t rv = ld_bits(pg, rbit + (uint64_t)k * F.rvs, F.rvs);
+      const uint32_t bucket = index_no * index_size + bo;
+      const uint32_t fp = (((F.rvs >= 32 ? 0u : (bucket << F.rvs)) | rv) >> F.vs);  // :786-787
+      atomicOr(&bitmap[fp >> 5], 1u << (fp & 31));
+      k++;
+    }
+    ones_before = __shfl(ones_ex + ones, WAVE - 1, WAVE);
+    zeros_before = __shfl(zer_ex + zer, WAVE - 1, WAVE);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_popcount(const uint4* __restrict__ words, uint64_t n4,
+                                                  uint32_t* __restrict__ total) {
+  __shared__ uint32_t s_tmp[256 / WAVE + 1];
+  uint32_t c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256) {
+    const uint4 w = words[i];
+    c += __popc(w.x) + __popc(w.y) + __popc(w.z) + __popc(w.w);
+  }
+  uint32_t tot;
+  block_excl_scan<256>(c, s_tmp, &tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(total, tot);
+}
+
+// bitmap (zeroed by the caller, bitmap_words a multiple of 4) -> counters[0] = entries
+// decoded, counters[1] = distinct fingerprints
+extern "C" int rf_launch_estimate(void* stream, const EstFilter* fl, uint32_t num_filters, uint32_t total_idx,
+                                  uint32_t lis, uint32_t* bitmap, uint64_t bitmap_words, uint32_t* counters) {
+  if (total_idx) {
+    hipLaunchKernelGGL(k_est_decode, dim3((total_idx + 3) / 4), dim3(256), 0, (hipStream_t)stream, fl, num_filters,
+                       total_idx, lis, bitmap, counters);
+    if (hipGetLastError() != hipSuccess) return 1;
+  }
+  const uint64_t n4 = bitmap_words / 4;
+  const uint64_t want = (n4 + 255) / 256 + 1;
+  const uint32_t grid = (uint32_t)(want < 2048 ? want : 2048);
+  hipLaunchKernelGGL(k_popcount, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4*)bitmap, n4,
+                     counters + 1);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// routing_filter_verify (src/routing_filter.c:1163-1183): keys whose found_values lacks `value`
+__global__ __launch_bounds__(256) void k_count_missing(const uint64_t* __restrict__ found, uint64_t n,
+                                                       uint32_t value, unsigned long long* __restrict__ missing) {
+  uint32_t c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    c += ((found[i] >> value) & 1ull) ? 0u : 1u;
+  c = wave_incl_scan(c);
+  if ((threadIdx.x & (WAVE - 1)) == WAVE - 1 && c) atomicAdd(missing, (unsigned long long)c);
+}
+
+extern "C" int rf_launch_count_missing(void* stream, const uint64_t* found, uint64_t n, uint32_t value,
+                                       unsigned long long* missing) {
+  const uint64_t want = (n + 255) / 256;
+  hipLaunchKernelGGL(k_count_missing, dim3((uint32_t)(want < 4096 ? (want ? want : 1) : 4096)), dim3(256), 0,
+                     (hipStream_t)stream, found, n, value, missing);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// ======================================================================================
 // Probe: routing_filter_lookup (src/routing_filter.c:985-1073), one lane per probe
 // ======================================================================================
 // position of the r-th (0-based) set bit of the 128-bit value hi:lo

@@ -52,6 +52,16 @@ struct FilterPlan {
   const uint64_t* old_slots;
 };
 
+// one filter of routing_filter_estimate_unique_fp (src/routing_filter.c:702-848): the first
+// num_indices/16 indices of its image are decoded into a fingerprint bitmap
+struct EstFilter {
+  const uint8_t* pages;   // the filter's data pages (relocatable slots index into them)
+  const uint64_t* slots;  // index slots
+  uint32_t vs, rvs;       // value_size, remainder + value bits
+  uint32_t num_idx;       // indices to decode (num_indices / 16)
+  uint32_t idx_first;     // prefix sum of num_idx over the filters before this one
+};
+
 struct FilterOut {
   uint32_t num_unique;
   uint32_t num_pages;

@@ -39,7 +39,13 @@ EXPORTED = [
     "rf_amd_image_free",
     "rf_amd_max_fingerprints", "rf_amd_estimate_unique_keys_from_count",
     "rf_amd_space_use_bytes",
+    "rf_amd_estimate_unique_fp", "rf_amd_batch_estimate_unique_fp", "rf_amd_estimate_unique_keys",
+    "rf_amd_lookup_async", "rf_amd_lookup_async_poll", "rf_amd_lookup_async_wait",
+    "rf_amd_lookup_async_free", "rf_amd_filter_verify", "rf_amd_filter_print",
 ]
+ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
+ASYNC_STATUS_DONE = 1
+CALLBACK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
 
 
 class PlatformStatusError(RuntimeError):
@@ -120,6 +126,20 @@ def load_library(build_if_missing=True):
     L.rf_amd_estimate_unique_keys_from_count.restype = u32
     L.rf_amd_space_use_bytes.argtypes = [ctypes.POINTER(RfConfig), u32]
     L.rf_amd_space_use_bytes.restype = u64
+    L.rf_amd_estimate_unique_fp.argtypes = [vp, ctypes.POINTER(RfConfig), vp, u64,
+                                            ctypes.POINTER(u32)]
+    L.rf_amd_batch_estimate_unique_fp.argtypes = [vp, vp, u64, ctypes.POINTER(u32)]
+    L.rf_amd_estimate_unique_keys.argtypes = [ctypes.POINTER(RfFilterInfo), ctypes.POINTER(RfConfig)]
+    L.rf_amd_estimate_unique_keys.restype = u32
+    L.rf_amd_lookup_async.argtypes = [vp, vp, u32, vp, u64, vp, CALLBACK_FN, vp, vp,
+                                      ctypes.POINTER(vp)]
+    L.rf_amd_lookup_async_poll.argtypes = [vp]
+    L.rf_amd_lookup_async_wait.argtypes = [vp]
+    L.rf_amd_lookup_async_free.argtypes = [vp]
+    L.rf_amd_lookup_async_free.restype = None
+    L.rf_amd_filter_verify.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), vp, u32,
+                                       u64, ctypes.c_uint16, ctypes.POINTER(u64)]
+    L.rf_amd_filter_print.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), vp]
     _lib = L
     return L
 
@@ -292,7 +312,121 @@ def routing_filter_estimate_unique_keys_from_count(cfg: RoutingConfig, num_uniqu
 
 
 def routing_filter_estimate_unique_keys(filt: RoutingFilter, cfg: RoutingConfig) -> int:
-    return routing_filter_estimate_unique_keys_from_count(cfg, filt.num_unique)
+    """src/routing_filter.h:165-167, .c:1141-1146."""
+    info = RfFilterInfo(filt.num_fingerprints, filt.num_unique, filt.value_size,
+                        filt.num_indices, filt.num_pages, 0)
+    return load_library().rf_amd_estimate_unique_keys(ctypes.byref(info), ctypes.byref(cfg.c()))
+
+
+def routing_filter_estimate_unique_fp(cfg: RoutingConfig, filters, engine=None) -> int:
+    """routing_filter_estimate_unique_fp (src/routing_filter.h:169-175, .c:702-848) over
+    host images; None entries are NULL_ROUTING_FILTER. Returns num_unique_fp."""
+    eng = engine or default_engine()
+    arr = (RfImage * max(1, len(filters)))()
+    keep = []
+    for i, f in enumerate(filters):
+        if f is None:
+            arr[i] = RfImage()
+        else:
+            arr[i] = f._c()
+            keep.append(f)
+    out = ctypes.c_uint32(0)
+    _check(load_library().rf_amd_estimate_unique_fp(eng.h, ctypes.byref(cfg.c()), ctypes.addressof(arr),
+                                                    len(filters), ctypes.byref(out)))
+    return out.value
+
+
+def batch_estimate_unique_fp(members) -> int:
+    """estimate_unique_fp over device-resident filters: members = [(FilterBatch, f) or None]."""
+    n = len(members)
+    hs = (ctypes.c_void_p * max(1, n))()
+    idx = np.zeros(max(1, n), dtype=np.uint32)
+    for i, m in enumerate(members):
+        if m is not None:
+            hs[i] = m[0].h.value
+            idx[i] = m[1]
+    out = ctypes.c_uint32(0)
+    _check(load_library().rf_amd_batch_estimate_unique_fp(ctypes.addressof(hs), idx.ctypes.data, n,
+                                                          ctypes.byref(out)))
+    return out.value
+
+
+def routing_filter_verify(cfg: RoutingConfig, filt, keys: np.ndarray, value: int, engine=None) -> int:
+    """routing_filter_verify (src/routing_filter.c:1163-1183) over fixed-length keys: raises
+    PlatformStatusError(EINVAL) if a key does not find `value` (the reference asserts)."""
+    eng = engine or default_engine()
+    k = np.ascontiguousarray(keys, dtype=np.uint8)
+    if k.ndim == 1:
+        k = k.reshape(1, -1)
+    missing = ctypes.c_uint64(0)
+    fc = filt._c() if filt is not None else None
+    rc = load_library().rf_amd_filter_verify(eng.h, ctypes.byref(cfg.c()),
+                                             ctypes.byref(fc) if fc is not None else None,
+                                             k.ctypes.data, k.shape[1], k.shape[0], value,
+                                             ctypes.byref(missing))
+    if rc:
+        err = PlatformStatusError(rc, load_library().rf_amd_last_error().decode())
+        err.num_missing = missing.value
+        raise err
+    return 0
+
+
+def routing_filter_print(cfg: RoutingConfig, filt, path=None) -> str:
+    """routing_filter_print (src/routing_filter.c:1260-1286); returns the text."""
+    import tempfile
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    fd, tmp = tempfile.mkstemp(suffix=".txt")
+    os.close(fd)
+    fh = libc.fopen((path or tmp).encode(), b"w")
+    try:
+        fc = filt._c()
+        _check(load_library().rf_amd_filter_print(ctypes.byref(cfg.c()), ctypes.byref(fc), fh))
+    finally:
+        libc.fclose(fh)
+    with open(path or tmp) as t:
+        text = t.read()
+    os.unlink(tmp)
+    return text
+
+
+class LookupAsync:
+    """routing_filter_lookup_async (src/routing_filter.h:130-155) for a batch of host keys
+    against a built FilterBatch: poll() returns ASYNC_STATUS_RUNNING / ASYNC_STATUS_DONE;
+    callback() (optional, no arguments) runs once the results are in `found`."""
+
+    def __init__(self, batch, keys: np.ndarray, filter_id=None, callback=None, stream=None):
+        k = np.ascontiguousarray(keys, dtype=np.uint8)
+        if k.ndim == 1:
+            k = k.reshape(1, -1)
+        self.found = np.zeros(k.shape[0], dtype=np.uint64)
+        self._fid = None if filter_id is None else np.ascontiguousarray(filter_id, dtype=np.uint32)
+        self._cb = CALLBACK_FN(lambda _arg: callback()) if callback else CALLBACK_FN()
+        self.batch = batch
+        self.h = ctypes.c_void_p()
+        _check(load_library().rf_amd_lookup_async(
+            batch.h, k.ctypes.data, k.shape[1], None if self._fid is None else self._fid.ctypes.data,
+            k.shape[0], self.found.ctypes.data, self._cb, None, stream, ctypes.byref(self.h)))
+
+    def poll(self) -> int:
+        return load_library().rf_amd_lookup_async_poll(self.h)
+
+    def wait(self) -> np.ndarray:
+        _check(load_library().rf_amd_lookup_async_wait(self.h))
+        return self.found
+
+    def close(self):
+        if self.h:
+            load_library().rf_amd_lookup_async_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def routing_filter_space_use_bytes(cfg: RoutingConfig, filt: RoutingFilter) -> int:
