@@ -39,6 +39,8 @@ WORKLOADS = {
     "c2": (8, 8_000_000, "weak", "C2: 64M x 24B keys per GPU = 8 filters x 8,000,000, build + full probe"),
     "c3": (256, 1 << 20, "weak", "C3: 256M x 24B keys per GPU = 256 filters x 2^20, build + full probe"),
     "c4": (1024, 1 << 20, "strong", "C4: 2^30 x 24B keys = 1024 filters x 2^20 split by key range, build + full probe"),
+    "c5": (8, 1 << 21, "weak", "C5: 16.8M variable-length (8-100 B) keys per GPU = 8 filters x 2^21, build + "
+                               "as many probes (90% Zipf(0.99) positives, 10% negatives, shuffled)"),
 }
 
 METRIC = "routing_filter build Mkeys/s + probe Mkeys/s, device-resident, 24B keys"
@@ -50,9 +52,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2",
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                    help="c2: 8 x 8,000,000 keys per GPU (weak); c3: 256 x 2^20 per GPU (weak); "
-                        "c4: 1024 x 2^20 keys in total, split over the GPUs (strong)")
+                        "c4: 1024 x 2^20 keys in total, split over the GPUs (strong); "
+                        "c5: 8 x 2^21 variable-length keys per GPU + Zipf probe mix (weak)")
     p.add_argument("--filters", type=int, default=0, help="override filters (per GPU for c2/c3)")
     p.add_argument("--keys-per-filter", type=int, default=0)
     p.add_argument("--log-index-size", type=int, default=8)
@@ -64,13 +67,16 @@ def parse():
     return p.parse_args()
 
 
-def stage_bytes(stage, N, P, image_bytes, slot_bytes, unique):
-    """Algorithmic bytes per launch of each stage (DESIGN.md 'Roofline')."""
+def stage_bytes(stage, N, P, image_bytes, slot_bytes, unique, key_bytes=None, probe_key_bytes=None):
+    """Algorithmic bytes per launch of each stage (DESIGN.md 'Roofline'). Fixed 24 B keys
+    unless key_bytes / probe_key_bytes give the variable-length totals (bytes + offsets)."""
+    kb = N * 24 if key_bytes is None else key_bytes
+    pkb = P * 24 if probe_key_bytes is None else probe_key_bytes
     return {
-        "partition": N * 24 + N * 4,           # fused K1+K3: read keys, write bucketed entries
+        "partition": kb + N * 4,               # fused K1+K3: read keys, write bucketed entries
         "cb_sort": N * 4 + unique * 4,         # read bucketed entries, write sorted unique
         "assemble": unique * 4 + image_bytes,  # read sorted entries, write pages
-        "probe": P * 24 + P * 8 + image_bytes + slot_bytes,  # SURVEY.md §8(d) probe figure
+        "probe": pkb + P * 8 + image_bytes + slot_bytes,  # SURVEY.md §8(d) probe figure
     }.get(stage)
 
 
@@ -108,6 +114,37 @@ def cpu_baseline(args, cfg_lis, n):
     }
 
 
+def cpu_baseline_var(args, cfg_lis, w, F, n):
+    """C5 CPU baseline: the oracle's routing_filter_add over variable-length keys, one filter
+    per thread, then routing_filter_lookup of the whole probe mix."""
+    from oracle import oracle as O
+    import ctypes
+    threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
+    ocfg = O.make_config(log_index_size=cfg_lis)
+    starts = (np.arange(F, dtype=np.uint64) * n)
+    counts = np.full(F, n, dtype=np.uint32)
+    keep = (O.Filter * F)()
+    L = O.lib()
+    t_build = L.rfo_bench_build_var(ctypes.byref(ocfg), w["bytes"].ctypes.data, w["offs"].ctypes.data,
+                                    starts.ctypes.data, counts.ctypes.data, F, 0, threads, keep)
+    P = w["probe_fid"].size
+    found = np.zeros(P, dtype=np.uint64)
+    t_probe = L.rfo_bench_probe_var(ctypes.byref(ocfg), keep, w["probe_bytes"].ctypes.data,
+                                    w["probe_offs"].ctypes.data, w["probe_fid"].ctypes.data, P, threads,
+                                    found.ctypes.data)
+    ok = bool((found[w["positive"]] & np.uint64(1)).all())
+    for i in range(F):
+        L.rfo_filter_release(ctypes.byref(keep[i]))
+    total = F * n
+    return {
+        "value": total / (t_build + t_probe) / 1e6, "unit": "Mkeys/s", "cores": threads, "kind": "port",
+        "sample": f"the whole C5 workload: {F} filters x {n} var-length keys, hash+routing_filter_add one "
+                  f"filter per thread ({t_build:.2f} s), routing_filter_lookup of {P} mixed probes "
+                  f"({t_probe:.2f} s); positives found: {ok}",
+        "build_mkeys_s": total / t_build / 1e6, "probe_mkeys_s": P / t_probe / 1e6,
+    }
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -121,6 +158,7 @@ def main():
     dev = torch.device("cuda", local)
 
     wf, wn, scaling, wdesc = WORKLOADS[args.workload]
+    var = args.workload == "c5"
     n = args.keys_per_filter or wn
     if scaling == "weak":
         F_total = (args.filters or wf) * world
@@ -132,18 +170,37 @@ def main():
     cfg = E.routing_config_init(fingerprint_size=26, log_index_size=args.log_index_size, seed=42)
     eng = E.Engine(local)
     stream = torch.cuda.Stream(device=dev)
+    w = None
+    key_bytes = probe_key_bytes = None
     with torch.cuda.stream(stream):
-        # key-range shard of this rank: ids [key_begin, key_end), filter f = ids of its range
-        keys = K.seq_keys_torch(me.key_begin, N, 24, dev)
-        fid = (torch.arange(N, device=dev, dtype=torch.int64) // n).to(torch.int32)
-        found = torch.empty(N, dtype=torch.int64, device=dev)
+        if var:
+            # C5: host-generated variable-length keys + Zipf probe mix, copied to HBM once
+            w = K.c5_inputs(F, n, seed=0x5EED + me.key_begin)
+            d_bytes, d_offs = torch.from_numpy(w["bytes"]).to(dev), torch.from_numpy(w["offs"].view(np.int64)).to(dev)
+            p_bytes = torch.from_numpy(w["probe_bytes"]).to(dev)
+            p_offs = torch.from_numpy(w["probe_offs"].view(np.int64)).to(dev)
+            fid = torch.from_numpy(w["probe_fid"].view(np.int32)).to(dev)
+            positive = torch.from_numpy(w["positive"]).to(dev)
+            P = int(w["probe_fid"].size)
+            key_bytes = w["bytes"].nbytes + w["offs"].nbytes
+            probe_key_bytes = w["probe_bytes"].nbytes + w["probe_offs"].nbytes + 4 * P
+        else:
+            # key-range shard of this rank: ids [key_begin, key_end), filter f = ids of its range
+            keys = K.seq_keys_torch(me.key_begin, N, 24, dev)
+            fid = (torch.arange(N, device=dev, dtype=torch.int64) // n).to(torch.int32)
+            P = N
+        found = torch.empty(P, dtype=torch.int64, device=dev)
     stream.synchronize()
     batch = E.FilterBatch(cfg, [n] * F, engine=eng)
     batch.set_timing(True)
 
     def step():
-        batch.build_keys(keys, 24, stream=stream.cuda_stream)
-        batch.probe_keys(keys, 24, fid, N, found, stream=stream.cuda_stream)
+        if var:
+            batch.build_var_keys(d_bytes, d_offs, stream=stream.cuda_stream)
+            batch.probe_var_keys(p_bytes, p_offs, fid, P, found, stream=stream.cuda_stream)
+        else:
+            batch.build_keys(keys, 24, stream=stream.cuda_stream)
+            batch.probe_keys(keys, 24, fid, N, found, stream=stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -157,14 +214,10 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
     for _ in range(args.steps):
         step()
         for k, v in batch.timings().items():  # waits for this step's events
             stages[k].append(v)
-    ev1.record(stream)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -172,13 +225,16 @@ def main():
     keys_all = S.sum_over_ranks(float(N), dist, dev)
 
     # ---- verification (outside the timed region) -------------------------------------
-    ok = bool(((found & 1) == 1).all().item())
+    if var:
+        ok = bool(((found[positive] & 1) == 1).all().item())
+    else:
+        ok = bool(((found & 1) == 1).all().item())
     infos = [batch.info(f) for f in range(F)]
     image_bytes = sum(i.num_pages for i in infos) * cfg.page_size
     slot_bytes = sum(i.num_indices for i in infos) * 8
     unique = sum(i.num_unique for i in infos)
     verified = ok and all(i.error == 0 for i in infos)
-    if rank == 0 and me.key_begin == 0 and n == 8_000_000 and args.log_index_size == 8:
+    if not var and rank == 0 and me.key_begin == 0 and n == 8_000_000 and args.log_index_size == 8:
         with open(os.path.join(ROOT, "tests", "golden", "sha256.json")) as fh:
             want = json.load(fh)["seq_n8000000_lis8"]["pages_sha256"]
         img = batch.image(0)
@@ -189,8 +245,15 @@ def main():
     # index slots D2H into pinned host buffers (the clockcache page buffers' stand-in).
     e2e = None
     if not args.no_e2e:
-        hk = torch.from_numpy(K.seq_keys(me.key_begin, N).reshape(-1)).pin_memory()
-        hfound = torch.empty(N, dtype=torch.int64).pin_memory()
+        if var:
+            h_in = [(d_bytes, torch.from_numpy(w["bytes"]).pin_memory()),
+                    (d_offs, torch.from_numpy(w["offs"].view(np.int64)).pin_memory()),
+                    (p_bytes, torch.from_numpy(w["probe_bytes"]).pin_memory()),
+                    (p_offs, torch.from_numpy(w["probe_offs"].view(np.int64)).pin_memory()),
+                    (fid, torch.from_numpy(w["probe_fid"].view(np.int32)).pin_memory())]
+        else:
+            h_in = [(keys.view(-1), torch.from_numpy(K.seq_keys(me.key_begin, N).reshape(-1)).pin_memory())]
+        hfound = torch.empty(P, dtype=torch.int64).pin_memory()
         hpages = [torch.empty(i.num_pages * cfg.page_size, dtype=torch.uint8).pin_memory() for i in infos]
         hslots = [torch.empty(i.num_indices, dtype=torch.int64).pin_memory() for i in infos]
         reps = 3
@@ -198,7 +261,8 @@ def main():
         te = time.perf_counter()
         for _ in range(reps):
             with torch.cuda.stream(stream):
-                keys.view(-1).copy_(hk, non_blocking=True)
+                for d, h in h_in:
+                    d.copy_(h, non_blocking=True)
             step()
             with torch.cuda.stream(stream):
                 hfound.copy_(found, non_blocking=True)
@@ -206,13 +270,16 @@ def main():
                 batch.read_image_async(f, hpages[f], hslots[f], stream.cuda_stream)
         stream.synchronize()
         e2e = S.sum_over_ranks(N * reps / (time.perf_counter() - te) / 1e6, dist, dev)
-        ok_e2e = bool(((hfound & 1) == 1).all().item())
+        if var:
+            ok_e2e = bool(((hfound[torch.from_numpy(w["positive"])] & 1) == 1).all().item())
+        else:
+            ok_e2e = bool(((hfound & 1) == 1).all().item())
         verified = verified and ok_e2e
 
     ms = {k: float(np.mean(v)) for k, v in stages.items()}
     kern = {}
     for k in ("partition", "count_scan", "scatter", "cb_sort", "cb_sort_big", "layout", "assemble", "probe"):
-        b = stage_bytes(k, N, N, image_bytes, slot_bytes, unique)
+        b = stage_bytes(k, N, P, image_bytes, slot_bytes, unique, key_bytes, probe_key_bytes)
         kern[k] = {"ms": round(ms[k], 4)}
         if b:
             kern[k]["alg_bytes"] = int(b)
@@ -220,7 +287,7 @@ def main():
     dom = max(("partition", "cb_sort", "assemble", "probe"), key=lambda k: ms[k])
     achieved = kern[dom]["gbs"]
     traffic = None
-    if os.path.exists(args.pmc):
+    if not var and os.path.exists(args.pmc):
         try:
             with open(args.pmc) as fh:
                 pm = json.load(fh)
@@ -242,13 +309,15 @@ def main():
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic: sequential-id 24 B keys (filter_test format), generated in HBM",
+        "data": ("synthetic: variable-length 8-100 B keys (splitmix64), Zipf(0.99) probe mix, copied to HBM "
+                 "before timing" if var else
+                 "synthetic: sequential-id 24 B keys (filter_test format), generated in HBM"),
         "config": {"workload": wdesc, "filters_total": F_total,
-                   "filters_per_gpu": F, "keys_per_filter": n, "key_len": 24,
+                   "filters_per_gpu": F, "keys_per_filter": n, "key_len": "8-100" if var else 24,
                    "fingerprint_size": 26, "log_index_size": args.log_index_size, "seed": 42,
                    "parallelism": f"key-range shards, {world} rank(s), no data-path collective"},
         "build_mkeys_s": round(keys_all / (build_ms * 1e-3) / 1e6, 1),
-        "probe_mkeys_s": round(keys_all / (probe_ms * 1e-3) / 1e6, 1),
+        "probe_mkeys_s": round(S.sum_over_ranks(float(P), dist, dev) / (probe_ms * 1e-3) / 1e6, 1),
         "e2e_pcie_mkeys_s": round(e2e, 1) if e2e else None,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -257,7 +326,8 @@ def main():
         "verified": verified,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args, args.log_index_size, n)
+        cb = cpu_baseline_var(args, args.log_index_size, w, F, n) if var else \
+            cpu_baseline(args, args.log_index_size, n)
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu"] = round(value / cb["value"], 1)
     if rank == 0:

@@ -83,6 +83,14 @@ def lib():
         L.rfo_bench_probe.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Filter),
                                       ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                       ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        L.rfo_bench_build_var.restype = ctypes.c_double
+        L.rfo_bench_build_var.argtypes = [ctypes.POINTER(Config), ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                          ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(Filter)]
+        L.rfo_bench_probe_var.restype = ctypes.c_double
+        L.rfo_bench_probe_var.argtypes = [ctypes.POINTER(Config), ctypes.POINTER(Filter),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         _lib = L
     return _lib
 

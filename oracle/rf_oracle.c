@@ -778,6 +778,7 @@ typedef struct bench_ctx {
    rfo_filter *keep;
    _Atomic uint32_t next;
    _Atomic int err;
+   const uint64_t *offs; /* variable-length keys: key i = keys[offs[i] .. offs[i+1]) */
    /* probe */
    const rfo_filter *filters;
    const uint32_t *filter_id;
@@ -802,7 +803,9 @@ static void *build_worker(void *arg)
       }
       uint32_t n = c->key_count[f];
       uint32_t *fps = (uint32_t *)malloc((size_t)n * sizeof(uint32_t) + 4);
-      if (c->hash_keys) {
+      if (c->offs) {
+         rfo_hash_var(c->keys, c->offs + c->key_start[f], n, c->cfg->seed, fps);
+      } else if (c->hash_keys) {
          rfo_hash_fixed(c->keys + c->key_start[f] * c->key_len, n, c->key_len, c->cfg->seed, fps);
       } else {
          memcpy(fps, (const uint32_t *)c->keys + c->key_start[f], (size_t)n * 4);
@@ -821,12 +824,14 @@ static void *build_worker(void *arg)
    return NULL;
 }
 
-double rfo_bench_build(const rfo_config *cfg, const uint8_t *keys, uint32_t key_len,
-                       int hash_keys, const uint64_t *key_start, const uint32_t *key_count,
-                       uint32_t num_filters, uint16_t value, int threads, rfo_filter *keep)
+static double bench_build(const rfo_config *cfg, const uint8_t *keys, const uint64_t *offs,
+                          uint32_t key_len, int hash_keys, const uint64_t *key_start,
+                          const uint32_t *key_count, uint32_t num_filters, uint16_t value,
+                          int threads, rfo_filter *keep)
 {
    bench_ctx c;
    memset(&c, 0, sizeof(c));
+   c.offs = offs;
    c.cfg = cfg;
    c.keys = keys;
    c.key_len = key_len;
@@ -863,19 +868,38 @@ static void *probe_worker(void *arg)
       }
       uint64_t e = s + chunk < c->n ? s + chunk : c->n;
       for (uint64_t i = s; i < e; i++) {
-         uint32_t h = rfo_xxh32(c->keys + i * c->key_len, c->key_len, c->cfg->seed);
+         uint32_t h = c->offs ? rfo_xxh32(c->keys + c->offs[i], (size_t)(c->offs[i + 1] - c->offs[i]),
+                                          c->cfg->seed)
+                              : rfo_xxh32(c->keys + i * c->key_len, c->key_len, c->cfg->seed);
          c->found[i] = rfo_filter_lookup_hash(c->cfg, &c->filters[c->filter_id[i]], h);
       }
    }
    return NULL;
 }
 
-double rfo_bench_probe(const rfo_config *cfg, const rfo_filter *filters, const uint8_t *keys,
-                       uint32_t key_len, const uint32_t *filter_id, uint64_t n, int threads,
-                       uint64_t *found)
+double rfo_bench_build(const rfo_config *cfg, const uint8_t *keys, uint32_t key_len,
+                       int hash_keys, const uint64_t *key_start, const uint32_t *key_count,
+                       uint32_t num_filters, uint16_t value, int threads, rfo_filter *keep)
+{
+   return bench_build(cfg, keys, NULL, key_len, hash_keys, key_start, key_count, num_filters,
+                      value, threads, keep);
+}
+
+double rfo_bench_build_var(const rfo_config *cfg, const uint8_t *bytes, const uint64_t *offs,
+                           const uint64_t *key_start, const uint32_t *key_count,
+                           uint32_t num_filters, uint16_t value, int threads, rfo_filter *keep)
+{
+   return bench_build(cfg, bytes, offs, 0, 1, key_start, key_count, num_filters, value, threads,
+                      keep);
+}
+
+static double bench_probe(const rfo_config *cfg, const rfo_filter *filters, const uint8_t *keys,
+                          const uint64_t *offs, uint32_t key_len, const uint32_t *filter_id,
+                          uint64_t n, int threads, uint64_t *found)
 {
    bench_ctx c;
    memset(&c, 0, sizeof(c));
+   c.offs = offs;
    c.cfg = cfg;
    c.keys = keys;
    c.key_len = key_len;
@@ -897,4 +921,18 @@ double rfo_bench_probe(const rfo_config *cfg, const rfo_filter *filters, const u
    double t1 = now_s();
    free(th);
    return t1 - t0;
+}
+
+double rfo_bench_probe(const rfo_config *cfg, const rfo_filter *filters, const uint8_t *keys,
+                       uint32_t key_len, const uint32_t *filter_id, uint64_t n, int threads,
+                       uint64_t *found)
+{
+   return bench_probe(cfg, filters, keys, NULL, key_len, filter_id, n, threads, found);
+}
+
+double rfo_bench_probe_var(const rfo_config *cfg, const rfo_filter *filters, const uint8_t *bytes,
+                           const uint64_t *offs, const uint32_t *filter_id, uint64_t n,
+                           int threads, uint64_t *found)
+{
+   return bench_probe(cfg, filters, bytes, offs, 0, filter_id, n, threads, found);
 }

@@ -102,6 +102,13 @@ double rfo_bench_build(const rfo_config *cfg, const uint8_t *keys, uint32_t key_
 double rfo_bench_probe(const rfo_config *cfg, const rfo_filter *filters,
                        const uint8_t *keys, uint32_t key_len, const uint32_t *filter_id,
                        uint64_t n, int threads, uint64_t *found);
+/* variable-length keys (bytes + n+1 offsets, default_data_config hashing) */
+double rfo_bench_build_var(const rfo_config *cfg, const uint8_t *bytes, const uint64_t *offs,
+                           const uint64_t *key_start, const uint32_t *key_count,
+                           uint32_t num_filters, uint16_t value, int threads, rfo_filter *keep);
+double rfo_bench_probe_var(const rfo_config *cfg, const rfo_filter *filters, const uint8_t *bytes,
+                           const uint64_t *offs, const uint32_t *filter_id, uint64_t n,
+                           int threads, uint64_t *found);
 
 #ifdef __cplusplus
 }

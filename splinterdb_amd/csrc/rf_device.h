@@ -61,24 +61,28 @@ __device__ __forceinline__ uint32_t xxh32_words(const uint32_t* p, uint32_t len,
   return xavalanche(h);
 }
 
-// Arbitrary alignment (variable-length keys): byte loads, assembled little-endian.
-__device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-__device__ __forceinline__ uint32_t xxh32_bytes(const uint8_t* p, uint32_t len, uint32_t seed) {
+// Arbitrary alignment: gfx950 global loads accept unaligned addresses, so each 16-byte
+// stripe is ONE dwordx4 load (memcpy lets the compiler emit it) and every load stays inside
+// the key's own bytes.
+__device__ __forceinline__ uint32_t xxh32_unaligned(const uint8_t* p, uint32_t len, uint32_t seed) {
   uint32_t h, i = 0;
   if (len >= 16) {
     uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
     for (; i + 16 <= len; i += 16) {
-      v1 = xround(v1, ld_u32_bytes(p + i)); v2 = xround(v2, ld_u32_bytes(p + i + 4));
-      v3 = xround(v3, ld_u32_bytes(p + i + 8)); v4 = xround(v4, ld_u32_bytes(p + i + 12));
+      uint4 w;
+      __builtin_memcpy(&w, p + i, 16);
+      v1 = xround(v1, w.x); v2 = xround(v2, w.y); v3 = xround(v3, w.z); v4 = xround(v4, w.w);
     }
     h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
   } else {
     h = seed + XP5;
   }
   h += len;
-  for (; i + 4 <= len; i += 4) h = rotl32(h + ld_u32_bytes(p + i) * XP3, 17) * XP4;
+  for (; i + 4 <= len; i += 4) {
+    uint32_t w;
+    __builtin_memcpy(&w, p + i, 4);
+    h = rotl32(h + w * XP3, 17) * XP4;
+  }
   for (; i < len; i++) h = rotl32(h + (uint32_t)p[i] * XP5, 11) * XP1;
   return xavalanche(h);
 }
