@@ -413,6 +413,19 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   }
 }
 
+// Diagnostics: with g_dbg_ts set (rf_amd_debug_phase_buffer), workgroup b's thread 0
+// stamps the shader clock at phase k of a kernel into g_dbg_ts[b * 16 + k] (phase timing).
+__device__ uint64_t* g_dbg_ts = nullptr;
+#define DBG_PHASE(k)                                                         \
+  do {                                                                       \
+    uint64_t* _ts = g_dbg_ts;                                                \
+    if (_ts && threadIdx.x == 0) _ts[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_ts), &d_buf, sizeof(d_buf)) == hipSuccess ? 0 : 1;
+}
+
 // ======================================================================================
 // K4: per coarse bucket sort / dedupe / index counts
 // ======================================================================================
@@ -429,6 +442,14 @@ __device__ __forceinline__ bool ent_drop(EntT x, EntT prev) {
   else return x == prev;
 }
 
+// 8-input sorting network (Batcher odd-even merge, 19 compare-exchanges)
+template <typename T>
+__device__ __forceinline__ void sort8(T (&x)[8]) {
+#define CE(a, b) { const T lo = x[a] < x[b] ? x[a] : x[b], hi = x[a] < x[b] ? x[b] : x[a]; x[a] = lo; x[b] = hi; }
+  CE(0, 1) CE(2, 3) CE(4, 5) CE(6, 7) CE(0, 2) CE(1, 3) CE(4, 6) CE(5, 7) CE(1, 2) CE(5, 6)
+  CE(0, 4) CE(1, 5) CE(2, 6) CE(3, 7) CE(2, 4) CE(3, 5) CE(1, 2) CE(3, 4) CE(5, 6)
+#undef CE
+}
 // Finish a sorted coarse bucket held in `B` (LDS or global): write per-index counts and
 // starts, the compacted entries, and the num_unique contribution. Shared by K4 and K4b.
 struct CbCtx {
@@ -473,7 +494,7 @@ __device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_
 }
 
 template <typename EntT>
-__global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restrict__ plans,
+__global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ cb_filter,
                                                      const uint32_t* __restrict__ cb_count,
                                                      const uint32_t* __restrict__ cb_start,
@@ -487,11 +508,16 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
                                                      uint32_t* __restrict__ has_old,
                                                      const uint32_t* __restrict__ spill) {
   constexpr int PER = SORT_CAP / SORT_NT;
+  DBG_PHASE(15);
   __shared__ EntT s_b[SORT_CAP];
   __shared__ uint32_t s_bin[MAX_BINS + 1];
   __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
   __shared__ uint32_t s_fo[sizeof(EntT) == 8 ? MAX_IPC : 1];
   __shared__ uint32_t s_ho[sizeof(EntT) == 8 ? MAX_IPC : 1];
+  constexpr uint32_t BIG_LIST = 64;
+  __shared__ uint32_t s_big[BIG_LIST];  // bins over 8 entries (s_nbig may exceed the list)
+  __shared__ uint32_t s_nbig;
+  uint32_t* s_first = s_bin;  // compacted start of each index: reuses s_bin once bins are sorted
   const uint32_t cb = blockIdx.x;
   const uint32_t f = cb_filter[cb];
   const FilterPlan& P = plans[f];
@@ -511,7 +537,9 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
   if constexpr (sizeof(EntT) == 8) {
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
+  if (threadIdx.x == 0) s_nbig = 0;
   __syncthreads();
+  DBG_PHASE(0);
   // load + per-bin rank (bin = filter bucket within the coarse bucket)
   EntT v[PER];
   uint32_t r[PER];
@@ -529,6 +557,7 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
     }
   }
   __syncthreads();
+  DBG_PHASE(1);
   // exclusive scan of bin counts (nbins <= MAX_BINS = 8 * SORT_NT)
   {
     constexpr int BPT = MAX_BINS / SORT_NT;
@@ -550,6 +579,7 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
     if (threadIdx.x == 0) s_bin[nbins] = n;
   }
   __syncthreads();
+  DBG_PHASE(2);
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t i = threadIdx.x + k * SORT_NT;
@@ -560,26 +590,96 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
     }
   }
   __syncthreads();
-  // insertion sort inside each bin (bins hold ~1-2 entries for random keys)
-  for (uint32_t b = threadIdx.x; b < nbins; b += SORT_NT) {
-    const uint32_t s = s_bin[b], e = s_bin[b + 1];
-    for (uint32_t i = s + 1; i < e; i++) {
-      const EntT x = s_b[i];
-      uint32_t j = i;
-      while (j > s && s_b[j - 1] > x) {
-        s_b[j] = s_b[j - 1];
-        j--;
+  DBG_PHASE(3);
+  // order inside each bin: one thread per bin; bins of up to 8 entries (all but ~1 in 3000
+  // for random keys) are loaded into registers together, put through an 8-input sorting
+  // network and written back (two bins per step, so their LDS reads share one wait). Larger
+  // bins are listed and ranked afterwards by a whole wave each: lane j's entry goes to the
+  // bin start + the number of entries that sort before it (smaller, or equal and earlier).
+  {
+    constexpr EntT EMAX = ~EntT(0);
+    static_assert(MAX_BINS % (2 * SORT_NT) == 0, "two bins per thread and step");
+    for (uint32_t b0 = threadIdx.x; b0 < nbins; b0 += 2 * SORT_NT) {
+      uint32_t st[2], cnt[2];
+      EntT x[2][8];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t b = b0 + h * SORT_NT;
+        st[h] = b < nbins ? s_bin[b] : 0u;
+        cnt[h] = b < nbins ? s_bin[b + 1] - st[h] : 0u;
       }
-      s_b[j] = x;
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[h][j] = ((uint32_t)j < cnt[h] && cnt[h] <= 8) ? s_b[st[h] + j] : EMAX;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        sort8(x[h]);
+        if (cnt[h] >= 2 && cnt[h] <= 8) {
+#pragma unroll
+          for (int j = 0; j < 8; j++)
+            if ((uint32_t)j < cnt[h]) s_b[st[h] + j] = x[h][j];
+        } else if (cnt[h] > 8) {
+          const uint32_t q = atomicAdd(&s_nbig, 1u);
+          if (q < BIG_LIST) s_big[q] = b0 + h * SORT_NT;
+        }
+      }
     }
   }
   __syncthreads();
+  if (s_nbig) {
+    const uint32_t nb = s_nbig;
+    if (nb <= BIG_LIST) {
+      const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+      for (uint32_t q = wv; q < nb; q += SORT_NT / WAVE) {
+        const uint32_t b = s_big[q], st = s_bin[b], cnt = s_bin[b + 1] - st;
+        if (cnt <= WAVE) {
+          EntT mine = lane < cnt ? s_b[st + lane] : EntT(0);
+          uint32_t before = 0;
+          for (uint32_t j = 0; j < cnt; j++) {
+            const EntT y = s_b[st + j];  // same address in every lane: a broadcast
+            before += (y < mine || (y == mine && j < lane)) ? 1u : 0u;
+          }
+          __builtin_amdgcn_wave_barrier();  // all reads of the bin before any write
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+          if (lane < cnt) s_b[st + before] = mine;
+        } else if (lane == 0) {  // > 64 entries in one bucket: insertion sort
+          for (uint32_t i = st + 1; i < st + cnt; i++) {
+            const EntT y = s_b[i];
+            uint32_t j = i;
+            while (j > st && s_b[j - 1] > y) {
+              s_b[j] = s_b[j - 1];
+              j--;
+            }
+            s_b[j] = y;
+          }
+        }
+      }
+    } else {  // many large bins (duplicate-heavy input): insertion sort each
+      for (uint32_t b = threadIdx.x; b < nbins; b += SORT_NT) {
+        const uint32_t st = s_bin[b], en = s_bin[b + 1];
+        if (en - st <= 8) continue;
+        for (uint32_t i = st + 1; i < en; i++) {
+          const EntT y = s_b[i];
+          uint32_t j = i;
+          while (j > st && s_b[j - 1] > y) {
+            s_b[j] = s_b[j - 1];
+            j--;
+          }
+          s_b[j] = y;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  DBG_PHASE(4);
   // dedupe + compaction: thread t owns the contiguous run [t*PER, t*PER + PER)
   uint32_t keep_mask = 0, cnt = 0;
   EntT w[PER];
+  const uint32_t i0 = threadIdx.x * PER;
+  const EntT prev0 = (i0 > 0 && i0 <= n) ? s_b[i0 - 1] : EntT(0);
   {
-    const uint32_t i0 = threadIdx.x * PER;
-    EntT prev = (i0 > 0 && i0 <= n) ? s_b[i0 - 1] : EntT(0);
+    EntT prev = prev0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const uint32_t i = i0 + k;
@@ -594,21 +694,46 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
   uint32_t kept;
   uint32_t pos = block_excl_scan<SORT_NT>(cnt, s_tmp, &kept);  // has barriers: reads done
   uint32_t* s_sorted = reinterpret_cast<uint32_t*>(s_b);        // compacted e values (u32)
+  // Index bounds and num_unique in the same pass. A dropped entry equals its sorted
+  // predecessor, so the previous SORTED entry has the index and fingerprint of the previous
+  // KEPT one. Indices (index of previous entry, index of this kept entry] start here.
+  // num_unique (:558, :572-574): per index, entries whose fingerprint differs from the
+  // previous entry's; an index's first entry compares against UINT32_MAX >> value_size.
+  const uint32_t NONE = 0xffffffffu;
+  auto index_of = [&](uint32_t e) -> uint32_t { return ish >= 32 ? 0u : ((e >> ish) & (ipc - 1)); };
+  uint32_t lprev = (i0 > 0 && i0 <= n) ? index_of(ent_e(prev0)) : NONE;
+  uint32_t fprev = (i0 > 0 && i0 <= n) ? (ent_e(prev0) >> P.vs) : 0u;
+  uint32_t uniq = 0;
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    if (keep_mask & (1u << k)) {
+    const uint32_t i = i0 + k;
+    if (i < n) {
       const uint32_t e = ent_e(w[k]);
-      s_sorted[pos++] = e;
-      if constexpr (sizeof(EntT) == 8) {
-        if (!(w[k] & 1ull)) {  // old entry: remember each index's smallest (num_unique quirk)
-          const uint32_t li = ish >= 32 ? 0u : ((e >> ish) & (ipc - 1));
-          atomicMin(&s_fo[li], e);
-          s_ho[li] = 1;
+      const uint32_t li = index_of(e), fp = e >> P.vs;
+      if (keep_mask & (1u << k)) {
+        s_sorted[pos] = e;
+        for (uint32_t l = lprev + 1; l <= li; l++) s_first[l] = pos;  // lprev NONE: from 0
+        uniq += (fp != (li != lprev ? (0xffffffffu >> P.vs) : fprev)) ? 1u : 0u;
+        pos++;
+        if constexpr (sizeof(EntT) == 8) {
+          if (!(w[k] & 1ull)) {  // old entry: remember each index's smallest (num_unique quirk)
+            atomicMin(&s_fo[li], e);
+            s_ho[li] = 1;
+          }
         }
       }
+      lprev = li;
+      fprev = fp;
     }
   }
   __syncthreads();
+  DBG_PHASE(5);
+  {  // indices after the last entry's start at `kept`
+    const uint32_t llast = kept ? index_of(s_sorted[kept - 1]) : NONE;
+    for (uint32_t l = threadIdx.x; l < ipc; l += SORT_NT)
+      if (llast == NONE || l > llast) s_first[l] = kept;
+    if (threadIdx.x == 0) s_first[ipc] = kept;
+  }
   if constexpr (sizeof(EntT) == 8) {
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) {
       first_old[c.idx0 + i] = s_fo[i];
@@ -617,10 +742,17 @@ __global__ __launch_bounds__(SORT_NT) void k_cb_sort(const FilterPlan* __restric
   }
   uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
   for (uint32_t i = threadIdx.x; i < kept; i += SORT_NT) dst[i] = s_sorted[i];
-  uint32_t uniq, tot_uniq;
-  write_index_bounds(c, s_sorted, kept, idx_cnt, idx_start, &uniq);
+  __syncthreads();
+  DBG_PHASE(6);
+  for (uint32_t l = threadIdx.x; l < ipc; l += SORT_NT) {
+    idx_cnt[c.idx0 + l] = s_first[l + 1] - s_first[l];
+    idx_start[c.idx0 + l] = c.cb_rel + s_first[l];
+  }
+  DBG_PHASE(7);
+  uint32_t tot_uniq;
   block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
   if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
+  DBG_PHASE(8);
 }
 
 // K4b: coarse buckets larger than LDS (duplicate-heavy inputs). One workgroup per listed

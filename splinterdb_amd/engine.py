@@ -34,7 +34,7 @@ EXPORTED = [
     "rf_amd_batch_probe_var_keys", "rf_amd_batch_probe_hashes", "rf_amd_batch_info",
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
     "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_debug_probe_ablate",
-    "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines",
+    "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer",
     "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",
     "rf_amd_image_free",
     "rf_amd_max_fingerprints", "rf_amd_estimate_unique_keys_from_count",
@@ -109,6 +109,7 @@ def load_library(build_if_missing=True):
     L.rf_amd_debug_probe_ablate.argtypes = [u32]
     L.rf_amd_debug_read_lines.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
     L.rf_amd_debug_rebuild_lines.argtypes = [vp]
+    L.rf_amd_debug_phase_buffer.argtypes = [vp]
     L.rf_amd_debug_probe_ablate.restype = None
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
