@@ -125,9 +125,10 @@ void rf_amd_debug_probe_ablate(uint32_t mode);
  * host (h_lines == NULL: only *num_lines is set); rebuild_lines re-cuts them from the
  * filter images with the image-upload kernel (k_plines), so a test can check that the
  * build's lines and the image's lines are byte-identical. */
-/* diagnostics: a device buffer of 16 u64 per workgroup (NULL = off); instrumented kernels
- * (the bucket sort) stamp the shader clock at each phase into it (tools/phase_times.py). */
-int rf_amd_debug_phase_buffer(void *d_buf);
+/* diagnostics: a device buffer of 16 u64 per workgroup (NULL = off); the instrumented kernel
+ * chosen by `kernel` (1 = bucket sort, 2 = fused partition) stamps the shader clock at each
+ * of its phases into it (tools/phase_times.py). */
+int rf_amd_debug_phase_buffer(void *d_buf, uint32_t kernel);
 int rf_amd_debug_read_lines(rf_amd_batch *b, uint8_t *h_lines, uint64_t bytes, uint64_t *num_lines);
 int rf_amd_debug_rebuild_lines(rf_amd_batch *b);
 int rf_amd_batch_timings(rf_amd_batch *b, float *ms, uint32_t n);

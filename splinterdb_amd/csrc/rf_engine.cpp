@@ -491,9 +491,9 @@ extern "C" int rf_amd_batch_probe_hashes(rf_amd_batch* b, const uint32_t* d_hash
 // the probe kernel at that many waves per SIMD via LDS padding (occupancy experiments).
 extern "C" void rf_amd_debug_probe_ablate(uint32_t mode) { g_probe_ablate = mode; }
 
-extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf);
-extern "C" int rf_amd_debug_phase_buffer(void* d_buf) {
-  return rf_debug_set_phase_buffer(static_cast<uint64_t*>(d_buf)) ? fail(RF_AMD_EINVAL, "phase buffer") : 0;
+extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid);
+extern "C" int rf_amd_debug_phase_buffer(void* d_buf, uint32_t kernel) {
+  return rf_debug_set_phase_buffer(static_cast<uint64_t*>(d_buf), kernel) ? fail(RF_AMD_EINVAL, "phase buffer") : 0;
 }
 
 extern "C" int rf_amd_debug_read_lines(rf_amd_batch* b, uint8_t* h_lines, uint64_t bytes, uint64_t* num_lines) {

@@ -280,6 +280,24 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
   }
 }
 
+// Diagnostics: with g_dbg_ts set (rf_amd_debug_phase_buffer), workgroup b's thread 0
+// stamps the shader clock at phase k of a kernel into g_dbg_ts[b * 16 + k] (phase timing).
+// g_dbg_kid selects the kernel: 1 = bucket sort (K4), 2 = fused partition (K1+K3).
+__device__ uint64_t* g_dbg_ts = nullptr;
+__device__ uint32_t g_dbg_kid = 0;
+#define DBG_PHASE_K(kid, k)                                                  \
+  do {                                                                       \
+    uint64_t* _ts = g_dbg_ts;                                                \
+    if (_ts && g_dbg_kid == (kid) && threadIdx.x == 0)                       \
+      _ts[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();             \
+  } while (0)
+#define DBG_PHASE(k) DBG_PHASE_K(1, k)
+
+extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_kid), &kid, sizeof(kid)) != hipSuccess) return 1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_ts), &d_buf, sizeof(d_buf)) == hipSuccess ? 0 : 1;
+}
+
 // ======================================================================================
 // K1+K3 fused (fresh builds, 32-bit entries): hash a tile, rank its entries by coarse
 // bucket in LDS, reserve each bucket's run with one atomic, and write the runs straight
@@ -303,6 +321,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   __shared__ uint32_t s_tmp[SCAT_NT / WAVE + 1];
   constexpr int PER = TILE_KEYS / SCAT_NT;
   constexpr int BPT = MAX_CB / SCAT_NT;
+  DBG_PHASE_K(2, 15);
   const uint32_t t = blockIdx.x;
   const FilterPlan& P = plans[tile_filter[t]];
   const uint32_t start = tile_start[t];
@@ -310,6 +329,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   const uint32_t num_cb = 1u << P.cbits;
   for (uint32_t i = threadIdx.x; i < num_cb; i += SCAT_NT) s_off[i] = 0;
   __syncthreads();
+  DBG_PHASE_K(2, 0);
   const uint32_t esh = fp_size + P.vs - P.cbits;  // entry >> esh = coarse bucket
   auto cb_of = [&](uint32_t e) -> uint32_t { return P.cbits ? (e >> esh) : 0u; };
   uint32_t v[PER], rank[PER];
@@ -365,6 +385,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
     if (threadIdx.x + k * SCAT_NT < count) rank[k] = atomicAdd(&s_off[cb_of(v[k])], 1u);
   }
   __syncthreads();
+  DBG_PHASE_K(2, 1);
   uint32_t cnt[BPT], sum = 0;
 #pragma unroll
   for (int k = 0; k < BPT; k++) {
@@ -392,18 +413,21 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   }
   if (over) atomicOr(spill, 1u);
   __syncthreads();
+  DBG_PHASE_K(2, 2);
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = threadIdx.x + k * SCAT_NT;
     if (j < count) s_stage[s_off[cb_of(v[k])] + rank[k]] = v[k];
   }
   __syncthreads();
+  DBG_PHASE_K(2, 3);
 #pragma unroll
   for (int k = 0; k < BPT; k++) {
     const uint32_t b = threadIdx.x * BPT + k;
     if (b < num_cb) s_off[b] = gslot[k];
   }
   __syncthreads();
+  DBG_PHASE_K(2, 4);
   uint32_t* dst = part + P.e_first;
   for (uint32_t j = threadIdx.x; j < total; j += SCAT_NT) {
     const uint32_t x = s_stage[j];
@@ -411,19 +435,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
     const uint32_t slot = s_off[cb] + j;  // position inside the bucket's region
     if (slot < (uint32_t)SORT_CAP) dst[(uint64_t)cb * SORT_CAP + slot] = x;
   }
-}
-
-// Diagnostics: with g_dbg_ts set (rf_amd_debug_phase_buffer), workgroup b's thread 0
-// stamps the shader clock at phase k of a kernel into g_dbg_ts[b * 16 + k] (phase timing).
-__device__ uint64_t* g_dbg_ts = nullptr;
-#define DBG_PHASE(k)                                                         \
-  do {                                                                       \
-    uint64_t* _ts = g_dbg_ts;                                                \
-    if (_ts && threadIdx.x == 0) _ts[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-
-extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_ts), &d_buf, sizeof(d_buf)) == hipSuccess ? 0 : 1;
+  DBG_PHASE_K(2, 8);
 }
 
 // ======================================================================================
@@ -1024,6 +1036,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
     __syncthreads();
     uint32_t after_wave = 0xffffffffu;
     for (int w2 = wv + 1; w2 < LAYOUT_NT / WAVE; w2++) after_wave = min(after_wave, s_tmp[w2]);
+    __syncthreads();  // every wave has read s_tmp before block_excl_scan below rewrites it
     uint32_t xn = __shfl_down(x, 1, WAVE);
     if (lane == WAVE - 1) xn = 0xffffffffu;
     const uint32_t beyond = min(xn, after_wave);  // min over threads > t

@@ -208,6 +208,31 @@ def test_duplicate_heavy_overflow_path(oracle):
         assert (img.slots == of.slots()[: of.num_indices]).all()
 
 
+def test_repeated_fingerprint_bins(oracle):
+    """Buckets of 9-64 entries (ranked by a whole wave in K4) and over 64 (insertion sort),
+    in LDS-resident coarse buckets, fresh and incremental (64-bit entries)."""
+    cfg = E.routing_config_init()
+    ocfg = oracle.make_config()
+    rng = np.random.default_rng(3)
+    for rep in (10, 30, 70, 200):
+        base = rng.integers(0, 1 << 32, size=200_000 // rep, dtype=np.uint64).astype(np.uint32)
+        h = rng.permutation(np.repeat(base, rep)).astype(np.uint32)
+        b = E.FilterBatch(cfg, [h.size], [1])
+        b.build_hashes(dev(h))
+        img = b.image(0)
+        of = oracle.filter_add(ocfg, h, value=1)
+        assert (img.num_unique, img.num_pages) == (of.num_unique, of.num_pages), rep
+        assert (img.pages == of.pages()).all(), rep
+        assert (img.slots == of.slots()[: of.num_indices]).all(), rep
+        # incremental: the same multiset again with value 2, merged into the old filter
+        b2 = E.FilterBatch(cfg, [h.size], [2], old=[(b, 0)])
+        b2.build_hashes(dev(h))
+        img2 = b2.image(0)
+        of2 = oracle.filter_add(ocfg, h, value=2, old=of)
+        assert (img2.num_unique, img2.num_pages) == (of2.num_unique, of2.num_pages), rep
+        assert (img2.pages == of2.pages()).all(), rep
+
+
 def test_multi_filter_random_sizes_vs_oracle(oracle):
     """C3-style concurrent builds: mixed sizes/values in one batch, random probe routing"""
     cfg = E.routing_config_init(log_index_size=9)

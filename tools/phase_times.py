@@ -10,8 +10,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from splinterdb_amd import engine as E  # noqa: E402
 from splinterdb_amd import keys as K  # noqa: E402
 
-F = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 8_000_000
+KID = int(sys.argv[1]) if len(sys.argv) > 1 else 1  # 1 = bucket sort, 2 = fused partition
+F = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+n = int(sys.argv[3]) if len(sys.argv) > 3 else 8_000_000
 cfg = E.routing_config_init()
 keys = K.seq_keys_torch(0, F * n, 24, "cuda:0")
 b = E.FilterBatch(cfg, [n] * F)
@@ -20,21 +21,24 @@ for _ in range(2):
 torch.cuda.synchronize()
 buf = torch.zeros(1 << 22, dtype=torch.int64, device="cuda:0")
 L = E.load_library()
-E._check(L.rf_amd_debug_phase_buffer(buf.data_ptr()))
+E._check(L.rf_amd_debug_phase_buffer(buf.data_ptr(), KID))
 b.build_keys(keys, 24)
 torch.cuda.synchronize()
-E._check(L.rf_amd_debug_phase_buffer(None))
+E._check(L.rf_amd_debug_phase_buffer(None, 0))
 ts = buf.cpu().numpy().reshape(-1, 16)
 used = ts[:, 8] != 0
 ts = ts[used]
 print(f"workgroups stamped: {ts.shape[0]}")
-names = {15: "entry", 0: "init", 1: "load+rank", 2: "bin scan", 3: "scatter", 4: "bin sort",
-         5: "dedupe+compact", 6: "write out", 7: "index bounds", 8: "uniq+end"}
-order = [15, 0, 1, 2, 3, 4, 5, 6, 7, 8]
+if KID == 1:
+    names = {15: "entry", 0: "init", 1: "load+rank", 2: "bin scan", 3: "scatter", 4: "bin sort",
+             5: "dedupe+compact", 6: "write out", 7: "index bounds", 8: "uniq+end"}
+    order = [15, 0, 1, 2, 3, 4, 5, 6, 7, 8]
+else:
+    names = {15: "entry", 0: "init", 1: "load+hash+rank", 2: "scan+reserve", 3: "stage", 4: "slots",
+             8: "write runs"}
+    order = [15, 0, 1, 2, 3, 4, 8]
 tot = (ts[:, 8] - ts[:, 15]).astype(np.float64)
 print(f"per workgroup: mean {tot.mean():.0f} cycles, median {np.median(tot):.0f}")
 for a, c in zip(order[:-1], order[1:]):
     d = (ts[:, c] - ts[:, a]).astype(np.float64)
     print(f"  {names[c]:16s} {d.mean():9.0f} cycles  ({100 * d.mean() / tot.mean():5.1f} %)")
-span = (ts[:, 8].max() - ts[:, 15].min())
-print(f"kernel span {span} cycles")
