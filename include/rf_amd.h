@@ -116,7 +116,11 @@ uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
  * build; 8 = last probe kernel.
  * Milliseconds, -1 if a stage did not run. */
 #define RF_AMD_NUM_TIMINGS 9
+/* enable = number of event sets kept (0 = off): each build starts the next set of a ring,
+ * so the stages of the last `enable` build+probe rounds can be read without synchronising
+ * between them (rf_amd_batch_timings_back: back = 0 is the latest round). */
 int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
+int rf_amd_batch_timings_back(rf_amd_batch *b, uint32_t back, float *ms, uint32_t n);
 /* diagnostics: truncate later probes after 1 = hashing, 2 = the probe-line load
  * (results are then NOT found_values); 0 restores normal probes. Bits 8+: cap the probe
  * kernel at that many waves per SIMD (occupancy experiments). */

@@ -82,7 +82,8 @@ struct rf_amd_batch {
       d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill;
   std::vector<uint32_t> old_num_indices;
   bool built = false;
-  std::vector<hipEvent_t> events;  // per-stage timing (rf_amd_batch_set_timing)
+  std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
+  uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
   ~rf_amd_batch() {
     for (auto ev : events) (void)hipEventDestroy(ev);
   }
@@ -397,7 +398,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.num_page_slots = b->PS;
   a.pages = b->d_pages.as<uint8_t>();
   a.outs = b->d_outs.p ? b->d_outs.as<FilterOut>() : nullptr;
-  a.events = b->events.empty() ? nullptr : reinterpret_cast<void**>(b->events.data());
+  a.events = b->events.empty() ? nullptr : reinterpret_cast<void**>(b->events.data() + (size_t)b->ev_set * NUM_EVENTS);
   return a;
 }
 
@@ -408,12 +409,13 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   HIPCHK(hipSetDevice(b->eng->device));
   hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
   (void)hipGetLastError();  // launch checks below must see only their own errors
+  if (b->ev_sets) b->ev_set = (b->ev_set + 1) % b->ev_sets;
   LaunchArgs a = make_args(b, st);
   a.kind = kind;
   a.in0 = in0;
   a.offs = offs;
   a.key_len = key_len;
-  if (a.events) HIPCHK(hipEventRecord(b->events[EV_B_START], st));
+  if (a.events) HIPCHK(hipEventRecord(((hipEvent_t*)a.events)[EV_B_START], st));
   HIPCHK(hipMemsetAsync(b->d_cb_count.p, 0, 4 * (size_t)b->CB, st));
   HIPCHK(hipMemsetAsync(b->d_outs.p, 0, sizeof(FilterOut) * b->F, st));
   HIPCHK(hipMemsetAsync(b->d_overflow.p, 0, 4, st));
@@ -522,31 +524,36 @@ extern "C" int rf_amd_debug_rebuild_lines(rf_amd_batch* b) {
 extern "C" int rf_amd_batch_set_timing(rf_amd_batch* b, int enable) {
   if (!b) return fail(RF_AMD_EINVAL, "null batch");
   HIPCHK(hipSetDevice(b->eng->device));
-  if (enable && b->events.empty()) {
-    b->events.resize(NUM_EVENTS);
+  for (auto ev : b->events) (void)hipEventDestroy(ev);
+  b->events.clear();
+  b->ev_sets = b->ev_set = 0;
+  if (enable > 0) {
+    b->events.resize((size_t)NUM_EVENTS * enable);
     for (auto& ev : b->events) HIPCHK(hipEventCreate(&ev));
-  } else if (!enable) {
-    for (auto ev : b->events) (void)hipEventDestroy(ev);
-    b->events.clear();
+    b->ev_sets = (uint32_t)enable;
   }
   return 0;
 }
-
-extern "C" int rf_amd_batch_timings(rf_amd_batch* b, float* ms, uint32_t n) {
+extern "C" int rf_amd_batch_timings_back(rf_amd_batch* b, uint32_t back, float* ms, uint32_t n) {
   if (!b || b->events.empty() || !ms || n < RF_AMD_NUM_TIMINGS) return fail(RF_AMD_EINVAL, "timing not enabled");
+  if (back >= b->ev_sets) return fail(RF_AMD_EINVAL, "timing set out of range");
   HIPCHK(hipSetDevice(b->eng->device));
+  const hipEvent_t* ev = b->events.data() + (size_t)((b->ev_set + b->ev_sets - back) % b->ev_sets) * NUM_EVENTS;
   static const int pairs[RF_AMD_NUM_TIMINGS][2] = {
       {EV_B_START, EV_B_HASH},    {EV_B_HASH, EV_B_SCAN},     {EV_B_SCAN, EV_B_SCATTER},
       {EV_B_SCATTER, EV_B_SORT},  {EV_B_SORT, EV_B_SORT_BIG}, {EV_B_SORT_BIG, EV_B_LAYOUT},
       {EV_B_LAYOUT, EV_B_ASSEMBLE}, {EV_B_START, EV_B_ASSEMBLE}, {EV_P_START, EV_P_END}};
   for (uint32_t i = 0; i < RF_AMD_NUM_TIMINGS; i++) {
     ms[i] = -1.f;
-    if (hipEventSynchronize(b->events[pairs[i][1]]) != hipSuccess) continue;
+    if (hipEventSynchronize(ev[pairs[i][1]]) != hipSuccess) continue;
     float t = 0;
-    if (hipEventElapsedTime(&t, b->events[pairs[i][0]], b->events[pairs[i][1]]) == hipSuccess) ms[i] = t;
+    if (hipEventElapsedTime(&t, ev[pairs[i][0]], ev[pairs[i][1]]) == hipSuccess) ms[i] = t;
   }
   (void)hipGetLastError();  // a stage not run yet (e.g. no probe) must not poison later launches
   return 0;
+}
+extern "C" int rf_amd_batch_timings(rf_amd_batch* b, float* ms, uint32_t n) {
+  return rf_amd_batch_timings_back(b, 0, ms, n);
 }
 
 extern "C" int rf_amd_batch_info(rf_amd_batch* b, uint32_t f, rf_amd_filter_info* out) {

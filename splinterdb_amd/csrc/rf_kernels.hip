@@ -282,7 +282,8 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
 
 // Diagnostics: with g_dbg_ts set (rf_amd_debug_phase_buffer), workgroup b's thread 0
 // stamps the shader clock at phase k of a kernel into g_dbg_ts[b * 16 + k] (phase timing).
-// g_dbg_kid selects the kernel: 1 = bucket sort (K4), 2 = fused partition (K1+K3).
+// g_dbg_kid selects the kernel: 1 = bucket sort (K4), 2 = fused partition (K1+K3),
+// 3 = page assembly (K6), 4 = layout (K5).
 __device__ uint64_t* g_dbg_ts = nullptr;
 __device__ uint32_t g_dbg_kid = 0;
 #define DBG_PHASE_K(kid, k)                                                  \
@@ -380,6 +381,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
                  : "v"(v[k0]), "v"(v[k0 + 1]), "v"(v[k0 + 2]), "v"(v[k0 + 3]), "v"(v[k0 + 4]),
                    "v"(v[k0 + 5]), "v"(v[k0 + 6]), "v"(v[k0 + 7]));
   }
+  DBG_PHASE_K(2, 5);  // thread 0's keys loaded and hashed (no barrier)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     if (threadIdx.x + k * SCAT_NT < count) rank[k] = atomicAdd(&s_off[cb_of(v[k])], 1u);
@@ -395,23 +397,20 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   }
   uint32_t total;
   uint32_t run = block_excl_scan<SCAT_NT>(sum, s_tmp, &total);
-  uint32_t gslot[BPT];
-  bool over = false;
+  // reserve each bucket's run in its region (global atomics), then stage the tile in LDS
+  // while the reservations are in flight; their results are first needed after staging
+  uint32_t g[BPT], lstart[BPT];
 #pragma unroll
   for (int k = 0; k < BPT; k++) {
     const uint32_t b = threadIdx.x * BPT + k;
-    gslot[k] = 0;
+    g[k] = 0;
+    lstart[k] = run;
     if (b < num_cb) {
+      if (cnt[k]) g[k] = atomicAdd(&cb_fill[P.cb_base + b], cnt[k]);
       s_off[b] = run;
-      if (cnt[k]) {
-        const uint32_t g = atomicAdd(&cb_fill[P.cb_base + b], cnt[k]);
-        over |= g + cnt[k] > (uint32_t)SORT_CAP;
-        gslot[k] = g - run;
-      }
       run += cnt[k];
     }
   }
-  if (over) atomicOr(spill, 1u);
   __syncthreads();
   DBG_PHASE_K(2, 2);
 #pragma unroll
@@ -421,11 +420,16 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   }
   __syncthreads();
   DBG_PHASE_K(2, 3);
+  bool over = false;
 #pragma unroll
   for (int k = 0; k < BPT; k++) {
     const uint32_t b = threadIdx.x * BPT + k;
-    if (b < num_cb) s_off[b] = gslot[k];
+    if (b < num_cb) {
+      over |= cnt[k] && g[k] + cnt[k] > (uint32_t)SORT_CAP;
+      s_off[b] = g[k] - lstart[k];
+    }
   }
+  if (over) atomicOr(spill, 1u);
   __syncthreads();
   DBG_PHASE_K(2, 4);
   uint32_t* dst = part + P.e_first;
@@ -914,11 +918,13 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   __shared__ uint8_t s_mark[MAX_INDICES + 1];
   __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
   __shared__ uint32_t s_err;
+  __shared__ uint32_t s_flag[2];
   const uint32_t f = blockIdx.x;
   const FilterPlan& P = plans[f];
   const uint32_t n = P.num_indices;
   const uint32_t index_size = 1u << lis;
   constexpr int PER = MAX_INDICES / LAYOUT_NT;
+  DBG_PHASE_K(4, 15);
   if (threadIdx.x == 0) s_err = 0;
   __syncthreads();
   // sizes -> exclusive prefix (contiguous ownership: thread t owns [t*PER, t*PER+PER))
@@ -954,33 +960,71 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
     }
     return;
   }
+  DBG_PHASE_K(4, 0);
   if (threadIdx.x == 0) pplans[f].w = 0;
-  // next(j) by binary search on the prefix sums
-  for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT) {
-    uint32_t q = n;
-    if (j < n) {
+  // next(j) = first block that does not fit on a page opened at block j: gallop forward
+  // from j + 1, then bisect (pages hold a handful of blocks: a few LDS reads per j). j is
+  // strided over the threads so a wave's reads fall on consecutive words (no bank conflicts).
+  {
+#pragma unroll 1
+    for (uint32_t j = threadIdx.x; j < n; j += LAYOUT_NT) {
       const uint32_t lim = s_excl[j] + page_size;
-      uint32_t lo = j + 1, hi = n + 1;  // first q in [j+1, n] with excl[q] > lim, else n+1
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_excl[mid] > lim) hi = mid; else lo = mid + 1;
+      uint32_t qp = j + 1;  // first q' > j with excl[q'] > lim (n + 1: none)
+      if (qp <= n && s_excl[qp] <= lim) {
+        uint32_t lo = qp, hi = qp + 1, step = 1;  // excl[lo] <= lim
+        while (hi <= n && s_excl[hi] <= lim) {
+          lo = hi;
+          step <<= 1;
+          hi = lo + step;
+        }
+        if (hi > n + 1) hi = n + 1;
+        while (hi - lo > 1) {  // excl[lo] <= lim < excl[hi] (hi == n + 1: past the end)
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_excl[mid] <= lim) lo = mid; else hi = mid;
+        }
+        qp = hi;
       }
-      q = lo - 1;  // block q is the first that does not fit (q == n: none)
+      s_jA[j] = (uint16_t)(qp - 1);  // block qp-1 is the first that does not fit (n: none)
     }
-    s_jA[j] = (uint16_t)q;
-    s_mark[j] = (j == 0) ? 1 : 0;
+    for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT) s_mark[j] = (j == 0) ? 1 : 0;
+    if (threadIdx.x == 0) {
+      s_jA[n] = (uint16_t)n;
+      s_flag[0] = s_flag[1] = 0;
+    }
   }
   __syncthreads();
+  DBG_PHASE_K(4, 1);
+  // mark the orbit of block 0 under next() by pointer doubling; stop once a round adds no
+  // mark (the marked set is then closed under every later jump)
   uint16_t* cur = s_jA;
   uint16_t* nxt = s_jB;
-  for (uint32_t span = 1; span <= n; span <<= 1) {
+  for (uint32_t r = 0;; r++) {
+    if (threadIdx.x == 0) s_flag[(r + 1) & 1] = 0;
     for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT)
-      if (s_mark[j]) s_mark[cur[j]] = 1;
+      if (s_mark[j]) {
+        const uint32_t t = cur[j];
+        if (!s_mark[t]) {
+          s_mark[t] = 1;
+          s_flag[r & 1] = 1;
+        }
+      }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT) nxt[j] = cur[cur[j]];
+    if (!s_flag[r & 1]) break;
+    uint32_t c1[PER + 1];  // all first reads, then all second reads (2 LDS round trips)
+#pragma unroll
+    for (int k = 0; k <= PER; k++) {
+      const uint32_t j = threadIdx.x + k * LAYOUT_NT;
+      c1[k] = j <= n ? cur[j] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k <= PER; k++) {
+      const uint32_t j = threadIdx.x + k * LAYOUT_NT;
+      if (j <= n) nxt[j] = cur[c1[k]];
+    }
     __syncthreads();
     uint16_t* t = cur; cur = nxt; nxt = t;
   }
+  DBG_PHASE_K(4, 2);
   // page numbers: inclusive scan of marks over [0, n)
   uint32_t mk[PER], msum = 0;
 #pragma unroll
@@ -1011,6 +1055,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
       if (mk[k] && pg[k] < P.page_cap) pf[pg[k]] = j;
     }
   }
+  DBG_PHASE_K(4, 3);
   // num_unique quirk of the old/new merge (src/routing_filter.c:572-590): when index j runs
   // out of entries while its old index still holds entries of a later new index, the first
   // of those is counted before the bucket check puts it back, and counted again later.
@@ -1065,6 +1110,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
       pplans[f].w = ERR_PAGE_CAP;
     }
   }
+  DBG_PHASE_K(4, 8);
 }
 
 // ======================================================================================
@@ -1167,6 +1213,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   __shared__ uint32_t s_src[ASM_MAXB];
   __shared__ uint16_t s_rblk[ASM_MAXE / ASM_RUN];  // block of each run's first entry
   __shared__ uint32_t s_tmp[ASM_NT / WAVE + 1];
+  DBG_PHASE_K(3, 15);
   const uint32_t slot = blockIdx.x;
   const uint32_t f = pg_filter[slot];
   const FilterPlan& P = plans[f];
@@ -1206,6 +1253,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
     run += cj[q];
   }
   if (threadIdx.x == 0) { s_est[nb] = ne; s_off[nb] = page_size; }
+  DBG_PHASE_K(3, 0);
   if (ne > ASM_MAXE) {  // uniform (scan total)
     __syncthreads();
     assemble_atomic(P, p, slot, b0, b1, idx_cnt, idx_start, sorted32, slots, pages, lis, page_size, s_pg);
@@ -1241,6 +1289,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   }
   if (threadIdx.x < 4) s_pg[page_size / 4 + threadIdx.x] = 0;
   __syncthreads();
+  DBG_PHASE_K(3, 1);
   // (C) entry runs
   const uint32_t rmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
   const uint32_t* base = sorted32 + P.e_first;
@@ -1321,9 +1370,11 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   }
   }  // word-parallel path
   __syncthreads();
+  DBG_PHASE_K(3, 2);
   // (D) store
   const uint4* srcp = reinterpret_cast<const uint4*>(s_pg);
   for (uint32_t i = threadIdx.x; i < page_size / 16; i += ASM_NT) dst[i] = srcp[i];
+  DBG_PHASE_K(3, 3);
   if (!P.lines_asm) return;
   // (E) probe lines of the page's blocks, cut from the LDS image (format: "probe lines").
   // E1: popcount scan over the blocks' encoding words -> group boundaries in s_gs.
@@ -1380,6 +1431,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
     }
     __syncthreads();
   }
+  DBG_PHASE_K(3, 4);
   // E2: 4 lanes per line, 16 bytes each
   const uint32_t nt = nb * L * 4;
   for (uint32_t u = threadIdx.x; u < nt; u += ASM_NT) {
@@ -1408,6 +1460,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
     const uint64_t line = (uint64_t)P.line_base + (uint64_t)(b0 + j) * L + gl;
     lines[line * 4 + qq] = make_uint4((uint32_t)wv[0], (uint32_t)(wv[0] >> 32), (uint32_t)wv[1], (uint32_t)(wv[1] >> 32));
   }
+  DBG_PHASE_K(3, 8);
 }
 
 // ======================================================================================

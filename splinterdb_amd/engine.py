@@ -33,7 +33,7 @@ EXPORTED = [
     "rf_amd_batch_build_var_keys", "rf_amd_batch_build_hashes", "rf_amd_batch_probe_keys",
     "rf_amd_batch_probe_var_keys", "rf_amd_batch_probe_hashes", "rf_amd_batch_info",
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
-    "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_debug_probe_ablate",
+    "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_batch_timings_back", "rf_amd_debug_probe_ablate",
     "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer",
     "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",
     "rf_amd_image_free",
@@ -106,6 +106,7 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_image_ptrs.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(vp)]
     L.rf_amd_batch_set_timing.argtypes = [vp, i32]
     L.rf_amd_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), u32]
+    L.rf_amd_batch_timings_back.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_float), u32]
     L.rf_amd_debug_probe_ablate.argtypes = [u32]
     L.rf_amd_debug_read_lines.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
     L.rf_amd_debug_rebuild_lines.argtypes = [vp]
@@ -531,8 +532,9 @@ class FilterBatch:
     STAGES = ["partition", "count_scan", "scatter", "cb_sort", "cb_sort_big", "layout",
               "assemble", "build_total", "probe"]
 
-    def set_timing(self, enable=True):
-        _check(load_library().rf_amd_batch_set_timing(self.h, 1 if enable else 0))
+    def set_timing(self, enable=True, sets=1):
+        """Per-stage HIP-event timing; `sets` rounds (build + probe) kept in a ring."""
+        _check(load_library().rf_amd_batch_set_timing(self.h, sets if enable else 0))
 
     def debug_lines(self) -> np.ndarray:
         """The batch's device-only probe lines (diagnostics), as an (N, 64) uint8 array."""
@@ -546,10 +548,11 @@ class FilterBatch:
         """Re-cut the probe lines from the images with the image-upload kernel (diagnostics)."""
         _check(load_library().rf_amd_debug_rebuild_lines(self.h))
 
-    def timings(self):
-        """Per-stage milliseconds of the last build / probe (HIP events on the launch stream)."""
+    def timings(self, back=0):
+        """Per-stage milliseconds of a build / probe round (HIP events on the launch stream);
+        back = 0 is the latest round, up to sets - 1 (set_timing)."""
         arr = (ctypes.c_float * len(self.STAGES))()
-        _check(load_library().rf_amd_batch_timings(self.h, arr, len(self.STAGES)))
+        _check(load_library().rf_amd_batch_timings_back(self.h, back, arr, len(self.STAGES)))
         return dict(zip(self.STAGES, [float(x) for x in arr]))
 
     def info(self, f):

@@ -33,10 +33,17 @@ if KID == 1:
     names = {15: "entry", 0: "init", 1: "load+rank", 2: "bin scan", 3: "scatter", 4: "bin sort",
              5: "dedupe+compact", 6: "write out", 7: "index bounds", 8: "uniq+end"}
     order = [15, 0, 1, 2, 3, 4, 5, 6, 7, 8]
-else:
-    names = {15: "entry", 0: "init", 1: "load+hash+rank", 2: "scan+reserve", 3: "stage", 4: "slots",
-             8: "write runs"}
+elif KID == 4:
+    names = {15: "entry", 0: "sizes+scan", 1: "next()", 2: "doubling", 3: "pages+slots", 8: "quirk+end"}
+    order = [15, 0, 1, 2, 3, 8]
+elif KID == 3:
+    names = {15: "entry", 0: "metadata", 1: "fill", 2: "entry runs", 3: "store", 4: "line scan",
+             8: "line write"}
     order = [15, 0, 1, 2, 3, 4, 8]
+else:
+    names = {15: "entry", 0: "init", 5: "load+hash (thread 0)", 1: "rank", 2: "scan+reserve",
+             3: "stage", 4: "slots", 8: "write runs"}
+    order = [15, 0, 5, 1, 2, 3, 4, 8]
 tot = (ts[:, 8] - ts[:, 15]).astype(np.float64)
 print(f"per workgroup: mean {tot.mean():.0f} cycles, median {np.median(tot):.0f}")
 for a, c in zip(order[:-1], order[1:]):
