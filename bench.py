@@ -151,11 +151,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU; RF_BENCH_BACKEND=gloo (and ranks sharing a device) only to rehearse
+    # the multi-rank launch on a one-GPU box -- the data path has no collective either way
+    backend = os.environ.get("RF_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % max(1, ndev)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll_dev = dev if backend == "nccl" else None  # device of the timing reductions
 
     wf, wn, scaling, wdesc = WORKLOADS[args.workload]
     var = args.workload == "c5"
@@ -224,8 +233,8 @@ def main():
     for back in range(args.steps):  # HIP events of every timed step, recorded on its stream
         for k, v in batch.timings(back).items():
             stages[k].append(v)
-    elapsed = S.max_over_ranks(elapsed, dist, dev)
-    keys_all = S.sum_over_ranks(float(N), dist, dev)
+    elapsed = S.max_over_ranks(elapsed, dist, coll_dev)
+    keys_all = S.sum_over_ranks(float(N), dist, coll_dev)
 
     # ---- verification (outside the timed region) -------------------------------------
     if var:
@@ -272,7 +281,7 @@ def main():
             for f in range(F):
                 batch.read_image_async(f, hpages[f], hslots[f], stream.cuda_stream)
         stream.synchronize()
-        e2e = S.sum_over_ranks(N * reps / (time.perf_counter() - te) / 1e6, dist, dev)
+        e2e = S.sum_over_ranks(N * reps / (time.perf_counter() - te) / 1e6, dist, coll_dev)
         if var:
             ok_e2e = bool(((hfound[torch.from_numpy(w["positive"])] & 1) == 1).all().item())
         else:
@@ -320,7 +329,7 @@ def main():
                    "fingerprint_size": 26, "log_index_size": args.log_index_size, "seed": 42,
                    "parallelism": f"key-range shards, {world} rank(s), no data-path collective"},
         "build_mkeys_s": round(keys_all / (build_ms * 1e-3) / 1e6, 1),
-        "probe_mkeys_s": round(S.sum_over_ranks(float(P), dist, dev) / (probe_ms * 1e-3) / 1e6, 1),
+        "probe_mkeys_s": round(S.sum_over_ranks(float(P), dist, coll_dev) / (probe_ms * 1e-3) / 1e6, 1),
         "e2e_pcie_mkeys_s": round(e2e, 1) if e2e else None,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

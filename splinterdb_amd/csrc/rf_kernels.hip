@@ -1268,6 +1268,31 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
       for (uint32_t r = r0; r < r1; r++) s_rblk[r] = (uint16_t)j;
     }
   }
+  __syncthreads();
+  const uint32_t* base = sorted32 + P.e_first;
+  const uint32_t nruns = (ne + ASM_RUN - 1) / ASM_RUN;
+  // a run's entries: independent loads, all in flight together
+  auto load_run = [&](uint32_t r, uint32_t (&ev)[ASM_RUN]) {
+    const uint32_t q0 = r * ASM_RUN, q1 = min(q0 + ASM_RUN, ne);
+    uint32_t j = s_rblk[r], ej = s_est[j + 1];
+    const uint32_t* src = base + ((int64_t)s_src[j] - (int64_t)s_est[j]);  // src[q] = entry q
+#pragma unroll
+    for (uint32_t i = 0; i < ASM_RUN; i++) {
+      const uint32_t q = q0 + i;
+      ev[i] = 0;
+      if (q < q1) {
+        if (q >= ej) {  // next non-empty block
+          do { j++; } while (s_est[j + 1] <= q);
+          ej = s_est[j + 1];
+          src = base + ((int64_t)s_src[j] - (int64_t)s_est[j]);
+        }
+        ev[i] = src[q];
+      }
+    }
+  };
+  // the first run's loads are issued before the fill, so they land while it runs
+  uint32_t ev0[ASM_RUN];
+  if (threadIdx.x < nruns) load_run(threadIdx.x, ev0);
   // (B) fill: word w, bytes 4w..4w+3
   for (uint32_t w = threadIdx.x; w < page_size / 4; w += ASM_NT) {
     uint32_t lo = 0, hi = nb;  // block holding byte 4w
@@ -1292,29 +1317,15 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   DBG_PHASE_K(3, 1);
   // (C) entry runs
   const uint32_t rmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
-  const uint32_t* base = sorted32 + P.e_first;
-  const uint32_t nruns = (ne + ASM_RUN - 1) / ASM_RUN;
   for (uint32_t r = threadIdx.x; r < nruns; r += ASM_NT) {
     const uint32_t q0 = r * ASM_RUN, q1 = min(q0 + ASM_RUN, ne);
     const uint32_t jr = s_rblk[r];
-    // the run's entries first (independent loads, all in flight), then the bits
     uint32_t ev[ASM_RUN];
-    {
-      uint32_t j = jr, ej = s_est[j + 1];
-      const uint32_t* src = base + ((int64_t)s_src[j] - (int64_t)s_est[j]);  // src[q] = entry q
+    if (r == threadIdx.x) {
 #pragma unroll
-      for (uint32_t i = 0; i < ASM_RUN; i++) {
-        const uint32_t q = q0 + i;
-        ev[i] = 0;
-        if (q < q1) {
-          if (q >= ej) {  // next non-empty block
-            do { j++; } while (s_est[j + 1] <= q);
-            ej = s_est[j + 1];
-            src = base + ((int64_t)s_src[j] - (int64_t)s_est[j]);
-          }
-          ev[i] = src[q];
-        }
-      }
+      for (uint32_t i = 0; i < ASM_RUN; i++) ev[i] = ev0[i];
+    } else {
+      load_run(r, ev);
     }
     uint32_t j = jr, ej = s_est[j + 1], kq = s_est[j];
     uint64_t ebit = (uint64_t)(s_off[j] + 2) * 8;

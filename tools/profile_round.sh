@@ -12,11 +12,16 @@ export TMPDIR=/tmp
 O=gpurun_out/prof_$TAG
 mkdir -p $O
 BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e"
+SQ="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pf -o c2 -- python3 $BENCH > $O/pf.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pw -o c2 -- python3 $BENCH > $O/pw.log 2>&1 || { echo "pmc write failed"; exit 1; }
 python3 profiles/pmc_summary.py $O/pf/c2_counter_collection.csv $O/pw/c2_counter_collection.csv $O/pmc_$TAG.json || exit 1
+timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d $O/sq -o c2 -- python3 $BENCH > $O/sq.log 2>&1 || { echo "pmc sq failed"; exit 1; }
+python3 tools/sq_summary.py $O/sq/c2_counter_collection.csv > $O/sq_$TAG.txt || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o c2 -- python3 $BENCH > $O/kt.log 2>&1 || { echo "kernel trace failed"; exit 1; }
 timeout -k 10 400 python3 bench.py --pmc $O/pmc_$TAG.json > $O/bench_c2.json 2> $O/bench_c2.err || { echo "bench c2 failed"; exit 1; }
 timeout -k 10 300 python3 bench.py --workload c3 --no-cpu-baseline --pmc none > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench c3 failed"; exit 1; }
 timeout -k 10 300 python3 bench.py --workload c4 --no-cpu-baseline --pmc none > $O/bench_c4.json 2> $O/bench_c4.err || { echo "bench c4 failed"; exit 1; }
+timeout -k 10 300 python3 bench.py --workload c5 --pmc none > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 failed"; exit 1; }
+timeout -k 10 100 ./tools/gather_bench > $O/gather_$TAG.txt 2>&1 || { echo "gather bench failed"; exit 1; }
 cat $O/bench_c2.json
