@@ -1174,10 +1174,10 @@ __device__ __forceinline__ void assemble_atomic(const FilterPlan& P, uint32_t p,
   }
 }
 
-constexpr uint32_t ASM_MAXB = 512;  // blocks per page held in LDS (more: assemble_atomic)
+constexpr uint32_t ASM_MAXB = 128;  // blocks per page held in LDS (more: assemble_atomic)
 constexpr uint32_t ASM_RUN = 16;    // entries per thread-run in phase C
 constexpr uint32_t ASM_MAXE = 16384;  // entries per page covered by the run table
-constexpr uint32_t ASM_GT = 4096;     // group-start table entries per page (lines_asm bound)
+constexpr uint32_t ASM_GT = 1024;     // group-start table entries per page (lines_asm bound)
 
 // 64 bits of the LDS page image from bit `bitpos` (the image has 4 words of tail padding)
 __device__ __forceinline__ uint64_t lds_bits64(const uint32_t* s_pg, uint32_t bitpos) {
@@ -1328,8 +1328,8 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
       load_run(r, ev);
     }
     uint32_t j = jr, ej = s_est[j + 1], kq = s_est[j];
-    uint64_t ebit = (uint64_t)(s_off[j] + 2) * 8;
-    uint64_t rbit = (uint64_t)(s_off[j] + 2 + (s_c[j] + IS - 1) / 8 + 4) * 8;
+    uint32_t ebit = (s_off[j] + 2) * 8;  // page bit offsets < 2^15: 32-bit math
+    uint32_t rbit = (s_off[j] + 2 + (s_c[j] + IS - 1) / 8 + 4) * 8;
     uint32_t eW = 0xffffffffu, rW = 0xffffffffu;  // current 64-bit windows (page bit / 64)
     uint64_t eacc = 0, racc = 0;
     auto flush_e = [&]() {
@@ -1354,17 +1354,17 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
         do { j++; } while (s_est[j + 1] <= q);
         ej = s_est[j + 1];
         kq = s_est[j];
-        ebit = (uint64_t)(s_off[j] + 2) * 8;
-        rbit = (uint64_t)(s_off[j] + 2 + (s_c[j] + IS - 1) / 8 + 4) * 8;
+        ebit = (s_off[j] + 2) * 8;
+        rbit = (s_off[j] + 2 + (s_c[j] + IS - 1) / 8 + 4) * 8;
       }
       const uint32_t e = ev[i];
       const uint32_t k = q - kq;
-      const uint64_t hb = ebit + k + (rvs >= 32 ? 0u : ((e >> rvs) & (IS - 1)));
+      const uint32_t hb = ebit + k + (rvs >= 32 ? 0u : ((e >> rvs) & (IS - 1)));
       const uint32_t hw = (uint32_t)(hb >> 6);
       if (hw != eW) { flush_e(); eW = hw; }
       eacc |= 1ull << (hb & 63);
       if (rvs) {
-        const uint64_t rb = rbit + (uint64_t)k * rvs;
+        const uint32_t rb = rbit + k * rvs;
         const uint32_t rw = (uint32_t)(rb >> 6), sh = (uint32_t)(rb & 63);
         if (rw != rW) { flush_r(); rW = rw; }
         const uint64_t v = e & rmask;

@@ -24,8 +24,8 @@ constexpr int BIG_NT = 1024;
 constexpr int BIG_GRID = 64;
 constexpr int LAYOUT_NT = 1024;
 constexpr int ASM_NT = 256;
-constexpr uint32_t ASM_MAXB_HOST = 512;  // = ASM_MAXB in rf_kernels.hip (blocks per page in LDS)
-constexpr uint32_t ASM_GT_HOST = 4096;   // = ASM_GT (group-start table entries per page)
+constexpr uint32_t ASM_MAXB_HOST = 128;  // = ASM_MAXB in rf_kernels.hip (blocks per page in LDS)
+constexpr uint32_t ASM_GT_HOST = 1024;   // = ASM_GT (group-start table entries per page)
 
 enum InputKind { IN_KEYS24 = 0, IN_KEYS_W = 1, IN_KEYS_B = 2, IN_VAR = 3, IN_HASH = 4 };
 
