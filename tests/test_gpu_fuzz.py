@@ -1,0 +1,104 @@
+"""Randomised GPU parity sweep: seeded random geometries (fingerprint_size, log_index_size),
+sizes, values, incremental adds over an old filter, duplicate-heavy inputs and several
+filters per batch, every image and probe compared bit-for-bit with the oracle. Inputs the
+reference cannot take (the oracle rejects them: e.g. an index over 4096 entries or a
+block over one page) must be rejected by the engine as well."""
+import numpy as np
+import pytest
+
+from splinterdb_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+N_CASES = 150
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+
+
+def _case(rng):
+    fp = int(rng.integers(18, 33))
+    lis = int(rng.integers(3, 11)) if rng.random() < 0.85 else int(rng.integers(11, 13))
+    cap = min(2 * 4096 * (1 << lis) - 1, (1 << fp) - 1)
+    nf = int(rng.integers(1, 4))
+    sizes = [max(1, int(np.exp(rng.uniform(0, np.log(cap / 2))))) for _ in range(nf)]
+    vmax = min(63, (1 << (32 - fp)) - 1)
+    vals = [int(rng.integers(0, vmax + 1)) for _ in range(nf)]
+    dup = bool(rng.random() < 0.25)
+    incr = bool(rng.random() < 0.4)
+    return fp, lis, sizes, vals, dup, incr
+
+
+def _hashes(rng, n, dup):
+    h = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    if dup and n > 8:
+        h = h[rng.integers(0, max(1, n // 8), size=n)]
+    return h
+
+
+def _oracle_add(oracle, ocfg, h, v, old=None):
+    try:
+        return oracle.filter_add(ocfg, h, value=v, old=old)
+    except ValueError:
+        return None
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_geometry_parity(oracle, seed):
+    rng = np.random.default_rng(1000 + seed)
+    fp, lis, sizes, vals, dup, incr = _case(rng)
+    cfg = E.routing_config_init(fingerprint_size=fp, log_index_size=lis)
+    ocfg = oracle.make_config(fingerprint_size=fp, log_index_size=lis)
+    hs = [_hashes(rng, n, dup) for n in sizes]
+    ofs = [_oracle_add(oracle, ocfg, h, v) for h, v in zip(hs, vals)]
+    try:
+        b = E.FilterBatch(cfg, sizes, vals)
+    except E.PlatformStatusError:
+        assert any(o is None for o in ofs), "engine rejected a batch the oracle accepts"
+        return
+    b.build_hashes(dev(np.concatenate(hs)))
+    for f, of in enumerate(ofs):
+        if of is None:
+            with pytest.raises(E.PlatformStatusError):
+                b.image(f)
+            continue
+        img = b.image(f)
+        assert (img.num_unique, img.num_pages) == (of.num_unique, of.num_pages), (seed, f)
+        assert (img.pages == of.pages()).all(), (seed, f)
+        assert (img.slots == of.slots()[: of.num_indices]).all(), (seed, f)
+    # probes: each filter's own hashes plus random ones, routed at random
+    good = [f for f, of in enumerate(ofs) if of is not None]
+    if not good:
+        return
+    P = 20000
+    ph = np.concatenate([np.concatenate(hs)[rng.integers(0, sum(sizes), size=P // 2)],
+                         rng.integers(0, 1 << 32, size=P - P // 2, dtype=np.uint64).astype(np.uint32)])
+    fid = np.array(good, dtype=np.uint32)[rng.integers(0, len(good), size=P)]
+    found = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b.probe_hashes(dev(ph), dev(fid), P, found)
+    torch.cuda.synchronize()
+    got = found.cpu().numpy().view(np.uint64)
+    for f in good:
+        m = fid == f
+        assert (got[m] == ofs[f].lookup_hashes(ph[m])).all(), (seed, f)
+    # incremental add over filter `good[0]` with a value at least as wide
+    if incr:
+        f0 = good[0]
+        n2 = max(1, sizes[f0] // 2)
+        v2 = int(rng.integers(vals[f0], min(63, (1 << (32 - fp)) - 1) + 1))
+        h2 = _hashes(rng, n2, dup)
+        of2 = _oracle_add(oracle, ocfg, h2, v2, old=ofs[f0])
+        try:
+            b2 = E.FilterBatch(cfg, [n2], [v2], old=[(b, f0)])
+            b2.build_hashes(dev(h2))
+            img2 = b2.image(0)
+        except E.PlatformStatusError:
+            assert of2 is None, (seed, "engine rejected an incremental add the oracle accepts")
+            return
+        assert of2 is not None, (seed, "oracle rejected an incremental add the engine accepts")
+        assert (img2.num_unique, img2.num_pages) == (of2.num_unique, of2.num_pages), seed
+        assert (img2.pages == of2.pages()).all(), seed
+        assert (img2.slots == of2.slots()[: of2.num_indices]).all(), seed
