@@ -466,6 +466,19 @@ __device__ __forceinline__ void sort8(T (&x)[8]) {
   CE(0, 4) CE(1, 5) CE(2, 6) CE(3, 7) CE(2, 4) CE(3, 5) CE(1, 2) CE(3, 4) CE(5, 6)
 #undef CE
 }
+template <typename T>
+__device__ __forceinline__ void sort16(T (&x)[16]) {  // Batcher odd-even merge, 63 CEs
+#define CE(a, b) { const T lo = x[a] < x[b] ? x[a] : x[b], hi = x[a] < x[b] ? x[b] : x[a]; x[a] = lo; x[b] = hi; }
+  CE(0, 1) CE(2, 3) CE(0, 2) CE(1, 3) CE(1, 2) CE(4, 5) CE(6, 7) CE(4, 6) CE(5, 7) CE(5, 6) CE(0, 4)
+  CE(2, 6) CE(2, 4) CE(1, 5) CE(3, 7) CE(3, 5) CE(1, 2) CE(3, 4) CE(5, 6) CE(8, 9) CE(10, 11) CE(8, 10)
+  CE(9, 11) CE(9, 10) CE(12, 13) CE(14, 15) CE(12, 14) CE(13, 15) CE(13, 14) CE(8, 12) CE(10, 14)
+  CE(10, 12) CE(9, 13) CE(11, 15) CE(11, 13) CE(9, 10) CE(11, 12) CE(13, 14) CE(0, 8) CE(4, 12)
+  CE(4, 8) CE(2, 10) CE(6, 14) CE(6, 10) CE(2, 4) CE(6, 8) CE(10, 12) CE(1, 9) CE(5, 13) CE(5, 9)
+  CE(3, 11) CE(7, 15) CE(7, 11) CE(3, 5) CE(7, 9) CE(11, 13) CE(1, 2) CE(3, 4) CE(5, 6) CE(7, 8)
+  CE(9, 10) CE(11, 12) CE(13, 14)
+#undef CE
+}
+
 // Finish a sorted coarse bucket held in `B` (LDS or global): write per-index counts and
 // starts, the compacted entries, and the num_unique contribution. Shared by K4 and K4b.
 struct CbCtx {
@@ -607,37 +620,47 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   }
   __syncthreads();
   DBG_PHASE(3);
-  // order inside each bin: one thread per bin; bins of up to 8 entries (all but ~1 in 3000
-  // for random keys) are loaded into registers together, put through an 8-input sorting
-  // network and written back (two bins per step, so their LDS reads share one wait). Larger
-  // bins are listed and ranked afterwards by a whole wave each: lane j's entry goes to the
-  // bin start + the number of entries that sort before it (smaller, or equal and earlier).
+  // order inside each bin. The entries of S consecutive bins are one contiguous segment of
+  // s_b, and sorting a segment by value orders its bins (a bin is the value's high part)
+  // and every bin's entries at once. S makes a segment hold ~8 entries on average; one
+  // thread sorts it in registers with a 16-input network. A segment over 16 entries falls
+  // back to an 8-input network per bin; bins over 8 entries are listed and ranked
+  // afterwards by a whole wave each (lane j's entry goes to the bin start + the number of
+  // entries that sort before it: smaller, or equal and earlier).
   {
     constexpr EntT EMAX = ~EntT(0);
-    static_assert(MAX_BINS % (2 * SORT_NT) == 0, "two bins per thread and step");
-    for (uint32_t b0 = threadIdx.x; b0 < nbins; b0 += 2 * SORT_NT) {
-      uint32_t st[2], cnt[2];
-      EntT x[2][8];
+    uint32_t S = 8;  // largest power of two <= 8 with S * n / nbins <= 8
+    while (S > 1 && (uint64_t)S * n > 8ull * nbins) S >>= 1;
+    if (S > nbins) S = nbins;
+    const uint32_t nseg = nbins / S;
+    for (uint32_t sg = threadIdx.x; sg < nseg; sg += SORT_NT) {
+      const uint32_t b0 = sg * S, st = s_bin[b0], c = s_bin[b0 + S] - st;
+      if (c <= 16) {
+        EntT x[16];
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const uint32_t b = b0 + h * SORT_NT;
-        st[h] = b < nbins ? s_bin[b] : 0u;
-        cnt[h] = b < nbins ? s_bin[b + 1] - st[h] : 0u;
-      }
+        for (int j = 0; j < 16; j++) x[j] = (uint32_t)j < c ? s_b[st + j] : EMAX;
+        sort16(x);
+        if (c >= 2) {
 #pragma unroll
-      for (int h = 0; h < 2; h++)
+          for (int j = 0; j < 16; j++)
+            if ((uint32_t)j < c) s_b[st + j] = x[j];
+        }
+      } else {
+        for (uint32_t b = b0; b < b0 + S; b++) {
+          const uint32_t bs = s_bin[b], bc = s_bin[b + 1] - bs;
+          if (bc <= 1) continue;
+          if (bc <= 8) {
+            EntT y[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) x[h][j] = ((uint32_t)j < cnt[h] && cnt[h] <= 8) ? s_b[st[h] + j] : EMAX;
+            for (int j = 0; j < 8; j++) y[j] = (uint32_t)j < bc ? s_b[bs + j] : EMAX;
+            sort8(y);
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
-        sort8(x[h]);
-        if (cnt[h] >= 2 && cnt[h] <= 8) {
-#pragma unroll
-          for (int j = 0; j < 8; j++)
-            if ((uint32_t)j < cnt[h]) s_b[st[h] + j] = x[h][j];
-        } else if (cnt[h] > 8) {
-          const uint32_t q = atomicAdd(&s_nbig, 1u);
-          if (q < BIG_LIST) s_big[q] = b0 + h * SORT_NT;
+            for (int j = 0; j < 8; j++)
+              if ((uint32_t)j < bc) s_b[bs + j] = y[j];
+          } else {
+            const uint32_t q = atomicAdd(&s_nbig, 1u);
+            if (q < BIG_LIST) s_big[q] = b;
+          }
         }
       }
     }
