@@ -1923,15 +1923,17 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
   // the bucket's remainders: bits [s*rvs, (s+c)*rvs) of the 384-bit remainder area
   const uint32_t b = s * rvs, wi = b >> 5, off = b & 31;
   if (off + c * rvs > 96 || b + c * rvs > 384) return false;
-  const uint32_t R[12] = {Q[1].x, Q[1].y, Q[1].z, Q[1].w, Q[2].x, Q[2].y,
-                          Q[2].z, Q[2].w, Q[3].x, Q[3].y, Q[3].z, Q[3].w};
-  uint32_t w0 = 0, w1 = 0, w2 = 0;
+  // 96-bit window at dword wi (wi <= 9): pick the 4-dword group g = wi / 4, then dwords
+  // o..o+2 (o = wi % 4) of that group's 6-dword span -- 21 selects instead of 36
+  const uint32_t R[14] = {Q[1].x, Q[1].y, Q[1].z, Q[1].w, Q[2].x, Q[2].y, Q[2].z,
+                          Q[2].w, Q[3].x, Q[3].y, Q[3].z, Q[3].w, 0u, 0u};
+  const uint32_t g = wi >> 2, o = wi & 3;
+  uint32_t W[6];
 #pragma unroll
-  for (uint32_t k = 0; k < 12; k++) {  // 96-bit window at dword wi (branch-free picks)
-    w0 = wi == k ? R[k] : w0;
-    w1 = wi + 1 == k ? R[k] : w1;
-    w2 = wi + 2 == k ? R[k] : w2;
-  }
+  for (int k = 0; k < 6; k++) W[k] = g == 0 ? R[k] : (g == 1 ? R[4 + k] : R[8 + k]);
+  const uint32_t w0 = o == 0 ? W[0] : (o == 1 ? W[1] : (o == 2 ? W[2] : W[3]));
+  const uint32_t w1 = o == 0 ? W[1] : (o == 1 ? W[2] : (o == 2 ? W[3] : W[4]));
+  const uint32_t w2 = o == 0 ? W[2] : (o == 1 ? W[3] : (o == 2 ? W[4] : W[5]));
   const uint64_t wl = (uint64_t)w1 << 32 | w0;
   const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
   const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);

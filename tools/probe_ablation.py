@@ -1,5 +1,6 @@
 """Diagnostic: time k_probe truncated after each step (hash / + probe-line load / full),
-interleaved rounds in one process (cdna_hip_programming.md rule 24). C2 shape."""
+interleaved rounds in one process (cdna_hip_programming.md rule 24).
+usage: python tools/probe_ablation.py [filters=8] [keys_per_filter=8000000]  (C3: 256 1048576)"""
 import json
 import os
 import sys
@@ -11,7 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from splinterdb_amd import engine as E  # noqa: E402
 from splinterdb_amd import keys as K  # noqa: E402
 
-F, n = 8, 8_000_000
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 8_000_000
 N = F * n
 cfg = E.routing_config_init()
 dev = torch.device("cuda", 0)
