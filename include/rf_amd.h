@@ -137,6 +137,13 @@ int rf_amd_debug_read_lines(rf_amd_batch *b, uint8_t *h_lines, uint64_t bytes, u
 int rf_amd_debug_rebuild_lines(rf_amd_batch *b);
 int rf_amd_batch_timings(rf_amd_batch *b, float *ms, uint32_t n);
 
+/* XXH32(key, cfg->seed) of n device-resident keys into d_hashes (data_key_hash as
+ * btree_pack computes a compaction's fingerprints, src/btree.c:4020-4024); asynchronous */
+int rf_amd_hash_keys(rf_amd_engine *e, const rf_amd_config *cfg, const void *d_keys, uint32_t key_len,
+                     uint64_t n, uint32_t *d_hashes, void *stream);
+int rf_amd_hash_var_keys(rf_amd_engine *e, const rf_amd_config *cfg, const uint8_t *d_bytes,
+                         const uint64_t *d_offsets, uint64_t n, uint32_t *d_hashes, void *stream);
+
 /* ---- drop-in single-filter calls on HOST buffers ------------------------------------
  * rf_amd_filter_add replaces routing_filter_add (src/routing_filter.h:78-85): hashes
  * (32-bit XXH32 of the keys, as btree_pack produces them, src/btree.c:4020-4024) in,

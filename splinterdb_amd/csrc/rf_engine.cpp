@@ -1039,6 +1039,33 @@ extern "C" void rf_amd_lookup_async_free(rf_amd_lookup_async_state* s) {
   delete s;
 }
 
+// ---- batch hashing (data_key_hash, btree_pack's fingerprint loop) -------------------------
+extern "C" int rf_launch_hash(void* stream, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
+                              uint32_t seed, uint64_t n, uint32_t* out);
+
+extern "C" int rf_amd_hash_keys(rf_amd_engine* e, const rf_amd_config* cfg, const void* d_keys, uint32_t key_len,
+                                uint64_t n, uint32_t* d_hashes, void* stream) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (int rc = check_cfg(cfg)) return rc;
+  if (n && (!d_keys || !d_hashes || key_len == 0)) return fail(RF_AMD_EINVAL, "null keys / output");
+  HIPCHK(hipSetDevice(e->device));
+  if (rf_launch_hash(stream ? stream : e->stream, fixed_kind(d_keys, key_len), d_keys, nullptr, key_len, cfg->seed,
+                     n, d_hashes))
+    return fail(RF_AMD_EINVAL, "hash kernel launch failed");
+  return 0;
+}
+
+extern "C" int rf_amd_hash_var_keys(rf_amd_engine* e, const rf_amd_config* cfg, const uint8_t* d_bytes,
+                                    const uint64_t* d_offsets, uint64_t n, uint32_t* d_hashes, void* stream) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (int rc = check_cfg(cfg)) return rc;
+  if (n && (!d_bytes || !d_offsets || !d_hashes)) return fail(RF_AMD_EINVAL, "null keys / output");
+  HIPCHK(hipSetDevice(e->device));
+  if (rf_launch_hash(stream ? stream : e->stream, IN_VAR, d_bytes, d_offsets, 0, cfg->seed, n, d_hashes))
+    return fail(RF_AMD_EINVAL, "hash kernel launch failed");
+  return 0;
+}
+
 // ---- routing_filter_verify (src/routing_filter.c:1163-1183) ------------------------------
 extern "C" int rf_launch_count_missing(void* stream, const uint64_t* found, uint64_t n, uint32_t value,
                                        unsigned long long* missing);

@@ -1687,6 +1687,30 @@ extern "C" int rf_launch_estimate(void* stream, const EstFilter* fl, uint32_t nu
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// data_key_hash over a batch (btree_pack's fingerprint loop, src/btree.c:4020-4024)
+template <int KIND>
+__global__ __launch_bounds__(256) void k_hash(const void* __restrict__ in0, const uint64_t* __restrict__ offs,
+                                              uint32_t key_len, uint32_t seed, uint64_t n,
+                                              uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
+}
+
+extern "C" int rf_launch_hash(void* stream, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
+                              uint32_t seed, uint64_t n, uint32_t* out) {
+  if (n == 0) return 0;
+  const dim3 g((uint32_t)((n + 255) / 256)), b(256);
+#define L(K) hipLaunchKernelGGL((k_hash<K>), g, b, 0, (hipStream_t)stream, in0, offs, key_len, seed, n, out)
+  switch (kind) {
+    case IN_KEYS24: L(IN_KEYS24); break;
+    case IN_KEYS_W: L(IN_KEYS_W); break;
+    case IN_KEYS_B: L(IN_KEYS_B); break;
+    default: L(IN_VAR); break;
+  }
+#undef L
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // routing_filter_verify (src/routing_filter.c:1163-1183): keys whose found_values lacks `value`
 __global__ __launch_bounds__(256) void k_count_missing(const uint64_t* __restrict__ found, uint64_t n,
                                                        uint32_t value, unsigned long long* __restrict__ missing) {

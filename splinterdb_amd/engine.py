@@ -42,6 +42,7 @@ EXPORTED = [
     "rf_amd_estimate_unique_fp", "rf_amd_batch_estimate_unique_fp", "rf_amd_estimate_unique_keys",
     "rf_amd_lookup_async", "rf_amd_lookup_async_poll", "rf_amd_lookup_async_wait",
     "rf_amd_lookup_async_free", "rf_amd_filter_verify", "rf_amd_filter_print",
+    "rf_amd_hash_keys", "rf_amd_hash_var_keys",
 ]
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
 ASYNC_STATUS_DONE = 1
@@ -142,6 +143,8 @@ def load_library(build_if_missing=True):
     L.rf_amd_filter_verify.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), vp, u32,
                                        u64, ctypes.c_uint16, ctypes.POINTER(u64)]
     L.rf_amd_filter_print.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), vp]
+    L.rf_amd_hash_keys.argtypes = [vp, ctypes.POINTER(RfConfig), vp, u32, u64, vp, vp]
+    L.rf_amd_hash_var_keys.argtypes = [vp, ctypes.POINTER(RfConfig), vp, vp, u64, vp, vp]
     _lib = L
     return L
 
@@ -392,6 +395,19 @@ def routing_filter_print(cfg: RoutingConfig, filt, path=None) -> str:
         text = t.read()
     os.unlink(tmp)
     return text
+
+
+def hash_keys(cfg: RoutingConfig, d_keys, key_len, n, d_hashes, stream=None, engine=None):
+    """XXH32 of n device-resident fixed-length keys (data_key_hash) into d_hashes, on the GPU."""
+    eng = engine or default_engine()
+    _check(load_library().rf_amd_hash_keys(eng.h, ctypes.byref(cfg.c()), _dptr(d_keys), key_len, n,
+                                           _dptr(d_hashes), _stream(stream)))
+
+
+def hash_var_keys(cfg: RoutingConfig, d_bytes, d_offsets, n, d_hashes, stream=None, engine=None):
+    eng = engine or default_engine()
+    _check(load_library().rf_amd_hash_var_keys(eng.h, ctypes.byref(cfg.c()), _dptr(d_bytes), _dptr(d_offsets), n,
+                                               _dptr(d_hashes), _stream(stream)))
 
 
 class LookupAsync:

@@ -150,3 +150,18 @@ def test_verify(oracle):
     with pytest.raises(E.PlatformStatusError) as ei:
         E.routing_filter_verify(cfg, f, keys, 4)
     assert ei.value.code == E.STATUS_BAD_PARAM and ei.value.num_missing == 300_000
+
+
+def test_hash_keys_match_oracle(oracle):
+    """rf_amd_hash_keys / _var_keys: XXH32 (seed from the config) of device-resident keys."""
+    for key_len in (24, 16, 7, 100):
+        keys = K.random_keys(50_000, key_len=key_len, seed=key_len)
+        out = torch.zeros(50_000, dtype=torch.int32, device="cuda:0")
+        E.hash_keys(E.routing_config_init(seed=7), dev(keys), key_len, 50_000, out)
+        torch.cuda.synchronize()
+        assert (out.cpu().numpy().view(np.uint32) == oracle.hash_fixed(keys.reshape(-1), key_len, seed=7)).all()
+    d, o = K.var_keys(30_000)
+    out = torch.zeros(30_000, dtype=torch.int32, device="cuda:0")
+    E.hash_var_keys(E.routing_config_init(), dev(d), dev(o), 30_000, out)
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy().view(np.uint32) == oracle.hash_var(d, o)).all()
