@@ -24,6 +24,9 @@ extern "C" int rf_launch_build(const LaunchArgs* a);
 extern "C" int rf_launch_old_decode(const LaunchArgs* a, uint32_t f, uint32_t old_num_indices,
                                     uint32_t* d_cnt, uint32_t* d_pos);
 extern "C" int rf_launch_plines(const LaunchArgs* a);
+extern "C" int rf_launch_build_init(void* stream, uint32_t* cb_count, uint32_t* cb_cursor, uint32_t num_cb,
+                                    uint32_t* outs_words, uint32_t num_out_words, uint32_t* overflow,
+                                    uint32_t* spill);
 extern "C" int rf_launch_probe(const LaunchArgs* a, int kind, const void* in0, const uint64_t* offs,
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found);
 
@@ -416,13 +419,10 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   a.offs = offs;
   a.key_len = key_len;
   if (a.events) HIPCHK(hipEventRecord(((hipEvent_t*)a.events)[EV_B_START], st));
-  HIPCHK(hipMemsetAsync(b->d_cb_count.p, 0, 4 * (size_t)b->CB, st));
-  HIPCHK(hipMemsetAsync(b->d_outs.p, 0, sizeof(FilterOut) * b->F, st));
-  HIPCHK(hipMemsetAsync(b->d_overflow.p, 0, 4, st));
-  if (!b->wide) {
-    HIPCHK(hipMemsetAsync(b->d_cb_cursor.p, 0, 4 * (size_t)b->CB, st));
-    HIPCHK(hipMemsetAsync(b->d_spill.p, 0, 4, st));
-  }
+  if (rf_launch_build_init(st, b->d_cb_count.as<uint32_t>(), b->wide ? nullptr : b->d_cb_cursor.as<uint32_t>(),
+                           b->CB, b->d_outs.as<uint32_t>(), (uint32_t)(sizeof(FilterOut) / 4 * b->F),
+                           b->d_overflow.as<uint32_t>(), b->wide ? nullptr : b->d_spill.as<uint32_t>()))
+    return fail(RF_AMD_EINVAL, "init kernel launch failed");
   if (b->wide) {
     HIPCHK(hipMemsetAsync(b->d_ent.p, 0xff, b->d_ent.n, st));
     for (uint32_t f = 0; f < b->F; f++) {

@@ -1687,6 +1687,32 @@ extern "C" int rf_launch_estimate(void* stream, const EstFilter* fl, uint32_t nu
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// per-build counters zeroed in one launch (instead of one memset each)
+__global__ __launch_bounds__(256) void k_build_init(uint32_t* __restrict__ cb_count, uint32_t* __restrict__ cb_cursor,
+                                                    uint32_t num_cb, uint32_t* __restrict__ outs_words,
+                                                    uint32_t num_out_words, uint32_t* __restrict__ overflow,
+                                                    uint32_t* __restrict__ spill) {
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < num_cb; i += stride) {
+    cb_count[i] = 0;
+    if (cb_cursor) cb_cursor[i] = 0;
+  }
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < num_out_words; i += stride) outs_words[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    overflow[0] = 0;
+    if (spill) spill[0] = 0;
+  }
+}
+
+extern "C" int rf_launch_build_init(void* stream, uint32_t* cb_count, uint32_t* cb_cursor, uint32_t num_cb,
+                                    uint32_t* outs_words, uint32_t num_out_words, uint32_t* overflow,
+                                    uint32_t* spill) {
+  const uint32_t want = (num_cb > num_out_words ? num_cb : num_out_words) / 256 + 1;
+  hipLaunchKernelGGL(k_build_init, dim3(want < 1024 ? want : 1024), dim3(256), 0, (hipStream_t)stream, cb_count,
+                     cb_cursor, num_cb, outs_words, num_out_words, overflow, spill);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // data_key_hash over a batch (btree_pack's fingerprint loop, src/btree.c:4020-4024)
 template <int KIND>
 __global__ __launch_bounds__(256) void k_hash(const void* __restrict__ in0, const uint64_t* __restrict__ offs,
