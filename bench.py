@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 from splinterdb_amd import engine as E  # noqa: E402
 from splinterdb_amd import keys as K  # noqa: E402
+from splinterdb_amd import route as R  # noqa: E402
 from splinterdb_amd import shard as S  # noqa: E402
 
 WORKLOADS = {
@@ -63,6 +64,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--cpu-filters", type=int, default=0, help="sample filters (default = threads)")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--routed-probe", action="store_true",
+                   help="also time routed probes: each rank probes keys of every rank's filters, "
+                        "moved to the owner by all-to-all (route.py); reported beside value")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     return p.parse_args()
 
@@ -310,6 +314,43 @@ def main():
             e2e_h = S.sum_over_ranks(N * reps / (time.perf_counter() - te) / 1e6, dist, coll_dev)
             verified = verified and bool(((hfound & 1) == 1).all().item())
 
+    # ---- routed probes (serving across ranks, reported beside `value`, never as it) ------
+    # probe i of rank r looks up global key id (i * world + r) mod total: every rank's probes
+    # cover every rank's filters, so (world-1)/world of them cross to another GPU and back
+    routed = None
+    if args.routed_probe and not var:
+        total_keys = F_total * n
+        gid = (torch.arange(N, device=dev, dtype=torch.int64) * world + rank) % total_keys
+        rkeys = K.ids_keys_torch(gid, 24)
+        rfid = (gid // n).to(torch.int32)
+        del gid
+        d_rh = torch.empty(N, dtype=torch.int32, device=dev)
+        rfound = torch.zeros(N, dtype=torch.int64, device=dev)
+        router = R.ProbeRouter(S.plan_shards(F_total, n, world), rank, batch, dev, dist=dist,
+                               coll_device=coll_dev if coll_dev is not None else "cpu",
+                               ops=R.GpuRouteOps(eng))
+        reps = max(1, min(args.steps, 5))
+
+        def rstep():
+            with torch.cuda.stream(stream):
+                E.hash_keys(cfg, rkeys, 24, N, d_rh, stream=stream.cuda_stream, engine=eng)
+                router.lookup_hashes(d_rh, rfid, N, rfound)
+
+        rstep()
+        stream.synchronize()
+        barrier()
+        tr = time.perf_counter()
+        for _ in range(reps):
+            rstep()
+        stream.synchronize()
+        barrier()
+        tr = S.max_over_ranks(time.perf_counter() - tr, dist, coll_dev)
+        routed = {"mkeys_s": round(keys_all * reps / tr / 1e6, 1), "ms": round(tr / reps * 1e3, 3),
+                  "reps": reps, "verified": bool(((rfound & 1) == 1).all().item()),
+                  "exchange": "none (1 rank)" if world == 1 else
+                  ("all-to-all over RCCL" if coll_dev is not None else "all-to-all over gloo (rehearsal)")}
+        del rkeys, rfid, d_rh, rfound, router
+
     ms = {k: float(np.mean(v)) for k, v in stages.items()}
     kern = {}
     for k in ("partition", "count_scan", "scatter", "cb_sort", "cb_sort_big", "layout", "assemble", "probe"):
@@ -360,6 +401,8 @@ def main():
         "kernels": kern,
         "verified": verified,
     }
+    if routed is not None:
+        out["routed_probe"] = routed
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline_var(args, args.log_index_size, w, F, n) if var else \
             cpu_baseline(args, args.log_index_size, n)

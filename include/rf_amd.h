@@ -144,6 +144,27 @@ int rf_amd_hash_keys(rf_amd_engine *e, const rf_amd_config *cfg, const void *d_k
 int rf_amd_hash_var_keys(rf_amd_engine *e, const rf_amd_config *cfg, const uint8_t *d_bytes,
                          const uint64_t *d_offsets, uint64_t n, uint32_t *d_hashes, void *stream);
 
+/* ---- routed probes across ranks (multi-GPU serving) --------------------
+ * Each rank owns the filters of a contiguous key range (one filter per trunk pivot,
+ * src/trunk.c:4133-4170); a probe may arrive on any rank. rf_amd_route_probes partitions
+ * n probes (hash, global filter id) stably by owning rank, d_route[g] = local_id << 8 |
+ * rank, into d_pairs = (local_id << 32 | hash) grouped by rank (h_counts[r] pairs for
+ * rank r) plus d_perm (pair j came from probe d_perm[j]); it synchronises on the stream
+ * to return h_counts. One all-to-all of d_pairs (RCCL, by the caller) hands every rank
+ * its probes; rf_amd_batch_probe_pairs probes them against the owner's batch; the
+ * reverse all-to-all returns found_values in pair order, and rf_amd_unroute_found
+ * scatters them back (d_found[d_perm[j]] = d_back[j]). d_scratch holds
+ * rf_amd_route_scratch_bytes(n, world) bytes. Bad filter ids / ranks: EINVAL. */
+#define RF_AMD_ROUTE_MAX_WORLD 16
+uint64_t rf_amd_route_scratch_bytes(uint64_t n, uint32_t world);
+int rf_amd_route_probes(rf_amd_engine *e, const uint32_t *d_hashes, const uint32_t *d_filter_id, uint64_t n,
+                        const uint32_t *d_route, uint32_t num_filters, uint32_t world, uint64_t *d_pairs,
+                        uint32_t *d_perm, void *d_scratch, uint64_t *h_counts, void *stream);
+int rf_amd_batch_probe_pairs(rf_amd_batch *b, const uint64_t *d_pairs, uint64_t n, uint64_t *d_found,
+                             void *stream);
+int rf_amd_unroute_found(rf_amd_engine *e, const uint64_t *d_back, const uint32_t *d_perm, uint64_t n,
+                         uint64_t *d_found, void *stream);
+
 /* ---- drop-in single-filter calls on HOST buffers ------------------------------------
  * rf_amd_filter_add replaces routing_filter_add (src/routing_filter.h:78-85): hashes
  * (32-bit XXH32 of the keys, as btree_pack produces them, src/btree.c:4020-4024) in,

@@ -1066,6 +1066,61 @@ extern "C" int rf_amd_hash_var_keys(rf_amd_engine* e, const rf_amd_config* cfg, 
   return 0;
 }
 
+// ---- routed probes across ranks --------------------------------------------
+extern "C" uint64_t rf_route_scratch_words(uint64_t n, uint32_t world);
+extern "C" int rf_launch_route(void* stream, const uint32_t* hashes, const uint32_t* gfid, uint64_t n,
+                               const uint32_t* route, uint32_t num_g, uint32_t world, uint64_t* pairs,
+                               uint32_t* perm, uint32_t* scratch, uint64_t* totals);
+extern "C" int rf_launch_unroute(void* stream, const uint64_t* back, const uint32_t* perm, uint64_t n,
+                                 uint64_t* found);
+
+extern "C" uint64_t rf_amd_route_scratch_bytes(uint64_t n, uint32_t world) {
+  return 4 * rf_route_scratch_words(n, world) + 8 + 8 * (uint64_t)RF_AMD_ROUTE_MAX_WORLD;
+}
+
+extern "C" int rf_amd_route_probes(rf_amd_engine* e, const uint32_t* d_hashes, const uint32_t* d_filter_id,
+                                   uint64_t n, const uint32_t* d_route, uint32_t num_filters, uint32_t world,
+                                   uint64_t* d_pairs, uint32_t* d_perm, void* d_scratch, uint64_t* h_counts,
+                                   void* stream) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (world == 0 || world > RF_AMD_ROUTE_MAX_WORLD) return fail(RF_AMD_EINVAL, "world out of range");
+  if (!h_counts) return fail(RF_AMD_EINVAL, "null counts");
+  for (uint32_t d = 0; d < world; d++) h_counts[d] = 0;
+  if (n == 0) return 0;
+  if (n >= (1ull << 32)) return fail(RF_AMD_EINVAL, "more than 2^32 - 1 probes");
+  if (!d_hashes || !d_filter_id || !d_route || !d_pairs || !d_perm || !d_scratch)
+    return fail(RF_AMD_EINVAL, "null route buffer");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  uint32_t* scratch = static_cast<uint32_t*>(d_scratch);
+  const uint64_t words = rf_route_scratch_words(n, world);
+  uint64_t* d_tot = reinterpret_cast<uint64_t*>(scratch + ((words + 1) & ~1ull));
+  if (rf_launch_route(st, d_hashes, d_filter_id, n, d_route, num_filters, world, d_pairs, d_perm, scratch, d_tot))
+    return fail(RF_AMD_EINVAL, "route kernel launch failed");
+  uint32_t err = 0;
+  HIPCHK(hipMemcpyAsync(h_counts, d_tot, 8 * world, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&err, scratch + words - 4, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (err & 1u) return fail(RF_AMD_EINVAL, "probe filter id out of range");
+  if (err & 2u) return fail(RF_AMD_EINVAL, "route table names a rank >= world");
+  return 0;
+}
+
+extern "C" int rf_amd_unroute_found(rf_amd_engine* e, const uint64_t* d_back, const uint32_t* d_perm, uint64_t n,
+                                    uint64_t* d_found, void* stream) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (n && (!d_back || !d_perm || !d_found)) return fail(RF_AMD_EINVAL, "null unroute buffer");
+  HIPCHK(hipSetDevice(e->device));
+  if (rf_launch_unroute(stream ? stream : e->stream, d_back, d_perm, n, d_found))
+    return fail(RF_AMD_EINVAL, "unroute kernel launch failed");
+  return 0;
+}
+
+extern "C" int rf_amd_batch_probe_pairs(rf_amd_batch* b, const uint64_t* d_pairs, uint64_t n, uint64_t* d_found,
+                                        void* stream) {
+  return do_probe(b, IN_PAIR, d_pairs, nullptr, 8, reinterpret_cast<const uint32_t*>(d_pairs), n, d_found, stream);
+}
+
 // ---- routing_filter_verify (src/routing_filter.c:1163-1183) ------------------------------
 extern "C" int rf_launch_count_missing(void* stream, const uint64_t* found, uint64_t n, uint32_t value,
                                        unsigned long long* missing);

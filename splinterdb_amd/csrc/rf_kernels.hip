@@ -1737,6 +1737,149 @@ extern "C" int rf_launch_hash(void* stream, int kind, const void* in0, const uin
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// ======================================================================================
+// Routed probes across ranks: probes arrive on any rank with a global
+// filter id; each is sent to the rank that owns the filter's key range. k_route_count /
+// k_route_scan / k_route_scatter form a stable partition of the probes by destination
+// rank, packed as (local filter id << 32 | hash) pairs for one all-to-all; k_unroute puts
+// the returned found_values back in the caller's order. route[g] = local_id << 8 | rank.
+// ======================================================================================
+constexpr uint32_t ROUTE_NT = 256;
+constexpr uint32_t ROUTE_TILE = 16384;  // probes per workgroup
+constexpr uint32_t ROUTE_MAX_WORLD = 16;
+
+__device__ __forceinline__ uint32_t route_dest(const uint32_t* __restrict__ gfid, const uint32_t* __restrict__ route,
+                                               uint32_t num_g, uint32_t world, uint64_t i, uint32_t* err) {
+  const uint32_t g = gfid[i];
+  if (g >= num_g) { atomicOr(err, 1u); return 0; }
+  const uint32_t d = route[g] & 0xffu;
+  if (d >= world) { atomicOr(err, 2u); return 0; }
+  return d;
+}
+
+__global__ __launch_bounds__(ROUTE_NT) void k_route_count(const uint32_t* __restrict__ gfid, uint64_t n,
+                                                          const uint32_t* __restrict__ route, uint32_t num_g,
+                                                          uint32_t world, uint32_t* __restrict__ cnt,
+                                                          uint32_t* __restrict__ err) {
+  __shared__ uint32_t s_h[ROUTE_MAX_WORLD];
+  if (threadIdx.x < ROUTE_MAX_WORLD) s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+  const uint64_t b1 = min(b0 + ROUTE_TILE, n);
+  for (uint64_t i = b0 + threadIdx.x; i < b1; i += ROUTE_NT)
+    atomicAdd(&s_h[route_dest(gfid, route, num_g, world, i, err)], 1u);
+  __syncthreads();
+  if (threadIdx.x < world) cnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_h[threadIdx.x];
+}
+
+// exclusive scan of cnt[world * nblk] (destination-major) into off; totals[d] = probes to d
+__global__ __launch_bounds__(1024) void k_route_scan(const uint32_t* __restrict__ cnt, uint32_t m,
+                                                     uint32_t nblk, uint32_t world, uint32_t* __restrict__ off,
+                                                     uint64_t* __restrict__ totals) {
+  __shared__ uint32_t s_tmp[1024 / WAVE + 1];
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < m; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t x = i < m ? cnt[i] : 0u;
+    uint32_t tot;
+    const uint32_t r = block_excl_scan<1024>(x, s_tmp, &tot);
+    if (i < m) off[i] = carry + r;
+    carry += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x < world) {
+    const uint32_t d = threadIdx.x;
+    const uint32_t lo = off[d * nblk], hi = d + 1 < world ? off[(d + 1) * nblk] : carry;
+    totals[d] = hi - lo;
+  }
+}
+
+__global__ __launch_bounds__(ROUTE_NT) void k_route_scatter(const uint32_t* __restrict__ hashes,
+                                                            const uint32_t* __restrict__ gfid, uint64_t n,
+                                                            const uint32_t* __restrict__ route, uint32_t num_g,
+                                                            uint32_t world, const uint32_t* __restrict__ off,
+                                                            uint64_t* __restrict__ pairs,
+                                                            uint32_t* __restrict__ perm, uint32_t* __restrict__ err) {
+  constexpr uint32_t NW = ROUTE_NT / WAVE;
+  __shared__ uint32_t s_base[ROUTE_MAX_WORLD];
+  __shared__ uint32_t s_wc[NW][ROUTE_MAX_WORLD];
+  if (threadIdx.x < world) s_base[threadIdx.x] = off[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  const uint32_t w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const uint64_t lt = (1ull << lane) - 1;
+  const uint64_t b0 = (uint64_t)blockIdx.x * ROUTE_TILE;
+  const uint64_t b1 = min(b0 + ROUTE_TILE, n);
+  __syncthreads();
+  // chunks of ROUTE_NT consecutive probes: rank inside the chunk from per-destination
+  // ballots, so the partition keeps the input order within each destination
+  for (uint64_t c = b0; c < b1; c += ROUTE_NT) {
+    const uint64_t i = c + threadIdx.x;
+    const bool ok = i < b1;
+    const uint32_t d = ok ? route_dest(gfid, route, num_g, world, i, err) : 0xffffffffu;
+    uint32_t rank = 0;
+    for (uint32_t q = 0; q < world; q++) {
+      const uint64_t m = __ballot(d == q);
+      if (d == q) rank = __popcll(m & lt);
+      if (lane == 0) s_wc[w][q] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (ok) {
+      uint32_t pos = s_base[d] + rank;
+      for (uint32_t w2 = 0; w2 < w; w2++) pos += s_wc[w2][d];
+      const uint32_t g = gfid[i];
+      const uint32_t lid = g < num_g ? route[g] >> 8 : 0u;  // bad ids: reported through err
+      pairs[pos] = ((uint64_t)lid << 32) | hashes[i];
+      perm[pos] = (uint32_t)i;
+    }
+    __syncthreads();
+    if (threadIdx.x < world) {
+      uint32_t t = 0;
+      for (uint32_t w2 = 0; w2 < NW; w2++) t += s_wc[w2][threadIdx.x];
+      s_base[threadIdx.x] += t;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unroute(const uint64_t* __restrict__ back, const uint32_t* __restrict__ perm,
+                                                 uint64_t n, uint64_t* __restrict__ found) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < n) found[perm[j]] = back[j];
+}
+
+extern "C" uint64_t rf_route_scratch_words(uint64_t n, uint32_t world) {
+  const uint64_t nblk = (n + ROUTE_TILE - 1) / ROUTE_TILE;
+  return 2 * nblk * world + 4;  // cnt + off + err
+}
+
+// scratch: rf_route_scratch_words(n, world) u32 words; totals: world u64 (device)
+extern "C" int rf_launch_route(void* stream, const uint32_t* hashes, const uint32_t* gfid, uint64_t n,
+                               const uint32_t* route, uint32_t num_g, uint32_t world, uint64_t* pairs,
+                               uint32_t* perm, uint32_t* scratch, uint64_t* totals) {
+  if (world == 0 || world > ROUTE_MAX_WORLD) return 1;
+  const uint64_t nblk64 = (n + ROUTE_TILE - 1) / ROUTE_TILE;
+  if (nblk64 * world >= (1ull << 31) || n >= (1ull << 32)) return 1;
+  const uint32_t nblk = (uint32_t)nblk64, m = nblk * world;
+  uint32_t* cnt = scratch;
+  uint32_t* off = scratch + m;
+  uint32_t* err = scratch + 2 * (uint64_t)m;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(err, 0, 4, st) != hipSuccess) return 1;
+  if (nblk) hipLaunchKernelGGL(k_route_count, dim3(nblk), dim3(ROUTE_NT), 0, st, gfid, n, route, num_g, world, cnt, err);
+  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, st, cnt, m, nblk, world, off, totals);
+  if (nblk)
+    hipLaunchKernelGGL(k_route_scatter, dim3(nblk), dim3(ROUTE_NT), 0, st, hashes, gfid, n, route, num_g, world, off,
+                       pairs, perm, err);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+extern "C" int rf_launch_unroute(void* stream, const uint64_t* back, const uint32_t* perm, uint64_t n,
+                                 uint64_t* found) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_unroute, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, back, perm, n,
+                     found);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // routing_filter_verify (src/routing_filter.c:1163-1183): keys whose found_values lacks `value`
 __global__ __launch_bounds__(256) void k_count_missing(const uint64_t* __restrict__ found, uint64_t n,
                                                        uint32_t value, unsigned long long* __restrict__ missing) {
@@ -2042,8 +2185,14 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     fid[q] = 0xffffffffu;
     h[q] = 0;
     if (i < n) {
-      fid[q] = __builtin_nontemporal_load(filter_id + i);
-      h[q] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
+      if constexpr (KIND == IN_PAIR) {  // routed probes: (local filter id << 32 | hash)
+        const uint64_t pr = __builtin_nontemporal_load(static_cast<const uint64_t*>(in0) + i);
+        fid[q] = (uint32_t)(pr >> 32);
+        h[q] = (uint32_t)pr;
+      } else {
+        fid[q] = __builtin_nontemporal_load(filter_id + i);
+        h[q] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
+      }
     }
   }
   uint4 pp[PPL];
@@ -2263,6 +2412,7 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
       case IN_KEYS_W: PK(IN_KEYS_W, PROBE_LDS_PAD, PROBE_PPL); break;
       case IN_KEYS_B: PK(IN_KEYS_B, PROBE_LDS_PAD, PROBE_PPL); break;
       case IN_VAR: PK(IN_VAR, PROBE_LDS_PAD, PROBE_PPL); break;
+      case IN_PAIR: PK(IN_PAIR, PROBE_LDS_PAD, PROBE_PPL); break;
       default: PK(IN_HASH, PROBE_LDS_PAD, PROBE_PPL); break;
     }
   }

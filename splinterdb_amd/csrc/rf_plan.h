@@ -27,7 +27,7 @@ constexpr int ASM_NT = 256;
 constexpr uint32_t ASM_MAXB_HOST = 128;  // = ASM_MAXB in rf_kernels.hip (blocks per page in LDS)
 constexpr uint32_t ASM_GT_HOST = 1024;   // = ASM_GT (group-start table entries per page)
 
-enum InputKind { IN_KEYS24 = 0, IN_KEYS_W = 1, IN_KEYS_B = 2, IN_VAR = 3, IN_HASH = 4 };
+enum InputKind { IN_KEYS24 = 0, IN_KEYS_W = 1, IN_KEYS_B = 2, IN_VAR = 3, IN_HASH = 4, IN_PAIR = 5 };
 
 constexpr uint32_t ERR_INDEX_OVERFLOW = 1u, ERR_BLOCK_TOO_BIG = 2u, ERR_PAGE_CAP = 4u,
                    ERR_GEOMETRY = 8u;

@@ -43,7 +43,9 @@ EXPORTED = [
     "rf_amd_lookup_async", "rf_amd_lookup_async_poll", "rf_amd_lookup_async_wait",
     "rf_amd_lookup_async_free", "rf_amd_filter_verify", "rf_amd_filter_print",
     "rf_amd_hash_keys", "rf_amd_hash_var_keys",
+    "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
 ]
+ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
 ASYNC_STATUS_DONE = 1
 CALLBACK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
@@ -145,6 +147,11 @@ def load_library(build_if_missing=True):
     L.rf_amd_filter_print.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), vp]
     L.rf_amd_hash_keys.argtypes = [vp, ctypes.POINTER(RfConfig), vp, u32, u64, vp, vp]
     L.rf_amd_hash_var_keys.argtypes = [vp, ctypes.POINTER(RfConfig), vp, vp, u64, vp, vp]
+    L.rf_amd_route_scratch_bytes.argtypes = [u64, u32]
+    L.rf_amd_route_scratch_bytes.restype = u64
+    L.rf_amd_route_probes.argtypes = [vp, vp, vp, u64, vp, u32, u32, vp, vp, vp, ctypes.POINTER(u64), vp]
+    L.rf_amd_batch_probe_pairs.argtypes = [vp, vp, u64, vp, vp]
+    L.rf_amd_unroute_found.argtypes = [vp, vp, vp, u64, vp, vp]
     _lib = L
     return L
 
@@ -410,6 +417,28 @@ def hash_var_keys(cfg: RoutingConfig, d_bytes, d_offsets, n, d_hashes, stream=No
                                                _dptr(d_hashes), _stream(stream)))
 
 
+def route_scratch_bytes(n, world):
+    return int(load_library().rf_amd_route_scratch_bytes(n, world))
+
+
+def route_probes(d_hashes, d_filter_id, n, d_route, num_filters, world, d_pairs, d_perm, d_scratch,
+                 stream=None, engine=None):
+    """Stable partition of n probes by owning rank (rf_amd_route_probes); returns the
+    per-rank pair counts (list of `world` ints)."""
+    eng = engine or default_engine()
+    counts = (ctypes.c_uint64 * max(1, world))()
+    _check(load_library().rf_amd_route_probes(eng.h, _dptr(d_hashes), _dptr(d_filter_id), n, _dptr(d_route),
+                                              num_filters, world, _dptr(d_pairs), _dptr(d_perm),
+                                              _dptr(d_scratch), counts, _stream(stream)))
+    return [int(c) for c in counts[:world]]
+
+
+def unroute_found(d_back, d_perm, n, d_found, stream=None, engine=None):
+    eng = engine or default_engine()
+    _check(load_library().rf_amd_unroute_found(eng.h, _dptr(d_back), _dptr(d_perm), n, _dptr(d_found),
+                                               _stream(stream)))
+
+
 class LookupAsync:
     """routing_filter_lookup_async (src/routing_filter.h:130-155) for a batch of host keys
     against a built FilterBatch: poll() returns ASYNC_STATUS_RUNNING / ASYNC_STATUS_DONE;
@@ -540,6 +569,11 @@ class FilterBatch:
     def probe_hashes(self, d_hashes, d_filter_id, n, d_found, stream=None):
         _check(load_library().rf_amd_batch_probe_hashes(self.h, _dptr(d_hashes), _dptr(d_filter_id),
                                                         n, _dptr(d_found), _stream(stream)))
+
+    def probe_pairs(self, d_pairs, n, d_found, stream=None):
+        """Probes given as (local filter id << 32 | hash) u64 pairs (routed probes, route.py)."""
+        _check(load_library().rf_amd_batch_probe_pairs(self.h, _dptr(d_pairs), n, _dptr(d_found),
+                                                       _stream(stream)))
 
     # fresh builds: partition = fused hash + coarse-bucket partition (K1+K3); count_scan and
     # scatter = the spill fallback (near zero unless a coarse bucket overflowed); incremental

@@ -63,6 +63,15 @@ def seq_keys_torch(start: int, n: int, key_len: int, device):
     return k
 
 
+def ids_keys_torch(ids, key_len: int = 24):
+    """filter_test-format keys of the given ids (int64 device tensor), on its device."""
+    import torch
+    n = ids.numel()
+    k = torch.zeros((n, key_len), dtype=torch.uint8, device=ids.device)
+    k[:, :8] = ids.contiguous().view(torch.uint8).view(n, 8)
+    return k
+
+
 # ---- C5: variable-length keys + Zipf(0.99) probe mix (SURVEY.md §8(d)) -----------------
 def zipf_ids(n: int, count: int, s: float = 0.99, seed: int = 1) -> np.ndarray:
     """`count` ids in [0, n) with P(rank r) ~ r^-s (rank 1 hottest); ranks are scattered
