@@ -2178,9 +2178,49 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
   }
   const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (PROBE_NT * PPL) + threadIdx.x;
   uint32_t h[PPL], fid[PPL];
+  constexpr bool WAVE_KEYS = KIND == IN_KEYS24 && PPL == 1 && OCC_LDS == 0;
+  if constexpr (WAVE_KEYS) {
+    // 24-byte keys: the wave's 64 keys (1,536 contiguous bytes) are read with 16-byte
+    // coalesced loads -- 12 cache lines per wave, where three strided 8-byte loads per lane
+    // touch 36 -- and handed to their lanes through LDS
+    __shared__ v4u s_keys[PROBE_NT / WAVE][96];
+    const uint32_t lane = threadIdx.x & (WAVE - 1);
+    const uint64_t wf = i0 - lane;
+    fid[0] = 0xffffffffu;
+    h[0] = 0;
+    if (wf < n) {  // uniform per wave
+      if (i0 < n) fid[0] = __builtin_nontemporal_load(filter_id + i0);
+      if (((uintptr_t)in0 & 15) == 0) {
+        v4u* sw = s_keys[threadIdx.x / WAVE];
+        const uint32_t bytes = (uint32_t)min<uint64_t>(WAVE, n - wf) * 24;
+        const v4u* src = reinterpret_cast<const v4u*>(static_cast<const uint8_t*>(in0) + wf * 24);
+#pragma unroll
+        for (uint32_t j = lane; j < 96; j += WAVE) {
+          if ((j + 1) * 16 <= bytes) {
+            sw[j] = __builtin_nontemporal_load(src + j);
+          } else if (j * 16 < bytes) {  // an odd key count ends on an 8-byte half
+            const uint64_t t = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + j));
+            sw[j] = v4u{(uint32_t)t, (uint32_t)(t >> 32), 0u, 0u};
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (i0 < n) {
+          const uint2* k2 = reinterpret_cast<const uint2*>(sw) + 3 * lane;
+          const uint2 a = k2[0], b = k2[1], c = k2[2];
+          uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+          h[0] = xxh32_24(w, seed);
+        }
+      } else if (i0 < n) {
+        h[0] = hash_key<KIND, true>(in0, offs, key_len, seed, i0);
+      }
+    }
+  }
   // the keys (or hashes) and filter ids are independent loads: issue them all together
 #pragma unroll
   for (int q = 0; q < PPL; q++) {
+    if constexpr (WAVE_KEYS) break;
     const uint64_t i = i0 + (uint64_t)q * PROBE_NT;
     fid[q] = 0xffffffffu;
     h[q] = 0;
