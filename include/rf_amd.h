@@ -144,6 +144,18 @@ int rf_amd_hash_keys(rf_amd_engine *e, const rf_amd_config *cfg, const void *d_k
 int rf_amd_hash_var_keys(rf_amd_engine *e, const rf_amd_config *cfg, const uint8_t *d_bytes,
                          const uint64_t *d_offsets, uint64_t n, uint32_t *d_hashes, void *stream);
 
+/* Import filter images as a built, probe-only batch (e.g. images all-gathered from the
+ * other ranks when probes are replicated rather than routed). Filter f's
+ * pages are the infos[f].num_pages * page_size bytes after those of filters < f in
+ * `pages`; its relocatable index slots the infos[f].num_indices u64 after those of
+ * filters < f in `slots`. device_resident: the buffers are HIP device memory (else host).
+ * The batch copies them; probe lines are cut on the device. */
+int rf_amd_batch_export(rf_amd_batch *b, void *d_pages, uint64_t pages_bytes, uint64_t *d_slots,
+                        uint64_t num_slots, void *stream); /* all filters, packed as import reads them */
+int rf_amd_batch_import(rf_amd_engine *e, const rf_amd_config *cfg, uint32_t num_filters,
+                        const rf_amd_filter_info *infos, const void *pages, const uint64_t *slots,
+                        int device_resident, rf_amd_batch **out);
+
 /* ---- routed probes across ranks (multi-GPU serving) --------------------
  * Each rank owns the filters of a contiguous key range (one filter per trunk pivot,
  * src/trunk.c:4133-4170); a probe may arrive on any rank. rf_amd_route_probes partitions

@@ -618,70 +618,142 @@ extern "C" int rf_amd_batch_image_ptrs(rf_amd_batch* b, uint32_t f, void** d_pag
   return 0;
 }
 
-// ---- image batches: a host image uploaded as a built one-filter batch ------------------
-static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* img,
-                            rf_amd_batch** out) {
+// ---- image batches: images (host or device) imported as a built, probe-only batch --------
+// Filter f's pages are the num_pages[f] * page_size bytes after those of filters < f in
+// `pages`, its index slots (relocatable, filter-relative) the num_indices[f] u64 after
+// those of filters < f in `slots`. Probe lines are cut from the images by k_plines.
+static int batch_import(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t F, const rf_amd_filter_info* infos,
+                        const void* pages, const uint64_t* slots, hipMemcpyKind kind, rf_amd_batch** out) {
   if (int rc = check_cfg(cfg)) return rc;
-  if (!img || !img->pages || !img->slots || img->info.num_fingerprints == 0)
-    return fail(RF_AMD_EINVAL, "bad image");
+  if (F == 0 || !infos || !pages || !slots) return fail(RF_AMD_EINVAL, "bad image");
   HIPCHK(hipSetDevice(e->device));
   auto* b = new rf_amd_batch();
   b->eng = e;
   b->cfg = *cfg;
-  b->F = 1;
-  b->plans.resize(1);
-  FilterPlan& p = b->plans[0];
-  memset(&p, 0, sizeof(p));
+  b->F = F;
+  b->plans.resize(F);
   const uint32_t lis = cfg->log_index_size;
-  uint32_t lnb = 31 - __builtin_clz(img->info.num_fingerprints);
-  if (lnb < lis) lnb = lis;
-  if (lnb > cfg->fingerprint_size || (1u << (lnb - lis)) > MAX_INDICES) {
+  std::vector<uint4> pp(F);
+  std::vector<uint32_t> idx_filter;
+  uint64_t pages_total = 0, idx_total = 0, lines_total = 0;
+  for (uint32_t f = 0; f < F; f++) {
+    const rf_amd_filter_info& in = infos[f];
+    FilterPlan& p = b->plans[f];
+    memset(&p, 0, sizeof(p));
+    uint32_t lnb = in.num_fingerprints ? 31 - __builtin_clz(in.num_fingerprints) : 0;
+    if (lnb < lis) lnb = lis;
+    if (in.num_fingerprints == 0 || lnb > cfg->fingerprint_size || (1u << (lnb - lis)) > MAX_INDICES ||
+        in.num_indices != (1u << (lnb - lis)) || in.value_size > 32 - cfg->fingerprint_size || in.error ||
+        in.num_pages == 0) {
+      delete b;
+      return fail(RF_AMD_EINVAL, "image geometry out of range (filter " + std::to_string(f) + ")");
+    }
+    p.num_fp = in.num_fingerprints;
+    p.lnb = lnb;
+    p.vs = in.value_size;
+    p.rem = cfg->fingerprint_size - lnb;
+    p.rvs = p.rem + p.vs;
+    p.num_indices = in.num_indices;
+    p.page_cap = in.num_pages;
+    p.page_base = (uint32_t)pages_total;
+    p.idx_base = (uint32_t)idx_total;
+    p.lg_line = line_log_group(lis, p.rvs, (double)in.num_fingerprints / (double)(1ull << lnb));
+    p.line_base = (uint32_t)lines_total;
+    pp[f] = make_uint4(p.vs | (p.rem << 8) | (p.rvs << 16) | (p.lg_line << 24), p.line_base, p.idx_base, 0);
+    if (p.lg_line) {
+      lines_total += (uint64_t)p.num_indices << (lis - (p.lg_line - 1));
+      b->line_lmax = std::max(b->line_lmax, (1u << lis) >> (p.lg_line - 1));
+      b->plines_needed = true;
+    }
+    idx_filter.insert(idx_filter.end(), p.num_indices, f);
+    pages_total += in.num_pages;
+    idx_total += p.num_indices;
+  }
+  if (lines_total >= (1ull << 32) || pages_total >= (1ull << 32)) {
     delete b;
-    return fail(RF_AMD_EINVAL, "image geometry out of range");
+    return fail(RF_AMD_EINVAL, "import too large");
   }
-  p.num_fp = img->info.num_fingerprints;
-  p.lnb = lnb;
-  p.vs = img->info.value_size;
-  p.rem = cfg->fingerprint_size - lnb;
-  p.rvs = p.rem + p.vs;
-  p.num_indices = 1u << (lnb - lis);
-  p.page_cap = img->info.num_pages;
-  p.lg_line = line_log_group(lis, p.rvs, (double)img->info.num_fingerprints / (double)(1ull << lnb));
-  b->PS = img->info.num_pages;
-  b->I = p.num_indices;
-  if (p.lg_line) {
-    b->NL = (uint64_t)p.num_indices << (lis - (p.lg_line - 1));
-    b->line_lmax = (1u << lis) >> (p.lg_line - 1);
-    b->plines_needed = true;  // uploaded image: lines are cut by k_plines
-  }
-  int rc = b->d_plans.alloc(sizeof(FilterPlan));
-  rc |= b->d_pplans.alloc(16);
-  rc |= b->d_pages.alloc((size_t)img->info.num_pages * cfg->page_size + 256);
-  rc |= b->d_slots.alloc(8ull * p.num_indices);
+  b->PS = (uint32_t)pages_total;
+  b->I = (uint32_t)idx_total;
+  b->NL = lines_total;
+  const size_t page_bytes = (size_t)pages_total * cfg->page_size;
+  int rc = b->d_plans.alloc(sizeof(FilterPlan) * F);
+  rc |= b->d_pplans.alloc(16ull * F);
+  rc |= b->d_pages.alloc(page_bytes + 256);
+  rc |= b->d_slots.alloc(8ull * idx_total);
   rc |= b->d_lines.alloc(64ull * b->NL + 64);
-  rc |= b->d_idx_filter.alloc(4ull * p.num_indices);
+  rc |= b->d_idx_filter.alloc(4ull * idx_total);
+  rc |= b->d_outs.alloc(sizeof(FilterOut) * F);
   if (rc) {
     delete b;
     return fail(RF_AMD_ENOMEM, "device allocation failed");
   }
+  std::vector<FilterOut> outs(F);
+  for (uint32_t f = 0; f < F; f++) outs[f] = FilterOut{infos[f].num_unique, infos[f].num_pages, 0u, 0u};
   hipStream_t st = e->stream;
-  HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
-  HIPCHK(hipMemsetAsync(b->d_idx_filter.p, 0, b->d_idx_filter.n, st));
-  HIPCHK(hipMemcpyAsync(b->d_pages.p, img->pages, (size_t)img->info.num_pages * cfg->page_size,
-                        hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(b->d_slots.p, img->slots, 8ull * p.num_indices, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(b->d_plans.p, &p, sizeof(p), hipMemcpyHostToDevice, st));
-  const uint4 pp1 = make_uint4(p.vs | (p.rem << 8) | (p.rvs << 16) | (p.lg_line << 24), 0, 0, 0);
-  HIPCHK(hipMemcpyAsync(b->d_pplans.p, &pp1, sizeof(pp1), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(b->d_outs.p, outs.data(), sizeof(FilterOut) * F, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(b->d_pages.as<uint8_t>() + page_bytes, 0, 256, st));
+  HIPCHK(hipMemcpyAsync(b->d_pages.p, pages, page_bytes, kind, st));
+  HIPCHK(hipMemcpyAsync(b->d_slots.p, slots, 8ull * idx_total, kind, st));
+  HIPCHK(hipMemcpyAsync(b->d_idx_filter.p, idx_filter.data(), 4ull * idx_total, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(b->d_plans.p, b->plans.data(), sizeof(FilterPlan) * F, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(b->d_pplans.p, pp.data(), 16ull * F, hipMemcpyHostToDevice, st));
   {
     LaunchArgs a = make_args(b, st);
-    if (int lrc = rf_launch_plines(&a))
+    if (int lrc = rf_launch_plines(&a)) {
+      delete b;
       return fail(RF_AMD_EINVAL, std::string("probe-line launch: ") + hipGetErrorString((hipError_t)lrc));
+    }
   }
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipStreamSynchronize(st));  // host vectors above are released on return
   b->built = true;
   *out = b;
   return 0;
+}
+
+static int batch_from_image(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* img,
+                            rf_amd_batch** out) {
+  if (!img || !img->pages || !img->slots || img->info.num_fingerprints == 0)
+    return fail(RF_AMD_EINVAL, "bad image");
+  return batch_import(e, cfg, 1, &img->info, img->pages, img->slots, hipMemcpyHostToDevice, out);
+}
+
+extern "C" int rf_amd_batch_export(rf_amd_batch* b, void* d_pages, uint64_t pages_bytes, uint64_t* d_slots,
+                                   uint64_t num_slots, void* stream) {
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "export of an unbuilt batch");
+  uint64_t po = 0, so = 0;
+  std::vector<rf_amd_filter_info> inf(b->F);
+  for (uint32_t f = 0; f < b->F; f++) {
+    if (int rc = rf_amd_batch_info(b, f, &inf[f])) return rc;
+    if (inf[f].error) return fail(RF_AMD_EINVAL, "filter build reported error bits");
+    po += (uint64_t)inf[f].num_pages * b->cfg.page_size;
+    so += inf[f].num_indices;
+  }
+  if (!d_pages || !d_slots || pages_bytes < po || num_slots < so) return fail(RF_AMD_EINVAL, "export buffers too small");
+  hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  po = so = 0;
+  for (uint32_t f = 0; f < b->F; f++) {
+    const FilterPlan& p = b->plans[f];
+    const uint64_t pb = (uint64_t)inf[f].num_pages * b->cfg.page_size;
+    HIPCHK(hipMemcpyAsync(static_cast<uint8_t*>(d_pages) + po,
+                          b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size, pb,
+                          hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_slots + so, b->d_slots.as<uint64_t>() + p.idx_base, 8ull * p.num_indices,
+                          hipMemcpyDeviceToDevice, st));
+    po += pb;
+    so += p.num_indices;
+  }
+  return 0;
+}
+
+extern "C" int rf_amd_batch_import(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t num_filters,
+                                   const rf_amd_filter_info* infos, const void* pages, const uint64_t* slots,
+                                   int device_resident, rf_amd_batch** out) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (!out) return fail(RF_AMD_EINVAL, "null out-param");
+  *out = nullptr;
+  return batch_import(e, cfg, num_filters, infos, pages, slots,
+                      device_resident ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, out);
 }
 
 extern "C" int rf_amd_filter_add(rf_amd_engine* e, const rf_amd_config* cfg, const rf_amd_image* old_filter,

@@ -43,7 +43,7 @@ EXPORTED = [
     "rf_amd_lookup_async", "rf_amd_lookup_async_poll", "rf_amd_lookup_async_wait",
     "rf_amd_lookup_async_free", "rf_amd_filter_verify", "rf_amd_filter_print",
     "rf_amd_hash_keys", "rf_amd_hash_var_keys",
-    "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
+    "rf_amd_batch_export", "rf_amd_batch_import", "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -147,6 +147,9 @@ def load_library(build_if_missing=True):
     L.rf_amd_filter_print.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), vp]
     L.rf_amd_hash_keys.argtypes = [vp, ctypes.POINTER(RfConfig), vp, u32, u64, vp, vp]
     L.rf_amd_hash_var_keys.argtypes = [vp, ctypes.POINTER(RfConfig), vp, vp, u64, vp, vp]
+    L.rf_amd_batch_export.argtypes = [vp, vp, u64, vp, u64, vp]
+    L.rf_amd_batch_import.argtypes = [vp, ctypes.POINTER(RfConfig), u32, ctypes.POINTER(RfFilterInfo), vp, vp,
+                                      i32, ctypes.POINTER(vp)]
     L.rf_amd_route_scratch_bytes.argtypes = [u64, u32]
     L.rf_amd_route_scratch_bytes.restype = u64
     L.rf_amd_route_probes.argtypes = [vp, vp, vp, u64, vp, u32, u32, vp, vp, vp, ctypes.POINTER(u64), vp]
@@ -497,6 +500,13 @@ def _stream(stream):
     return None
 
 
+def _hptr(x):
+    """Address of a numpy array, torch tensor or int."""
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    return _dptr(x)
+
+
 def _dptr(x):
     """Device pointer of a torch tensor (or an int address)."""
     if x is None:
@@ -535,6 +545,33 @@ class FilterBatch:
                                      oi_arr.ctypes.data if oi_arr is not None else None,
                                      ctypes.byref(h)))
         self.h = h
+
+    @classmethod
+    def imported(cls, cfg: RoutingConfig, infos, d_pages, d_slots, device_resident=True, engine=None):
+        """A built, probe-only batch from packed images (rf_amd_batch_import); infos: one
+        RfFilterInfo per filter."""
+        self = cls.__new__(cls)
+        self.engine = engine or default_engine()
+        self.cfg = cfg
+        self.F = len(infos)
+        arr = (RfFilterInfo * max(1, self.F))(*infos)
+        self._keep = [arr]
+        h = ctypes.c_void_p()
+        _check(load_library().rf_amd_batch_import(self.engine.h, ctypes.byref(cfg.c()), self.F, arr,
+                                                  _hptr(d_pages), _hptr(d_slots), 1 if device_resident else 0,
+                                                  ctypes.byref(h)))
+        self.h = h
+        return self
+
+    def export(self, d_pages, d_slots, stream=None):
+        """Pack every filter's pages and slots (device tensors sized by export_sizes())."""
+        _check(load_library().rf_amd_batch_export(self.h, _dptr(d_pages), d_pages.numel() * d_pages.element_size(),
+                                                  _dptr(d_slots), d_slots.numel(), _stream(stream)))
+
+    def export_sizes(self):
+        """(infos, total page bytes, total index slots) of the packed export."""
+        infos = [self.info(f) for f in range(self.F)]
+        return infos, sum(i.num_pages for i in infos) * self.cfg.page_size, sum(i.num_indices for i in infos)
 
     def close(self):
         if getattr(self, "h", None):

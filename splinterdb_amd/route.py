@@ -6,7 +6,12 @@ of the trunk node owning the key's range (src/trunk.c:6008-6075). With filters s
 ranks, probes must move to the owning rank and the found_values bit-vectors come back:
 one all-to-all each way (RCCL over xGMI on the GPU box; gloo in the CPU tests).
 
-Per lookup batch on every rank:
+The alternative when lookups are frequent and filters change rarely: replicate the images
+once (replicate_images: one all-gather of every rank's packed pages + slots, imported on
+each rank as a probe-only batch of all filters) and probe locally with no per-lookup
+exchange.
+
+Per lookup batch on every rank (routed):
   1. hash the keys where they are (XXH32, rf_amd_hash_keys): 4 B instead of the key moves;
   2. rf_amd_route_probes: stable partition of (hash, local filter id) pairs by owner rank,
      with per-rank counts (the all-to-all split sizes);
@@ -118,3 +123,53 @@ class ProbeRouter:
         if n:
             self.ops.unroute(back, self.d_perm, n, d_found)
         return send, recv
+
+
+_INFO_FIELDS = ("num_fingerprints", "num_unique", "value_size", "num_indices", "num_pages", "error")
+
+
+def _all_gather_padded(dist, t, world):
+    """all_gather of 1-D tensors of different lengths (padded to the longest)."""
+    import torch
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    m = max(max(ns), 1)
+    pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+    pad[: t.numel()] = t
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    return [o[:k] for o, k in zip(outs, ns)]
+
+
+def replicate_images(batch, world, device, dist=None, coll_device=None, engine=None):
+    """Every rank's filters (in rank = global filter order) as one probe-only batch on this
+    rank: pack (rf_amd_batch_export), all-gather pages, slots and filter infos, import
+    (rf_amd_batch_import). Probes then use global filter ids locally."""
+    import torch
+    device = torch.device(device)
+    coll = torch.device(coll_device) if coll_device is not None else device
+    infos, pbytes, nslots = batch.export_sizes()
+    d_pages = torch.empty(max(pbytes, 1), dtype=torch.uint8, device=device)
+    d_slots = torch.empty(max(nslots, 1), dtype=torch.int64, device=device)
+    batch.export(d_pages, d_slots)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    d_pages, d_slots = d_pages[:pbytes], d_slots[:nslots]
+    inf = torch.tensor([[getattr(i, k) for k in _INFO_FIELDS] for i in infos], dtype=torch.int64).reshape(-1)
+    if world == 1:
+        parts = [(inf, d_pages, d_slots)]
+    else:
+        gi = _all_gather_padded(dist, inf.to(coll), world)
+        gp = _all_gather_padded(dist, d_pages.to(coll), world)
+        gs = _all_gather_padded(dist, d_slots.to(coll), world)
+        parts = list(zip(gi, gp, gs))
+    all_inf = torch.cat([p[0].cpu() for p in parts]).reshape(-1, len(_INFO_FIELDS)).tolist()
+    rinfos = [E.RfFilterInfo(*[int(x) for x in row]) for row in all_inf]
+    pages = torch.cat([p[1] for p in parts])
+    slots = torch.cat([p[2] for p in parts])
+    on_dev = pages.device.type == "cuda"
+    return E.FilterBatch.imported(batch.cfg, rinfos, pages, slots, device_resident=on_dev,
+                                  engine=engine or batch.engine)
+

@@ -233,3 +233,75 @@ def test_router_two_ranks_on_one_gpu(oracle):
         for r in range(world):
             z = np.load(os.path.join(d, f"g{r}.npz"))
             _check_against_oracle(oracle, F, n, z["h"], z["gfid"], z["found"])
+
+
+# ---- replicated probes: export / all-gather / import -------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_resident", [True, False])
+def test_export_import_round_trip(oracle, device_resident):
+    from splinterdb_amd import engine as E
+    cfg = E.routing_config_init()
+    sizes, vals = [30000, 1, 250000, 4097], [3, 0, 7, 1]
+    b = E.FilterBatch(cfg, sizes, vals)
+    kk = K.seq_keys(0, sum(sizes)).reshape(-1)
+    b.build_keys(_dev(kk), 24)
+    infos, pbytes, nslots = b.export_sizes()
+    d_p = torch.zeros(pbytes, dtype=torch.uint8, device="cuda:0")
+    d_s = torch.zeros(nslots, dtype=torch.int64, device="cuda:0")
+    b.export(d_p, d_s)
+    torch.cuda.synchronize()
+    src_p, src_s = (d_p, d_s) if device_resident else (d_p.cpu().numpy(), d_s.cpu().numpy())
+    imp = E.FilterBatch.imported(cfg, infos, src_p, src_s, device_resident=device_resident)
+    for f in range(len(sizes)):
+        a, c = b.image(f), imp.image(f)
+        assert (a.num_unique, a.num_pages) == (c.num_unique, c.num_pages)
+        assert (a.pages == c.pages).all() and (a.slots == c.slots).all()
+    rng = np.random.default_rng(5)
+    P = 50000
+    ids = rng.integers(0, 2 * sum(sizes), size=P).astype(np.uint64)
+    fid = rng.integers(0, len(sizes), size=P).astype(np.uint32)
+    pk = _dev(K.ids_keys(ids).reshape(-1))
+    f1 = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    f2 = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b.probe_keys(pk, 24, _dev(fid.view(np.int32)), P, f1)
+    imp.probe_keys(pk, 24, _dev(fid.view(np.int32)), P, f2)
+    torch.cuda.synchronize()
+    assert torch.equal(f1, f2)
+    with pytest.raises(E.PlatformStatusError):  # geometry that no build produces
+        bad = E.RfFilterInfo(infos[0].num_fingerprints, 1, 0, infos[0].num_indices * 2, infos[0].num_pages, 0)
+        E.FilterBatch.imported(cfg, [bad], d_p, d_s)
+
+
+def _replica_worker(rank, world, port, F, n, outdir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from splinterdb_amd import engine as E
+    cfg = E.routing_config_init()
+    me = S.plan_shards(F, n, world)[rank]
+    b = E.FilterBatch(cfg, [n] * me.num_filters, [f % 8 for f in range(me.filter_begin, me.filter_end)])
+    b.build_keys(_dev(K.seq_keys(me.filter_begin * n, me.num_filters * n).reshape(-1)), 24)
+    rep = R.replicate_images(b, world, "cuda:0", dist=dist, coll_device="cpu")
+    assert rep.F == F
+    rng = np.random.default_rng(11 + rank)
+    ids, gfid = _probe_set(rng, F, n, 30000)
+    keys = np.concatenate([K.seq_keys(int(i), 1) for i in ids]).reshape(-1)
+    found = torch.zeros(len(ids), dtype=torch.int64, device="cuda:0")
+    rep.probe_keys(_dev(keys), 24, _dev(gfid.view(np.int32)), len(ids), found)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(outdir, f"p{rank}.npz"), h=O.hash_fixed(keys, 24), gfid=gfid,
+             found=found.cpu().numpy().view(np.uint64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_replicated_images_two_ranks(oracle):
+    F, n, world = 5, 30000, 2
+    port = 30400 + (os.getpid() % 500)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_replica_worker, args=(world, port, F, n, d), nprocs=world, join=True)
+        for r in range(world):
+            z = np.load(os.path.join(d, f"p{r}.npz"))
+            _check_against_oracle(oracle, F, n, z["h"], z["gfid"], z["found"])
