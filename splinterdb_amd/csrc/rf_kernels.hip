@@ -924,6 +924,45 @@ __device__ __forceinline__ uint32_t block_size(uint32_t c, uint32_t index_size, 
   return enc + 2 + rbs;
 }
 
+// Exclusive scan of x[k] over the elements j = k * NT + threadIdx.x (k-major order), so the
+// global loads and stores around it are lane-consecutive (coalesced). s_w: PER * NT/64 + 1
+// words. Contains barriers: call from every thread.
+template <int NT, int PER>
+__device__ __forceinline__ void block_excl_scan_kmajor(const uint32_t (&x)[PER], uint32_t (&out)[PER],
+                                                       uint32_t* s_w, uint32_t* total) {
+  constexpr int NW = NT / WAVE, M = PER * NW, Q = (M + WAVE - 1) / WAVE;
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  uint32_t inc[PER];
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    inc[k] = wave_incl_scan(x[k]);
+    if (lane == WAVE - 1) s_w[k * NW + w] = inc[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < WAVE) {  // one wave scans the M wave totals in (k, wave) order
+    uint32_t v[Q], sum = 0;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int i = threadIdx.x * Q + q;
+      v[q] = i < M ? s_w[i] : 0u;
+      sum += v[q];
+    }
+    uint32_t e = wave_incl_scan(sum) - sum;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int i = threadIdx.x * Q + q;
+      if (i < M) s_w[i] = e;
+      e += v[q];
+    }
+    if (threadIdx.x == WAVE - 1) s_w[M] = e;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; k++) out[k] = s_w[k * NW + w] + inc[k] - x[k];
+  *total = s_w[M];
+  __syncthreads();
+}
+
 constexpr uint32_t LAYOUT_LIST = 520;
 __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restrict__ plans,
                                                       const uint32_t* __restrict__ idx_cnt,
@@ -943,6 +982,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
   __shared__ uint32_t s_err;
   __shared__ uint16_t s_list[LAYOUT_LIST];  // every 2^R-th page start (<= 2 * 2^R + 2 of them)
+  __shared__ uint32_t s_wt[MAX_INDICES / LAYOUT_NT * (LAYOUT_NT / WAVE) + 1];  // k-major scan totals
   __shared__ uint32_t s_nlist;
   const uint32_t f = blockIdx.x;
   const FilterPlan& P = plans[f];
@@ -952,11 +992,11 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   DBG_PHASE_K(4, 15);
   if (threadIdx.x == 0) s_err = 0;
   __syncthreads();
-  // sizes -> exclusive prefix (contiguous ownership: thread t owns [t*PER, t*PER+PER))
-  uint32_t sz[PER], sum = 0, err = 0;
+  // sizes -> exclusive prefix (element j = k * LAYOUT_NT + thread: coalesced loads)
+  uint32_t sz[PER], err = 0;
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x * PER + k;
+    const uint32_t j = k * LAYOUT_NT + threadIdx.x;
     sz[k] = 0;
     if (j < n) {
       const uint32_t c = idx_cnt[P.idx_base + j];
@@ -964,16 +1004,14 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
       sz[k] = block_size(c, index_size, P.rvs);
       if (sz[k] > page_size) err |= ERR_BLOCK_TOO_BIG;
     }
-    sum += sz[k];
   }
   if (err) atomicOr(&s_err, err);
-  uint32_t total;
-  uint32_t run = block_excl_scan<LAYOUT_NT>(sum, s_tmp, &total);
+  uint32_t total, ex[PER];
+  block_excl_scan_kmajor<LAYOUT_NT, PER>(sz, ex, s_wt, &total);
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x * PER + k;
-    if (j < n) s_excl[j] = run;
-    run += sz[k];
+    const uint32_t j = k * LAYOUT_NT + threadIdx.x;
+    if (j < n) s_excl[j] = ex[k];
   }
   // the total at j == n: no thread owns it when n == MAX_INDICES
   if (threadIdx.x == 0) s_excl[n] = total;
@@ -1074,29 +1112,26 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   }
   DBG_PHASE_K(4, 2);
   // page numbers: inclusive scan of marks over [0, n)
-  uint32_t mk[PER], msum = 0;
+  uint32_t mk[PER], pg[PER];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x * PER + k;
+    const uint32_t j = k * LAYOUT_NT + threadIdx.x;
     mk[k] = j < n ? s_mark[j] : 0u;
-    msum += mk[k];
   }
   uint32_t npages;
-  uint32_t mrun = block_excl_scan<LAYOUT_NT>(msum, s_tmp, &npages);
+  block_excl_scan_kmajor<LAYOUT_NT, PER>(mk, pg, s_wt, &npages);
   uint16_t* s_pstart = s_jB;  // reuse: page -> first block
-  uint32_t pg[PER];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x * PER + k;
-    mrun += mk[k];
-    pg[k] = mrun - 1;
+    const uint32_t j = k * LAYOUT_NT + threadIdx.x;
+    pg[k] += mk[k] - 1;  // inclusive count - 1
     if (j < n && mk[k]) s_pstart[pg[k]] = (uint16_t)j;
   }
   __syncthreads();
   uint32_t* pf = page_first + P.pf_base;
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x * PER + k;
+    const uint32_t j = k * LAYOUT_NT + threadIdx.x;
     if (j < n) {
       const uint32_t ps = s_pstart[pg[k]];
       slots[P.idx_base + j] = (uint64_t)pg[k] * page_size + (s_excl[j] - s_excl[ps]);
