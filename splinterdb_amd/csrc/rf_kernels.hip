@@ -1295,6 +1295,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   __shared__ uint32_t s_est[ASM_MAXB + 1];
   __shared__ uint32_t s_src[ASM_MAXB];
   __shared__ uint16_t s_rblk[ASM_MAXE / ASM_RUN];  // block of each run's first entry
+  __shared__ uint32_t s_wm[MAX_PAGE / 16];  // byte w: a block j >= 1 starts in word w
   __shared__ uint32_t s_tmp[ASM_NT / WAVE + 1];
   DBG_PHASE_K(3, 15);
   const uint32_t slot = blockIdx.x;
@@ -1313,15 +1314,18 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   }
   const uint32_t IS = 1u << lis, rvs = P.rvs;
   // (A) metadata + entry offsets (2 blocks per thread)
-  uint32_t cj[2], sum = 0;
+  uint32_t cj[2], oj[2], sum = 0;
+  if (threadIdx.x < MAX_PAGE / 16) s_wm[threadIdx.x] = 0;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const uint32_t j = threadIdx.x * 2 + q;
     cj[q] = 0;
+    oj[q] = 0;
     if (j < nb) {
       const uint32_t g = P.idx_base + b0 + j;
       cj[q] = idx_cnt[g];
-      s_off[j] = (uint32_t)(slots[g] - (uint64_t)p * page_size);
+      oj[q] = (uint32_t)(slots[g] - (uint64_t)p * page_size);
+      s_off[j] = oj[q];
       s_c[j] = cj[q];
       s_src[j] = idx_start[g];
     }
@@ -1342,7 +1346,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
     assemble_atomic(P, p, slot, b0, b1, idx_cnt, idx_start, sorted32, slots, pages, lis, page_size, s_pg);
   } else {
   __syncthreads();
-  // run table: block of each run's first entry
+  // run table: block of each run's first entry; word marks of the block starts
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const uint32_t j = threadIdx.x * 2 + q;
@@ -1350,8 +1354,16 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
       const uint32_t r0 = (s_est[j] + ASM_RUN - 1) / ASM_RUN, r1 = (s_est[j + 1] + ASM_RUN - 1) / ASM_RUN;
       for (uint32_t r = r0; r < r1; r++) s_rblk[r] = (uint16_t)j;
     }
+    if (j < nb && j > 0) reinterpret_cast<uint8_t*>(s_wm)[(oj[q] + 3) / 4] = 1;  // blocks >= 9 B apart
   }
   __syncthreads();
+  // block of word w (the block holding byte 4w) = block starts in words <= w: thread t
+  // owns words 4t..4t+3, so one exclusive scan of the per-thread mark counts
+  const uint32_t nwp = page_size / 4;
+  const uint32_t mw = 4 * threadIdx.x < nwp ? s_wm[threadIdx.x] : 0u;
+  uint32_t mtot;
+  const uint32_t jw0 = block_excl_scan<ASM_NT>((mw & 0xffu) + ((mw >> 8) & 0xffu) + ((mw >> 16) & 0xffu) + (mw >> 24),
+                                              s_tmp, &mtot);
   const uint32_t* base = sorted32 + P.e_first;
   const uint32_t nruns = (ne + ASM_RUN - 1) / ASM_RUN;
   // a run's entries: independent loads, all in flight together
@@ -1376,24 +1388,26 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   // the first run's loads are issued before the fill, so they land while it runs
   uint32_t ev0[ASM_RUN];
   if (threadIdx.x < nruns) load_run(threadIdx.x, ev0);
-  // (B) fill: word w, bytes 4w..4w+3
-  for (uint32_t w = threadIdx.x; w < page_size / 4; w += ASM_NT) {
-    uint32_t lo = 0, hi = nb;  // block holding byte 4w
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_off[mid] <= 4 * w) lo = mid; else hi = mid;
-    }
-    uint32_t j = lo, x = 0;
+  // (B) fill: thread t builds words 4t..4t+3 (bytes 16t..16t+15) and stores them at once
+  if (4 * threadIdx.x < nwp) {
+    uint32_t x4[4], jw = jw0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint32_t B = 4 * w + i;
-      if (j + 1 < nb && s_off[j + 1] <= B) j++;  // blocks are >= 9 bytes: at most one step
-      const uint32_t rel = B - s_off[j], c = s_c[j];
-      const uint32_t enc = (c + IS - 1) / 8 + 4;
-      const uint32_t byte = rel < 2 ? ((c >> (8 * rel)) & 0xffu) : (rel < 2 + enc ? 0xffu : 0u);
-      x |= byte << (8 * i);
+    for (int k = 0; k < 4; k++) {
+      jw += (mw >> (8 * k)) & 0xffu;
+      const uint32_t w = 4 * threadIdx.x + k;
+      uint32_t j = jw, x = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t B = 4 * w + i;
+        if (j + 1 < nb && s_off[j + 1] <= B) j++;  // blocks are >= 9 bytes: at most one step
+        const uint32_t rel = B - s_off[j], c = s_c[j];
+        const uint32_t enc = (c + IS - 1) / 8 + 4;
+        const uint32_t byte = rel < 2 ? ((c >> (8 * rel)) & 0xffu) : (rel < 2 + enc ? 0xffu : 0u);
+        x |= byte << (8 * i);
+      }
+      x4[k] = x;
     }
-    s_pg[w] = x;
+    reinterpret_cast<v4u*>(s_pg)[threadIdx.x] = v4u{x4[0], x4[1], x4[2], x4[3]};
   }
   if (threadIdx.x < 4) s_pg[page_size / 4 + threadIdx.x] = 0;
   __syncthreads();
