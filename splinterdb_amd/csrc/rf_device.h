@@ -120,6 +120,44 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_tmp,
   return r;
 }
 
+// In-place exclusive scan of x[k] over the elements j = k * NT + threadIdx.x (k-major
+// order), so the loads and stores around it are lane-consecutive (coalesced, no LDS bank
+// conflicts). s_w: PER * NT/64 + 1 words. Contains barriers: call from every thread.
+template <int NT, int PER>
+__device__ __forceinline__ void block_excl_scan_kmajor(uint32_t (&x)[PER], uint32_t* s_w, uint32_t* total) {
+  constexpr int NW = NT / WAVE, M = PER * NW, Q = (M + WAVE - 1) / WAVE;
+  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t inc = wave_incl_scan(x[k]);
+    if (lane == WAVE - 1) s_w[k * NW + w] = inc;
+    x[k] = inc - x[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < WAVE) {  // one wave scans the M wave totals in (k, wave) order
+    uint32_t v[Q], sum = 0;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int i = threadIdx.x * Q + q;
+      v[q] = i < M ? s_w[i] : 0u;
+      sum += v[q];
+    }
+    uint32_t e = wave_incl_scan(sum) - sum;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int i = threadIdx.x * Q + q;
+      if (i < M) s_w[i] = e;
+      e += v[q];
+    }
+    if (threadIdx.x == WAVE - 1) s_w[M] = e;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; k++) x[k] += s_w[k * NW + w];
+  *total = s_w[M];
+  __syncthreads();
+}
+
 // ---- unaligned little-endian reads from filter page bytes (4-byte aligned buffer) -------
 __device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* base, uint64_t byte_off) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(base) + (byte_off >> 2);

@@ -539,7 +539,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   constexpr int PER = SORT_CAP / SORT_NT;
   DBG_PHASE(15);
   __shared__ EntT s_b[SORT_CAP];
-  __shared__ uint32_t s_bin[MAX_BINS + 1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_bin[MAX_BINS + 1];
   __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
   __shared__ uint32_t s_fo[sizeof(EntT) == 8 ? MAX_IPC : 1];
   __shared__ uint32_t s_ho[sizeof(EntT) == 8 ? MAX_IPC : 1];
@@ -587,23 +587,34 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   }
   __syncthreads();
   DBG_PHASE(1);
-  // exclusive scan of bin counts (nbins <= MAX_BINS = 8 * SORT_NT)
+  // exclusive scan of bin counts (nbins <= MAX_BINS = 8 * SORT_NT): thread t owns bins
+  // [8t, 8t + 8), read and written as two 16-byte LDS accesses (8 scalar accesses strided
+  // by 8 words were 16-way bank conflicts)
   {
     constexpr int BPT = MAX_BINS / SORT_NT;
-    uint32_t bv[BPT], sum = 0;
+    static_assert(BPT == 8, "two 16-byte accesses per thread");
+    v4u* sb4 = reinterpret_cast<v4u*>(s_bin) + 2 * threadIdx.x;
+    const bool own = threadIdx.x * BPT < nbins;  // nbins is a power of two >= 8 or < 8
+    v4u a = own ? sb4[0] : v4u{0u, 0u, 0u, 0u}, b = own ? sb4[1] : v4u{0u, 0u, 0u, 0u};
+    if (own && nbins < BPT) {  // fewer than 8 bins: only the first nbins words are counts
+      uint32_t t8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int k = 0; k < BPT; k++) {
-      const uint32_t i = threadIdx.x * BPT + k;
-      bv[k] = i < nbins ? s_bin[i] : 0u;
-      sum += bv[k];
+      for (int k = 0; k < 8; k++) if ((uint32_t)k >= nbins) t8[k] = 0;
+      a = v4u{t8[0], t8[1], t8[2], t8[3]};
+      b = v4u{t8[4], t8[5], t8[6], t8[7]};
     }
+    const uint32_t sum = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
     uint32_t total;
     uint32_t run = block_excl_scan<SORT_NT>(sum, s_tmp, &total);
-#pragma unroll
-    for (int k = 0; k < BPT; k++) {
-      const uint32_t i = threadIdx.x * BPT + k;
-      if (i < nbins) s_bin[i] = run;
-      run += bv[k];
+    v4u ea, eb;
+    ea.x = run; run += a.x; ea.y = run; run += a.y; ea.z = run; run += a.z; ea.w = run; run += a.w;
+    eb.x = run; run += b.x; eb.y = run; run += b.y; eb.z = run; run += b.z; eb.w = run;
+    if (own && nbins >= BPT) {
+      sb4[0] = ea;
+      sb4[1] = eb;
+    } else if (own) {
+      const uint32_t e8[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
+      for (uint32_t k = 0; k < nbins; k++) s_bin[k] = e8[k];
     }
     if (threadIdx.x == 0) s_bin[nbins] = n;
   }
@@ -924,45 +935,6 @@ __device__ __forceinline__ uint32_t block_size(uint32_t c, uint32_t index_size, 
   return enc + 2 + rbs;
 }
 
-// Exclusive scan of x[k] over the elements j = k * NT + threadIdx.x (k-major order), so the
-// global loads and stores around it are lane-consecutive (coalesced). s_w: PER * NT/64 + 1
-// words. Contains barriers: call from every thread.
-template <int NT, int PER>
-__device__ __forceinline__ void block_excl_scan_kmajor(const uint32_t (&x)[PER], uint32_t (&out)[PER],
-                                                       uint32_t* s_w, uint32_t* total) {
-  constexpr int NW = NT / WAVE, M = PER * NW, Q = (M + WAVE - 1) / WAVE;
-  const int w = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
-  uint32_t inc[PER];
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    inc[k] = wave_incl_scan(x[k]);
-    if (lane == WAVE - 1) s_w[k * NW + w] = inc[k];
-  }
-  __syncthreads();
-  if (threadIdx.x < WAVE) {  // one wave scans the M wave totals in (k, wave) order
-    uint32_t v[Q], sum = 0;
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-      const int i = threadIdx.x * Q + q;
-      v[q] = i < M ? s_w[i] : 0u;
-      sum += v[q];
-    }
-    uint32_t e = wave_incl_scan(sum) - sum;
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-      const int i = threadIdx.x * Q + q;
-      if (i < M) s_w[i] = e;
-      e += v[q];
-    }
-    if (threadIdx.x == WAVE - 1) s_w[M] = e;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < PER; k++) out[k] = s_w[k * NW + w] + inc[k] - x[k];
-  *total = s_w[M];
-  __syncthreads();
-}
-
 constexpr uint32_t LAYOUT_LIST = 520;
 __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restrict__ plans,
                                                       const uint32_t* __restrict__ idx_cnt,
@@ -1006,12 +978,12 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
     }
   }
   if (err) atomicOr(&s_err, err);
-  uint32_t total, ex[PER];
-  block_excl_scan_kmajor<LAYOUT_NT, PER>(sz, ex, s_wt, &total);
+  uint32_t total;
+  block_excl_scan_kmajor<LAYOUT_NT, PER>(sz, s_wt, &total);  // sz becomes the exclusive prefix
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = k * LAYOUT_NT + threadIdx.x;
-    if (j < n) s_excl[j] = ex[k];
+    if (j < n) s_excl[j] = sz[k];
   }
   // the total at j == n: no thread owns it when n == MAX_INDICES
   if (threadIdx.x == 0) s_excl[n] = total;
@@ -1117,9 +1089,10 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   for (int k = 0; k < PER; k++) {
     const uint32_t j = k * LAYOUT_NT + threadIdx.x;
     mk[k] = j < n ? s_mark[j] : 0u;
+    pg[k] = mk[k];
   }
   uint32_t npages;
-  block_excl_scan_kmajor<LAYOUT_NT, PER>(mk, pg, s_wt, &npages);
+  block_excl_scan_kmajor<LAYOUT_NT, PER>(pg, s_wt, &npages);
   uint16_t* s_pstart = s_jB;  // reuse: page -> first block
 #pragma unroll
   for (int k = 0; k < PER; k++) {

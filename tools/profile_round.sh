@@ -23,5 +23,9 @@ timeout -k 10 400 python3 bench.py --pmc $O/pmc_$TAG.json > $O/bench_c2.json 2> 
 timeout -k 10 300 python3 bench.py --workload c3 --no-cpu-baseline --pmc none > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench c3 failed"; exit 1; }
 timeout -k 10 300 python3 bench.py --workload c4 --no-cpu-baseline --pmc none > $O/bench_c4.json 2> $O/bench_c4.err || { echo "bench c4 failed"; exit 1; }
 timeout -k 10 300 python3 bench.py --workload c5 --pmc none > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 failed"; exit 1; }
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-e2e --routed-probe --pmc none > $O/bench_c2_routed.json 2> $O/bench_c2_routed.err || { echo "bench routed failed"; exit 1; }
+for k in 1 2 3 4; do
+  timeout -k 10 100 python3 tools/phase_times.py $k > $O/phases_k$k.txt 2>&1 || { echo "phase times $k failed"; exit 1; }
+done
 timeout -k 10 100 ./tools/gather_bench > $O/gather_$TAG.txt 2>&1 || { echo "gather bench failed"; exit 1; }
 cat $O/bench_c2.json
