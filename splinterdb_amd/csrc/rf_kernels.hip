@@ -81,6 +81,16 @@ __device__ __forceinline__ uint32_t select64_fast(uint64_t x, uint32_t r) {
 }
 __device__ __forceinline__ uint64_t lowmask64(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
 
+// XCD-aware block -> work-item remap (bijective for any grid): the blocks that share an XCD
+// (b % 8, round-robin dispatch) take one contiguous eighth of the work items, so one XCD's
+// L2 sees one range of tiles / coarse buckets / pages / probes (MI355X_MICROARCH.md, XCD
+// L2): partial lines written by neighbouring items merge in that L2 instead of reaching
+// HBM as separate partial writes, and the next kernel finds the same range in the same L2.
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
+  const uint32_t q = nb / 8, r = nb % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
 // ======================================================================================
 // K1: hash + coarse-bucket histogram
 // ======================================================================================
@@ -323,7 +333,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   constexpr int PER = TILE_KEYS / SCAT_NT;
   constexpr int BPT = MAX_CB / SCAT_NT;
   DBG_PHASE_K(2, 15);
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's tiles share an XCD
   const FilterPlan& P = plans[tile_filter[t]];
   const uint32_t start = tile_start[t];
   const uint32_t count = min((uint32_t)TILE_KEYS, P.num_new - start);
@@ -2187,14 +2197,6 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
     }
   }
   return true;
-}
-
-// XCD-aware block -> chunk remap (bijective for any grid): the blocks that share an XCD
-// (b % 8, round-robin dispatch) process one contiguous eighth of the probe array, so an
-// XCD's L2 holds the images of the filters its probes hit (MI355X_MICROARCH.md, XCD L2).
-__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
-  const uint32_t q = nb / 8, r = nb % 8, xcd = b % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
 constexpr int PROBE_NT = 256;
