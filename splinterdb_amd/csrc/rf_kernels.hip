@@ -557,7 +557,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   __shared__ uint32_t s_big[BIG_LIST];  // bins over 8 entries (s_nbig may exceed the list)
   __shared__ uint32_t s_nbig;
   uint32_t* s_first = s_bin;  // compacted start of each index: reuses s_bin once bins are sorted
-  const uint32_t cb = blockIdx.x;
+  const uint32_t cb = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's buckets share an XCD (its partition's L2)
   const uint32_t f = cb_filter[cb];
   const FilterPlan& P = plans[f];
   const uint32_t n = cb_count[cb];
@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   __shared__ uint32_t s_wm[MAX_PAGE / 16];  // byte w: a block j >= 1 starts in word w
   __shared__ uint32_t s_tmp[ASM_NT / WAVE + 1];
   DBG_PHASE_K(3, 15);
-  const uint32_t slot = blockIdx.x;
+  const uint32_t slot = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's pages share an XCD
   const uint32_t f = pg_filter[slot];
   const FilterPlan& P = plans[f];
   const uint32_t p = slot - P.page_base;
