@@ -200,7 +200,7 @@ def main():
         else:
             # key-range shard of this rank: ids [key_begin, key_end), filter f = ids of its range
             keys = K.seq_keys_torch(me.key_begin, N, 24, dev)
-            fid = (torch.arange(N, device=dev, dtype=torch.int64) // n).to(torch.int32)
+            counts = [n] * F  # probes grouped by filter: filter f's keys probe filter f
             P = N
         found = torch.empty(P, dtype=torch.int64, device=dev)
     stream.synchronize()
@@ -215,7 +215,7 @@ def main():
             batch.probe_var_keys(p_bytes, p_offs, fid, P, found, stream=stream.cuda_stream)
         else:
             batch.build_keys(keys, 24, stream=stream.cuda_stream)
-            batch.probe_keys(keys, 24, fid, N, found, stream=stream.cuda_stream)
+            batch.probe_keys_runs(keys, 24, counts, found, stream=stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -305,7 +305,7 @@ def main():
                 with torch.cuda.stream(stream):
                     d_h.copy_(hh, non_blocking=True)
                 batch.build_hashes(d_h, stream=stream.cuda_stream)
-                batch.probe_hashes(d_h, fid, N, found, stream=stream.cuda_stream)
+                batch.probe_hashes_runs(d_h, counts, found, stream=stream.cuda_stream)
                 with torch.cuda.stream(stream):
                     hfound.copy_(found, non_blocking=True)
                 for f in range(F):

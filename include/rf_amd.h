@@ -94,6 +94,13 @@ int rf_amd_batch_probe_var_keys(rf_amd_batch *b, const uint8_t *d_bytes,
 int rf_amd_batch_probe_hashes(rf_amd_batch *b, const uint32_t *d_hashes,
                               const uint32_t *d_filter_id, uint64_t n, uint64_t *d_found,
                               void *stream);
+/* probes grouped by filter, in filter order: filter f's h_counts[f] probes follow those of
+ * filters < f (one batch of routing_filter_lookup calls per filter). The filter of each
+ * probe follows from its position: no per-probe filter id is read. */
+int rf_amd_batch_probe_keys_runs(rf_amd_batch *b, const void *d_keys, uint32_t key_len,
+                                 const uint64_t *h_counts, uint64_t *d_found, void *stream);
+int rf_amd_batch_probe_hashes_runs(rf_amd_batch *b, const uint32_t *d_hashes, const uint64_t *h_counts,
+                                   uint64_t *d_found, void *stream);
 
 /* synchronising accessors */
 int rf_amd_batch_info(rf_amd_batch *b, uint32_t f, rf_amd_filter_info *out);

@@ -80,6 +80,8 @@ struct rf_amd_batch {
   uint64_t NL = 0;         // probe lines (64 B each)
   bool plines_needed = false;  // some filter's lines come from k_plines
   uint32_t line_lmax = 0;  // max probe lines per index
+  DevBuf d_runs;                    // probe run bounds (rf_amd_batch_probe_*_runs)
+  std::vector<uint64_t> runs_host;  // their last uploaded value
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
       d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill;
@@ -459,13 +461,15 @@ extern "C" int rf_amd_batch_build_hashes(rf_amd_batch* b, const uint32_t* d_hash
 }
 
 static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
-                    const uint32_t* fid, uint64_t n, uint64_t* found, void* stream) {
+                    const uint32_t* fid, uint64_t n, uint64_t* found, void* stream,
+                    const uint64_t* d_runs = nullptr) {
   if (!b || !b->built) return fail(RF_AMD_EINVAL, "probe on an unbuilt batch");
-  if (n && (!in0 || !fid || !found)) return fail(RF_AMD_EINVAL, "null probe buffer");
+  if (n && (!in0 || !(fid || d_runs) || !found)) return fail(RF_AMD_EINVAL, "null probe buffer");
   HIPCHK(hipSetDevice(b->eng->device));
   hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
   (void)hipGetLastError();
   LaunchArgs a = make_args(b, st);
+  a.probe_runs = d_runs;
   a.ablate = g_probe_ablate & 0xff;
   a.occ = (g_probe_ablate >> 8) & 0xff;
   a.ppl = (g_probe_ablate >> 16) & 0xff;
@@ -487,6 +491,38 @@ extern "C" int rf_amd_batch_probe_var_keys(rf_amd_batch* b, const uint8_t* d_byt
 extern "C" int rf_amd_batch_probe_hashes(rf_amd_batch* b, const uint32_t* d_hashes, const uint32_t* d_filter_id,
                                          uint64_t n, uint64_t* d_found, void* stream) {
   return do_probe(b, IN_HASH, d_hashes, nullptr, 4, d_filter_id, n, d_found, stream);
+}
+
+// Probes grouped by filter (filter f's h_counts[f] probes follow filter f-1's): the filter of
+// a probe comes from its position, so no per-probe filter id is read. The run bounds are
+// uploaded when they change.
+static int probe_runs(rf_amd_batch* b, int kind, const void* in0, uint32_t key_len, const uint64_t* h_counts,
+                      uint64_t* d_found, void* stream) {
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "probe on an unbuilt batch");
+  if (!h_counts) return fail(RF_AMD_EINVAL, "null counts");
+  std::vector<uint64_t> runs(b->F + 1, 0);
+  for (uint32_t f = 0; f < b->F; f++) runs[f + 1] = runs[f] + h_counts[f];
+  const uint64_t n = runs[b->F];
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(b->eng->device));
+  if (runs != b->runs_host) {
+    if (!b->d_runs.p && b->d_runs.alloc(8ull * (b->F + 1))) return RF_AMD_ENOMEM;
+    hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+    HIPCHK(hipStreamSynchronize(st));  // earlier probes may still read the old bounds
+    HIPCHK(hipMemcpy(b->d_runs.p, runs.data(), 8ull * (b->F + 1), hipMemcpyHostToDevice));
+    b->runs_host = runs;
+  }
+  return do_probe(b, kind, in0, nullptr, key_len, nullptr, n, d_found, stream, b->d_runs.as<uint64_t>());
+}
+
+extern "C" int rf_amd_batch_probe_keys_runs(rf_amd_batch* b, const void* d_keys, uint32_t key_len,
+                                            const uint64_t* h_counts, uint64_t* d_found, void* stream) {
+  if (key_len == 0) return fail(RF_AMD_EINVAL, "key_len 0");
+  return probe_runs(b, fixed_kind(d_keys, key_len), d_keys, key_len, h_counts, d_found, stream);
+}
+extern "C" int rf_amd_batch_probe_hashes_runs(rf_amd_batch* b, const uint32_t* d_hashes, const uint64_t* h_counts,
+                                              uint64_t* d_found, void* stream) {
+  return probe_runs(b, IN_HASH, d_hashes, 4, h_counts, d_found, stream);
 }
 
 // Diagnostic: low byte 1 = hash only, 2 = + probe record; 0 = normal probe. Bits 8+: cap

@@ -2209,6 +2209,21 @@ constexpr int PROBE_PPL = 1;  // probes per lane (production)
 // OCC_LDS > 0 pads LDS to cap workgroups per CU (occupancy experiments; 0 = none).
 // A lane handles PPL probes (i, i + PROBE_NT, ...): all their key loads, then all their
 // line loads, then the decodes -- PPL independent random line fetches in flight per lane.
+// filter of probe i when the probes come as per-filter runs: runs[f] <= i < runs[f + 1].
+// The search runs once per wave on its first probe (wave-uniform: scalar loads); lanes past
+// a run boundary step forward.
+__device__ __forceinline__ uint32_t run_filter(const uint64_t* __restrict__ runs, uint32_t nf, uint64_t i) {
+  const uint64_t wf = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(i >> 32)) << 32) |
+                      __builtin_amdgcn_readfirstlane((uint32_t)i);
+  uint32_t lo = 0, hi = nf;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (runs[mid] <= wf) lo = mid; else hi = mid;
+  }
+  while (lo + 1 < nf && runs[lo + 1] <= i) lo++;
+  return lo;
+}
+
 template <int KIND, int OCC_LDS = 0, int PPL = 1>
 __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
                                                     const FilterPlan* __restrict__ plans,
@@ -2217,7 +2232,8 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
                                                     const uint4* __restrict__ lines,
                                                     const void* __restrict__ in0,
                                                     const uint64_t* __restrict__ offs, uint32_t key_len,
-                                                    const uint32_t* __restrict__ filter_id, uint64_t n,
+                                                    const uint32_t* __restrict__ filter_id,
+                                                    const uint64_t* __restrict__ runs, uint64_t n,
                                                     uint64_t* __restrict__ found, uint32_t fp_size,
                                                     uint32_t seed, uint32_t lis, uint32_t page_size,
                                                     uint32_t num_filters, uint32_t ablate) {
@@ -2238,7 +2254,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     fid[0] = 0xffffffffu;
     h[0] = 0;
     if (wf < n) {  // uniform per wave
-      if (i0 < n) fid[0] = __builtin_nontemporal_load(filter_id + i0);
+      if (i0 < n) fid[0] = runs ? run_filter(runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
       if (((uintptr_t)in0 & 15) == 0) {
         v4u* sw = s_keys[threadIdx.x / WAVE];
         const uint32_t bytes = (uint32_t)min<uint64_t>(WAVE, n - wf) * 24;
@@ -2279,7 +2295,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
         fid[q] = (uint32_t)(pr >> 32);
         h[q] = (uint32_t)pr;
       } else {
-        fid[q] = __builtin_nontemporal_load(filter_id + i);
+        fid[q] = runs ? run_filter(runs, num_filters, i) : __builtin_nontemporal_load(filter_id + i);
         h[q] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
       }
     }
@@ -2480,7 +2496,7 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
   const int ppl = a.ppl ? (int)a.ppl : PROBE_PPL;
   dim3 g((uint32_t)((n + PROBE_NT * ppl - 1) / (PROBE_NT * ppl))), b(PROBE_NT);
   REC(EV_P_START);
-#define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
+#define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
   if (kind == IN_KEYS24 && (a.occ || a.ppl)) {  // experiment variants: waves/SIMD cap, probes per lane
     const int o = a.occ ? (int)a.occ : 8;
     if (ppl == 2) {

@@ -115,6 +115,7 @@ struct LaunchArgs {
   uint32_t ablate;  // probe diagnostics (0 = normal)
   uint32_t occ;     // probe occupancy experiment (0 = normal)
   uint32_t ppl;     // probe probes-per-lane experiment (0 = production)
+  const uint64_t* probe_runs;  // probes grouped by filter: runs[f] <= i < runs[f+1] (nullptr: per-probe ids)
   void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)
 };
 

@@ -32,6 +32,7 @@ EXPORTED = [
     "rf_amd_batch_create", "rf_amd_batch_destroy", "rf_amd_batch_build_keys",
     "rf_amd_batch_build_var_keys", "rf_amd_batch_build_hashes", "rf_amd_batch_probe_keys",
     "rf_amd_batch_probe_var_keys", "rf_amd_batch_probe_hashes", "rf_amd_batch_info",
+    "rf_amd_batch_probe_keys_runs", "rf_amd_batch_probe_hashes_runs",
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
     "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_batch_timings_back", "rf_amd_debug_probe_ablate",
     "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer",
@@ -103,6 +104,8 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_probe_keys.argtypes = [vp, vp, u32, vp, u64, vp, vp]
     L.rf_amd_batch_probe_var_keys.argtypes = [vp, vp, vp, vp, u64, vp, vp]
     L.rf_amd_batch_probe_hashes.argtypes = [vp, vp, vp, u64, vp, vp]
+    L.rf_amd_batch_probe_keys_runs.argtypes = [vp, vp, u32, ctypes.POINTER(u64), vp, vp]
+    L.rf_amd_batch_probe_hashes_runs.argtypes = [vp, vp, ctypes.POINTER(u64), vp, vp]
     L.rf_amd_batch_info.argtypes = [vp, u32, ctypes.POINTER(RfFilterInfo)]
     L.rf_amd_batch_read_image.argtypes = [vp, u32, vp, u64, vp, u32]
     L.rf_amd_batch_read_image_async.argtypes = [vp, u32, vp, u64, vp, u32, vp]
@@ -606,6 +609,17 @@ class FilterBatch:
     def probe_hashes(self, d_hashes, d_filter_id, n, d_found, stream=None):
         _check(load_library().rf_amd_batch_probe_hashes(self.h, _dptr(d_hashes), _dptr(d_filter_id),
                                                         n, _dptr(d_found), _stream(stream)))
+
+    def probe_keys_runs(self, d_keys, key_len, counts, d_found, stream=None):
+        """Probes grouped by filter: counts[f] probes of filter f, in filter order."""
+        c = (ctypes.c_uint64 * self.F)(*[int(x) for x in counts])
+        _check(load_library().rf_amd_batch_probe_keys_runs(self.h, _dptr(d_keys), key_len, c, _dptr(d_found),
+                                                           _stream(stream)))
+
+    def probe_hashes_runs(self, d_hashes, counts, d_found, stream=None):
+        c = (ctypes.c_uint64 * self.F)(*[int(x) for x in counts])
+        _check(load_library().rf_amd_batch_probe_hashes_runs(self.h, _dptr(d_hashes), c, _dptr(d_found),
+                                                             _stream(stream)))
 
     def probe_pairs(self, d_pairs, n, d_found, stream=None):
         """Probes given as (local filter id << 32 | hash) u64 pairs (routed probes, route.py)."""

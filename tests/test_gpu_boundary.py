@@ -165,3 +165,38 @@ def test_hash_keys_match_oracle(oracle):
     E.hash_var_keys(E.routing_config_init(), dev(d), dev(o), 30_000, out)
     torch.cuda.synchronize()
     assert (out.cpu().numpy().view(np.uint32) == oracle.hash_var(d, o)).all()
+
+
+@pytest.mark.gpu
+def test_probe_runs_equal_per_probe_filter_ids(oracle):
+    """rf_amd_batch_probe_{keys,hashes}_runs (filter from the probe's position) must equal the
+    per-probe filter-id probe, including empty runs and runs longer than the filter."""
+    from splinterdb_amd import keys as K
+    cfg = E.routing_config_init()
+    sizes, vals = [20000, 1, 70000, 3000, 9], [1, 0, 4, 2, 7]
+    b = E.FilterBatch(cfg, sizes, vals)
+    b.build_keys(torch.from_numpy(K.seq_keys(0, sum(sizes)).reshape(-1)).to("cuda:0"), 24)
+    rng = np.random.default_rng(3)
+    counts = [5000, 0, 100000, 17, 4099]
+    ids = rng.integers(0, 2 * sum(sizes), size=sum(counts)).astype(np.uint64)
+    fid = np.repeat(np.arange(len(counts), dtype=np.uint32), counts)
+    keys = torch.from_numpy(K.ids_keys(ids).reshape(-1)).to("cuda:0")
+    P = len(ids)
+    f_ids = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    f_runs = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b.probe_keys(keys, 24, torch.from_numpy(fid.view(np.int32)).to("cuda:0"), P, f_ids)
+    b.probe_keys_runs(keys, 24, counts, f_runs)
+    torch.cuda.synchronize()
+    assert torch.equal(f_ids, f_runs)
+    h = oracle.hash_fixed(K.ids_keys(ids).reshape(-1), 24)
+    f_h = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b.probe_hashes_runs(torch.from_numpy(h.view(np.int32)).to("cuda:0"), counts, f_h)
+    counts2 = [1, 1, 1, 1, P - 4]  # a second shape: the bounds are re-uploaded
+    f_r2 = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b.probe_keys_runs(keys, 24, counts2, f_r2)
+    fid2 = np.repeat(np.arange(5, dtype=np.uint32), counts2)
+    f_i2 = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b.probe_keys(keys, 24, torch.from_numpy(fid2.view(np.int32)).to("cuda:0"), P, f_i2)
+    torch.cuda.synchronize()
+    assert torch.equal(f_ids, f_h)
+    assert torch.equal(f_r2, f_i2)
