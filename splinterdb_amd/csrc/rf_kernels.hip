@@ -1354,6 +1354,18 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
     const uint32_t q0 = r * ASM_RUN, q1 = min(q0 + ASM_RUN, ne);
     uint32_t j = s_rblk[r], ej = s_est[j + 1];
     const uint32_t* src = base + ((int64_t)s_src[j] - (int64_t)s_est[j]);  // src[q] = entry q
+    if (q1 == q0 + ASM_RUN && q1 <= ej) {
+      // the whole run inside block j: 16-byte loads (a quarter of the cache-line requests of
+      // 16 dword loads strided by the run); gfx950 accepts unaligned global addresses
+      static_assert(ASM_RUN % 4 == 0, "runs of whole 16-byte loads");
+#pragma unroll
+      for (uint32_t i = 0; i < ASM_RUN; i += 4) {
+        v4u x;
+        __builtin_memcpy(&x, src + q0 + i, 16);
+        ev[i] = x.x; ev[i + 1] = x.y; ev[i + 2] = x.z; ev[i + 3] = x.w;
+      }
+      return;
+    }
 #pragma unroll
     for (uint32_t i = 0; i < ASM_RUN; i++) {
       const uint32_t q = q0 + i;
