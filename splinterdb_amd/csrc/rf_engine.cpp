@@ -327,6 +327,14 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     return fail(RF_AMD_ENOMEM, "device allocation failed");
   }
   hipStream_t st = e->stream;
+  if (const char* pz = getenv("RF_AMD_POISON")) {
+    // test hook: fill every work buffer with a pattern, so that a kernel reading memory it
+    // did not write in this build cannot pass the parity tests by reading stale results
+    const int v = atoi(pz) & 0xff;
+    for (DevBuf* d : {&b->d_ent, &b->d_part, &b->d_sorted, &b->d_cb_start, &b->d_idx_cnt, &b->d_idx_start,
+                      &b->d_slots, &b->d_lines, &b->d_page_first, &b->d_pages, &b->d_first_old, &b->d_has_old})
+      if (d->p) HIPCHK(hipMemsetAsync(d->p, v, d->n, st));
+  }
 #define UP(buf, vec) \
   if (!(vec).empty()) HIPCHK(hipMemcpyAsync(buf.p, (vec).data(), sizeof((vec)[0]) * (vec).size(), hipMemcpyHostToDevice, st))
   UP(b->d_plans, b->plans);
