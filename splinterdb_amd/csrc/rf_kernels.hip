@@ -572,21 +572,25 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   const uint32_t nbins = 1u << P.bbits;
   const uint32_t bmask = nbins - 1;
   const uint32_t ipc = 1u << (P.bbits - lis), ish = lis + P.rvs;
+  // the bucket's entry loads go out first (clamped, branch-free) and land while the bin
+  // counters are cleared; the barrier after the clearing orders only LDS (a full
+  // __syncthreads would also wait for the loads)
+  EntT v[PER];
+  uint32_t r[PER];
+  const EntT* src = part + P.e_first + c.cb_rel;
+  const uint32_t nm1 = n ? n - 1 : 0u;
+#pragma unroll
+  for (int k = 0; k < PER; k++) v[k] = src[min(threadIdx.x + k * SORT_NT, nm1)];
   for (uint32_t i = threadIdx.x; i <= nbins; i += SORT_NT) s_bin[i] = 0;
   if constexpr (sizeof(EntT) == 8) {
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
   if (threadIdx.x == 0) s_nbig = 0;
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   DBG_PHASE(0);
-  // load + per-bin rank (bin = filter bucket within the coarse bucket)
-  EntT v[PER];
-  uint32_t r[PER];
-  const EntT* src = part + P.e_first + c.cb_rel;
-  // loads first (clamped, branch-free), then the LDS ranking (see k_hash_scatter)
-  const uint32_t nm1 = n ? n - 1 : 0u;
-#pragma unroll
-  for (int k = 0; k < PER; k++) v[k] = src[min(threadIdx.x + k * SORT_NT, nm1)];
+  // per-bin rank (bin = filter bucket within the coarse bucket)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     if (threadIdx.x + k * SORT_NT < n) {
