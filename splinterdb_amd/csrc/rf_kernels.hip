@@ -296,12 +296,21 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
 // 3 = page assembly (K6), 4 = layout (K5).
 __device__ uint64_t* g_dbg_ts = nullptr;
 __device__ uint32_t g_dbg_kid = 0;
+// Compiled in only for the diagnostics library (RF_PHASE_STAMPS, build.py stamps=True):
+// reading the stamp buffer pointer is a vector load whose wait (vmcnt(0)) would also wait
+// for every load or atomic the kernel has in flight at that point.
+#ifdef RF_PHASE_STAMPS
 #define DBG_PHASE_K(kid, k)                                                  \
   do {                                                                       \
     uint64_t* _ts = g_dbg_ts;                                                \
     if (_ts && g_dbg_kid == (kid) && threadIdx.x == 0)                       \
       _ts[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();             \
   } while (0)
+#else
+#define DBG_PHASE_K(kid, k) \
+  do {                      \
+  } while (0)
+#endif
 #define DBG_PHASE(k) DBG_PHASE_K(1, k)
 
 extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid) {

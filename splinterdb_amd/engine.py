@@ -83,12 +83,13 @@ def load_library(build_if_missing=True):
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        if not build_if_missing:
-            raise PlatformStatusError(STATUS_NO_DEVICE, f"{LIB_PATH} missing (run build)")
+    path = os.environ.get("RF_AMD_LIB", LIB_PATH)  # e.g. the phase-stamp diagnostics build
+    if not os.path.exists(path):
+        if not build_if_missing or path != LIB_PATH:
+            raise PlatformStatusError(STATUS_NO_DEVICE, f"{path} missing (run build)")
         from . import build as _b
         _b.build()
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     L.rf_amd_last_error.restype = ctypes.c_char_p
     L.rf_amd_engine_create.argtypes = [i32, ctypes.POINTER(vp)]

@@ -7,6 +7,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from splinterdb_amd import build as B  # noqa: E402
+
+os.environ["RF_AMD_LIB"] = B.LIB_STAMPS  # stamps are compiled only into this build
 from splinterdb_amd import engine as E  # noqa: E402
 from splinterdb_amd import keys as K  # noqa: E402
 
