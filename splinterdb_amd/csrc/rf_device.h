@@ -64,6 +64,62 @@ __device__ __forceinline__ uint32_t xxh32_words(const uint32_t* p, uint32_t len,
 // Arbitrary alignment: gfx950 global loads accept unaligned addresses, so each 16-byte
 // stripe is ONE dwordx4 load (memcpy lets the compiler emit it) and every load stays inside
 // the key's own bytes.
+__device__ __forceinline__ uint32_t pick4u(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return q == 0 ? a : q == 1 ? b : q == 2 ? c : d;
+}
+
+__device__ __forceinline__ uint32_t xxh32_unaligned(const uint8_t* p, uint32_t len, uint32_t seed);
+
+// One key per lane with nothing else in flight (probes, k_hash): for keys of 16..128 bytes
+// every load of the key is issued before any is used; other lengths take xxh32_unaligned.
+// (The partition keeps the stripe loop: it hashes 8 keys per lane at once, and the extra
+// registers cost it more than the loop's waits.)
+__device__ __forceinline__ uint32_t xxh32_unaligned_prefetch(const uint8_t* p, uint32_t len, uint32_t seed) {
+  constexpr uint32_t MS = 8;
+  if (len >= 16 && len <= 16 * MS) {
+    // Every load of the key is issued before any is used (a stripe loop would wait for
+    // each stripe in turn): the full 16-byte stripes, and the key's last 16 bytes, which
+    // hold the tail (len % 16 bytes) at their end. All loads stay inside the key.
+    const uint32_t ns = len / 16;
+    uint4 st[MS];
+#pragma unroll
+    for (uint32_t s = 0; s < MS; s++)
+      if (s < ns) __builtin_memcpy(&st[s], p + 16 * s, 16);
+    uint4 tl;
+    __builtin_memcpy(&tl, p + len - 16, 16);
+    uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+#pragma unroll
+    for (uint32_t s = 0; s < MS; s++)
+      if (s < ns) {
+        v1 = xround(v1, st[s].x); v2 = xround(v2, st[s].y); v3 = xround(v3, st[s].z); v4 = xround(v4, st[s].w);
+      }
+    uint32_t h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18) + len;
+    const uint32_t r = len - 16 * ns;  // tail bytes, at offsets [16 - r, 16) of tl
+    // 4 bytes of tl from byte offset o (o <= 12)
+    auto word_at = [&](uint32_t o) -> uint32_t {
+      const uint32_t q = o >> 2, sh = (o & 3) * 8;
+      const uint32_t lo = pick4u(q, tl.x, tl.y, tl.z, tl.w), hi = pick4u(q, tl.y, tl.z, tl.w, 0u);
+      return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+    };
+    uint32_t o = 16 - r;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++)
+      if (o + 4 <= 16) {
+        h = rotl32(h + word_at(o) * XP3, 17) * XP4;
+        o += 4;
+      }
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++)
+      if (o < 16) {
+        const uint32_t q = o >> 2, sh = (o & 3) * 8;
+        h = rotl32(h + ((pick4u(q, tl.x, tl.y, tl.z, tl.w) >> sh) & 0xffu) * XP5, 11) * XP1;
+        o++;
+      }
+    return xavalanche(h);
+  }
+  return xxh32_unaligned(p, len, seed);
+}
+
 __device__ __forceinline__ uint32_t xxh32_unaligned(const uint8_t* p, uint32_t len, uint32_t seed) {
   uint32_t h, i = 0;
   if (len >= 16) {

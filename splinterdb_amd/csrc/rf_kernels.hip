@@ -59,10 +59,12 @@ __device__ __forceinline__ uint32_t hash_key(const void* __restrict__ in0, const
     return xxh32_words(reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(in0) + k * key_len),
                        key_len, seed);
   } else if constexpr (KIND == IN_KEYS_B) {
-    return xxh32_unaligned(static_cast<const uint8_t*>(in0) + k * key_len, key_len, seed);
+    const uint8_t* kp = static_cast<const uint8_t*>(in0) + k * key_len;
+    return NT ? xxh32_unaligned_prefetch(kp, key_len, seed) : xxh32_unaligned(kp, key_len, seed);
   } else if constexpr (KIND == IN_VAR) {
     const uint64_t o0 = offs[k], o1 = offs[k + 1];
-    return xxh32_unaligned(static_cast<const uint8_t*>(in0) + o0, (uint32_t)(o1 - o0), seed);
+    const uint8_t* kp = static_cast<const uint8_t*>(in0) + o0;
+    return NT ? xxh32_unaligned_prefetch(kp, (uint32_t)(o1 - o0), seed) : xxh32_unaligned(kp, (uint32_t)(o1 - o0), seed);
   } else {  // IN_HASH
     if constexpr (NT) return __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + k);
     else return static_cast<const uint32_t*>(in0)[k];
