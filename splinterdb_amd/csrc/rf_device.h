@@ -143,6 +143,116 @@ __device__ __forceinline__ uint32_t xxh32_unaligned(const uint8_t* p, uint32_t l
   return xavalanche(h);
 }
 
+// XXH32 of `len` bytes at byte offset `boff` of an LDS word array (any alignment): each
+// little-endian word is funnel-shifted out of two aligned LDS words (v_alignbyte_b32).
+// Reads up to two words past the key's last byte: the caller pads the array.
+__device__ __forceinline__ uint32_t xxh32_lds(const uint32_t* sw, uint32_t boff, uint32_t len, uint32_t seed) {
+  const uint32_t* p = sw + (boff >> 2);
+  const uint32_t sh = boff & 3;
+  auto word = [&](uint32_t i) -> uint32_t { return __builtin_amdgcn_alignbyte(p[i + 1], p[i], sh); };
+  uint32_t h, i = 0;
+  if (len >= 16) {
+    uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+    const uint32_t ns = len >> 4;
+    for (uint32_t s = 0; s < ns; s++) {
+      v1 = xround(v1, word(4 * s)); v2 = xround(v2, word(4 * s + 1));
+      v3 = xround(v3, word(4 * s + 2)); v4 = xround(v4, word(4 * s + 3));
+    }
+    i = 4 * ns;
+    h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+  } else {
+    h = seed + XP5;
+  }
+  h += len;
+  const uint32_t nw = len >> 2;
+  for (; i < nw; i++) h = rotl32(h + word(i) * XP3, 17) * XP4;
+  if (len & 3) {
+    uint32_t w = word(nw);
+    for (uint32_t b = 0; b < (len & 3); b++) {
+      h = rotl32(h + (w & 0xffu) * XP5, 11) * XP1;
+      w >>= 8;
+    }
+  }
+  return xavalanche(h);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t lane) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), lane) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+}
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Variable-length keys, one per lane, hashed from a wave-private LDS window of CAP bytes
+// (CAP a multiple of 16; `sw` holds CAP/4 + 2 words, 16-byte aligned). A wave's keys are
+// contiguous in the key buffer (offsets increase with the key number), so the window is
+// filled by coalesced 16-byte loads of the whole byte range -- where one unaligned load
+// per lane per stripe touches up to 64 cache lines per instruction -- and each lane then
+// reads its key from LDS. The window is 16-byte aligned in the address space, so its
+// loads never leave the 4 KiB pages that hold the keys. [*win0, *win1) is the staged
+// address range, kept across calls for keys that continue the same byte stream; a key
+// longer than CAP - 15 bytes is hashed straight from global memory.
+template <uint32_t CAP, bool NT>
+__device__ __forceinline__ uint32_t wave_hash_var(const uint8_t* keys, uint64_t o0, uint64_t o1, bool valid,
+                                                  uint32_t* sw, uint32_t seed, uint64_t* win0,
+                                                  uint64_t* win1) {
+  static_assert(CAP % 16 == 0, "window is whole 16-byte chunks");
+  constexpr uint32_t IT = (CAP / 16 + WAVE - 1) / WAVE;
+  typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t kb = (uint64_t)(uintptr_t)keys;
+  const uint64_t vm = __ballot(valid);
+  if (!vm) return 0;
+  const uint64_t aend = (kb + readlane64(o1, 63 - __builtin_clzll(vm)) + 15) & ~15ull;
+  uint32_t h = 0;
+  bool pending = valid;
+  for (;;) {
+    if (pending && kb + o0 >= *win0 && kb + o1 <= *win1) {
+      h = xxh32_lds(sw, (uint32_t)(kb + o0 - *win0), (uint32_t)(o1 - o0), seed);
+      pending = false;
+    }
+    const uint64_t m = __ballot(pending);
+    if (!m) break;
+    const uint32_t first = __builtin_ctzll(m);
+    const uint64_t a0 = (kb + readlane64(o0, first)) & ~15ull;
+    const uint64_t a1 = min(aend, a0 + CAP);
+    if (lane == first && kb + o1 > a1) {  // longer than the window: straight from HBM
+      h = xxh32_unaligned(keys + o0, (uint32_t)(o1 - o0), seed);
+      pending = false;
+    }
+    wave_sync_lds();  // every lane's reads of the old window are done
+    const uint32_t n16 = (uint32_t)(a1 - a0) / 16;
+    const v4* src = reinterpret_cast<const v4*>((uintptr_t)a0);
+    // GRP loads in flight per lane at a time (16 B each): 4 keeps the partition's 8 KiB
+    // window within its register budget
+    constexpr uint32_t GRP = IT < 4 ? IT : 4;
+#pragma unroll
+    for (uint32_t g = 0; g < IT; g += GRP) {
+      v4 t[GRP];
+#pragma unroll
+      for (uint32_t it = 0; it < GRP; it++) {
+        const uint32_t j = lane + (g + it) * WAVE;
+        if (j < n16) {
+          if constexpr (NT) t[it] = __builtin_nontemporal_load(src + j);
+          else t[it] = src[j];
+        }
+      }
+#pragma unroll
+      for (uint32_t it = 0; it < GRP; it++) {
+        const uint32_t j = lane + (g + it) * WAVE;
+        if (j < n16) reinterpret_cast<v4*>(sw)[j] = t[it];
+      }
+    }
+    wave_sync_lds();
+    *win0 = a0;
+    *win1 = a1;
+  }
+  return h;
+}
+
 // ---- scans ------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   const int lane = threadIdx.x & (WAVE - 1);

@@ -329,7 +329,7 @@ extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid) {
 // -> scatter pipeline (K1, K2, K3 gated on *spill) then rebuilds the partition.
 // ======================================================================================
 template <int KIND>
-__global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __restrict__ plans,
+__global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_hash_scatter(const FilterPlan* __restrict__ plans,
                                                           const uint32_t* __restrict__ tile_filter,
                                                           const uint32_t* __restrict__ tile_start,
                                                           const void* __restrict__ in0,
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
                                                           uint32_t* __restrict__ part,
                                                           uint32_t* __restrict__ cb_fill,
                                                           uint32_t* __restrict__ spill) {
-  __shared__ uint32_t s_stage[TILE_KEYS];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[TILE_KEYS];
   __shared__ uint32_t s_off[MAX_CB];  // local counts -> local starts -> (global slot - local start)
   __shared__ uint32_t s_tmp[SCAT_NT / WAVE + 1];
   constexpr int PER = TILE_KEYS / SCAT_NT;
@@ -362,6 +362,15 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   // compiler cannot hoist every key of the tile into registers (236 VGPRs, 2 waves/SIMD)
   constexpr int HASH_CHUNK = 8;
   uint32_t dep = 0;
+  // key j of the tile handled by this thread's k-th slot: strided across the block, except
+  // for variable-length keys, where a wave takes 64 * PER consecutive keys (one byte stream)
+  auto key_of = [&](int k) -> uint32_t {
+    if constexpr (KIND == IN_VAR) return (threadIdx.x & ~(WAVE - 1)) * PER + k * WAVE + (threadIdx.x & (WAVE - 1));
+    else return threadIdx.x + k * SCAT_NT;
+  };
+  constexpr uint32_t VWIN = (TILE_KEYS / (SCAT_NT / WAVE)) * 4 - 16;  // bytes (s_stage slice - pad)
+  uint32_t* s_vwin = s_stage + (threadIdx.x / WAVE) * (TILE_KEYS / (SCAT_NT / WAVE));
+  uint64_t vw0 = 0, vw1 = 0;
 #pragma unroll
   for (int k0 = 0; k0 < PER; k0 += HASH_CHUNK) {
     if constexpr (KIND == IN_KEYS24) {
@@ -389,6 +398,19 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
         const uint32_t h = xxh32_24(w, seed);
         v[k0 + k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
       }
+    } else if constexpr (KIND == IN_VAR) {
+      // variable-length keys: this wave's keys [wave * 64 * PER, +64 * PER) are one
+      // contiguous byte stream, read into the wave's 8 KiB slice of s_stage (unused until
+      // the ranking) with coalesced 16-byte loads and hashed from LDS (wave_hash_var).
+      // The window persists across k: a key already staged is hashed without a reload.
+#pragma unroll
+      for (int k = 0; k < HASH_CHUNK; k++) {
+        const uint32_t j = min(key_of(k0 + k), count - 1);
+        const uint64_t o0 = offs[P.key_first + start + j], o1 = offs[P.key_first + start + j + 1];
+        const uint32_t h = wave_hash_var<VWIN, false>(static_cast<const uint8_t*>(in0), o0, o1,
+                                                      key_of(k0 + k) < count, s_vwin, seed, &vw0, &vw1);
+        v[k0 + k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+      }
     } else {
 #pragma unroll
       for (int k = k0; k < k0 + HASH_CHUNK; k++) {
@@ -405,7 +427,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   DBG_PHASE_K(2, 5);  // thread 0's keys loaded and hashed (no barrier)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    if (threadIdx.x + k * SCAT_NT < count) rank[k] = atomicAdd(&s_off[cb_of(v[k])], 1u);
+    if (key_of(k) < count) rank[k] = atomicAdd(&s_off[cb_of(v[k])], 1u);
   }
   __syncthreads();
   DBG_PHASE_K(2, 1);
@@ -436,8 +458,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_hash_scatter(const FilterPlan* __re
   DBG_PHASE_K(2, 2);
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    const uint32_t j = threadIdx.x + k * SCAT_NT;
-    if (j < count) s_stage[s_off[cb_of(v[k])] + rank[k]] = v[k];
+    if (key_of(k) < count) s_stage[s_off[cb_of(v[k])] + rank[k]] = v[k];
   }
   __syncthreads();
   DBG_PHASE_K(2, 3);
@@ -2309,10 +2330,28 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
       }
     }
   }
+  constexpr bool WAVE_VAR = KIND == IN_VAR && PPL == 1 && OCC_LDS == 0;
+  if constexpr (WAVE_VAR) {
+    // variable-length keys: the wave's 64 keys are one contiguous byte range, read into a
+    // 4 KiB LDS window with coalesced 16-byte loads and hashed from there (wave_hash_var)
+    constexpr uint32_t VCAP = 4096;
+    __shared__ __attribute__((aligned(16))) uint32_t s_vk[PROBE_NT / WAVE][VCAP / 4 + 4];
+    fid[0] = 0xffffffffu;
+    h[0] = 0;
+    uint64_t o0 = 0, o1 = 0;
+    if (i0 < n) {
+      fid[0] = runs ? run_filter(runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
+      o0 = offs[i0];
+      o1 = offs[i0 + 1];
+    }
+    uint64_t w0 = 0, w1 = 0;
+    h[0] = wave_hash_var<VCAP, true>(static_cast<const uint8_t*>(in0), o0, o1, i0 < n,
+                                     s_vk[threadIdx.x / WAVE], seed, &w0, &w1);
+  }
   // the keys (or hashes) and filter ids are independent loads: issue them all together
 #pragma unroll
   for (int q = 0; q < PPL; q++) {
-    if constexpr (WAVE_KEYS) break;
+    if constexpr (WAVE_KEYS || WAVE_VAR) break;
     const uint64_t i = i0 + (uint64_t)q * PROBE_NT;
     fid[q] = 0xffffffffu;
     h[q] = 0;

@@ -428,3 +428,47 @@ def test_errors_match_reference_contract():
         E.FilterBatch(cfg, [E.routing_filter_max_fingerprints(cfg) + 1])
     with pytest.raises(E.PlatformStatusError):
         E.FilterBatch(cfg, [10], [200])  # fp_size + value_size > 32
+
+
+@pytest.mark.parametrize("shift", [0, 5])
+def test_var_keys_long_and_empty_wave_windows(oracle, shift):
+    """Variable-length keys through the wave-staged LDS windows (partition: 8 KiB per wave,
+    probe: 4 KiB per wave): empty and 1-15 B keys, and keys longer than either window
+    (hashed straight from HBM), from a key buffer at an odd address. Image and every probe
+    bit-exact against the oracle."""
+    rng = np.random.default_rng(7 + shift)
+    n = 40000
+    lens = rng.integers(0, 101, size=n)
+    lens[rng.random(n) < 0.05] = 0
+    short = rng.random(n) < 0.05
+    lens[short] = rng.integers(1, 16, size=int(short.sum()))
+    long_ix = rng.choice(n, size=300, replace=False)
+    lens[long_ix] = rng.integers(3000, 9500, size=300)
+    lens[:3] = [9000, 0, 8180]  # the first keys of the first wave: over both windows
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    data = rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)
+    cfg = E.routing_config_init()
+    ocfg = oracle.make_config()
+    buf = dev(np.concatenate([np.zeros(shift, np.uint8), data, np.zeros(16, np.uint8)]))
+    d_data = buf[shift:shift + data.size]
+    b = E.FilterBatch(cfg, [n])
+    b.build_var_keys(d_data, dev(offs))
+    img = b.image(0)
+    hv = oracle.hash_var(data, offs)
+    of = oracle.filter_add(ocfg, hv)
+    assert (img.pages == of.pages()).all() and (img.slots == of.slots()[: of.num_indices]).all()
+    hout = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    E.hash_var_keys(cfg, d_data, dev(offs), n, hout)
+    torch.cuda.synchronize()
+    assert (hout.cpu().numpy().view(np.uint32) == hv).all()
+    found = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    b.probe_var_keys(d_data, dev(offs), torch.zeros(n, dtype=torch.int32, device="cuda:0"), n, found)
+    torch.cuda.synchronize()
+    got = found.cpu().numpy().view(np.uint64)
+    assert (got & np.uint64(1)).all()
+    # negatives: the same lengths, other bytes
+    data2 = rng.integers(0, 256, size=data.size, dtype=np.uint8)
+    b.probe_var_keys(dev(data2), dev(offs), torch.zeros(n, dtype=torch.int32, device="cuda:0"), n, found)
+    torch.cuda.synchronize()
+    assert (found.cpu().numpy().view(np.uint64) == of.lookup_hashes(oracle.hash_var(data2, offs))).all()
