@@ -226,26 +226,17 @@ __device__ __forceinline__ uint32_t wave_hash_var(const uint8_t* keys, uint64_t 
     wave_sync_lds();  // every lane's reads of the old window are done
     const uint32_t n16 = (uint32_t)(a1 - a0) / 16;
     const v4* src = reinterpret_cast<const v4*>((uintptr_t)a0);
-    // GRP loads in flight per lane at a time (16 B each): 4 keeps the partition's 8 KiB
-    // window within its register budget
-    constexpr uint32_t GRP = IT < 4 ? IT : 4;
+    // LDS-DMA (global_load_lds_dwordx4): every chunk of the window in flight at once with
+    // no VGPR destination; instruction `it` fills bytes [1 KiB * it, +1 KiB) lane-linearly
 #pragma unroll
-    for (uint32_t g = 0; g < IT; g += GRP) {
-      v4 t[GRP];
-#pragma unroll
-      for (uint32_t it = 0; it < GRP; it++) {
-        const uint32_t j = lane + (g + it) * WAVE;
-        if (j < n16) {
-          if constexpr (NT) t[it] = __builtin_nontemporal_load(src + j);
-          else t[it] = src[j];
-        }
-      }
-#pragma unroll
-      for (uint32_t it = 0; it < GRP; it++) {
-        const uint32_t j = lane + (g + it) * WAVE;
-        if (j < n16) reinterpret_cast<v4*>(sw)[j] = t[it];
-      }
+    for (uint32_t it = 0; it < IT; it++) {
+      const uint32_t j = lane + it * WAVE;
+      if (j < n16)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j),
+                                         (__attribute__((address_space(3))) void*)(sw + it * WAVE * 4), 16, 0,
+                                         NT ? 2 : 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync_lds();
     *win0 = a0;
     *win1 = a1;

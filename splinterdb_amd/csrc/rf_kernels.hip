@@ -370,7 +370,12 @@ __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(4))) vo
   };
   constexpr uint32_t VWIN = (TILE_KEYS / (SCAT_NT / WAVE)) * 4 - 16;  // bytes (s_stage slice - pad)
   uint32_t* s_vwin = s_stage + (threadIdx.x / WAVE) * (TILE_KEYS / (SCAT_NT / WAVE));
-  uint64_t vw0 = 0, vw1 = 0;
+  uint64_t vw0 = 0, vw1 = 0, vo0 = 0, vo1 = 0;
+  if constexpr (KIND == IN_VAR) {
+    const uint32_t j = min(key_of(0), count - 1);
+    vo0 = offs[P.key_first + start + j];
+    vo1 = offs[P.key_first + start + j + 1];
+  }
 #pragma unroll
   for (int k0 = 0; k0 < PER; k0 += HASH_CHUNK) {
     if constexpr (KIND == IN_KEYS24) {
@@ -403,10 +408,15 @@ __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(4))) vo
       // contiguous byte stream, read into the wave's 8 KiB slice of s_stage (unused until
       // the ranking) with coalesced 16-byte loads and hashed from LDS (wave_hash_var).
       // The window persists across k: a key already staged is hashed without a reload.
+      // the next key's offsets load while this key's window is staged and hashed
 #pragma unroll
       for (int k = 0; k < HASH_CHUNK; k++) {
-        const uint32_t j = min(key_of(k0 + k), count - 1);
-        const uint64_t o0 = offs[P.key_first + start + j], o1 = offs[P.key_first + start + j + 1];
+        const uint64_t o0 = vo0, o1 = vo1;
+        if (k0 + k + 1 < PER) {
+          const uint32_t j = min(key_of(k0 + k + 1), count - 1);
+          vo0 = offs[P.key_first + start + j];
+          vo1 = offs[P.key_first + start + j + 1];
+        }
         const uint32_t h = wave_hash_var<VWIN, false>(static_cast<const uint8_t*>(in0), o0, o1,
                                                       key_of(k0 + k) < count, s_vwin, seed, &vw0, &vw1);
         v[k0 + k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
