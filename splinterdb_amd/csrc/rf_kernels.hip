@@ -1834,7 +1834,20 @@ __global__ __launch_bounds__(256) void k_hash(const void* __restrict__ in0, cons
                                               uint32_t key_len, uint32_t seed, uint64_t n,
                                               uint32_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
+  if constexpr (KIND == IN_VAR) {  // the wave's keys through a 4 KiB LDS window (wave_hash_var)
+    constexpr uint32_t VCAP = 4096;
+    __shared__ __attribute__((aligned(16))) uint32_t s_vk[256 / WAVE][VCAP / 4 + 4];
+    uint64_t o0 = 0, o1 = 0, w0 = 0, w1 = 0;
+    if (i < n) {
+      o0 = offs[i];
+      o1 = offs[i + 1];
+    }
+    const uint32_t h = wave_hash_var<VCAP, true>(static_cast<const uint8_t*>(in0), o0, o1, i < n,
+                                                 s_vk[threadIdx.x / WAVE], seed, &w0, &w1);
+    if (i < n) out[i] = h;
+  } else {
+    if (i < n) out[i] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
+  }
 }
 
 extern "C" int rf_launch_hash(void* stream, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
