@@ -2330,6 +2330,16 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
         v4u* sw = s_keys[threadIdx.x / WAVE];
         const uint32_t bytes = (uint32_t)min<uint64_t>(WAVE, n - wf) * 24;
         const v4u* src = reinterpret_cast<const v4u*>(static_cast<const uint8_t*>(in0) + wf * 24);
+        if (bytes == WAVE * 24) {  // full wave: LDS-DMA, no VGPR round trip
+#pragma unroll
+          for (uint32_t it = 0; it < 2; it++) {
+            const uint32_t j = lane + it * WAVE;
+            if (j < 96)
+              __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j),
+                                               (__attribute__((address_space(3))) void*)(sw + it * WAVE), 16, 0, 2);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else
 #pragma unroll
         for (uint32_t j = lane; j < 96; j += WAVE) {
           if ((j + 1) * 16 <= bytes) {
