@@ -345,12 +345,16 @@ def main():
         stream.synchronize()
         barrier()
         tr = S.max_over_ranks(time.perf_counter() - tr, dist, coll_dev)
+        r_ok = bool(((rfound & 1) == 1).all().item())
+        r_ok = S.max_over_ranks(0.0 if r_ok else 1.0, dist, coll_dev) == 0.0  # every rank's probes
         routed = {"mkeys_s": round(keys_all * reps / tr / 1e6, 1), "ms": round(tr / reps * 1e3, 3),
-                  "reps": reps, "verified": bool(((rfound & 1) == 1).all().item()),
+                  "reps": reps, "verified": r_ok,
                   "exchange": "none (1 rank)" if world == 1 else
                   ("all-to-all over RCCL" if coll_dev is not None else "all-to-all over gloo (rehearsal)")}
         del rkeys, rfid, d_rh, rfound, router
 
+    # every rank's checks, not only rank 0's: the line says verified only if all ranks agree
+    verified = S.max_over_ranks(0.0 if verified else 1.0, dist, coll_dev) == 0.0
     ms = {k: float(np.mean(v)) for k, v in stages.items()}
     kern = {}
     for k in ("partition", "count_scan", "scatter", "cb_sort", "cb_sort_big", "layout", "assemble", "probe"):
