@@ -1053,27 +1053,38 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   }
   DBG_PHASE_K(4, 0);
   if (threadIdx.x == 0) pplans[f].w = 0;
-  // next(j) = first block that does not fit on a page opened at block j: gallop forward
-  // from j + 1, then bisect (pages hold a handful of blocks: a few LDS reads per j). j is
-  // strided over the threads so a wave's reads fall on consecutive words (no bank conflicts).
+  // next(j) = first block that does not fit on a page opened at block j. next() is
+  // non-decreasing in j, so each thread takes a run of `run` consecutive blocks: the first
+  // is found by galloping from j + 1 then bisecting, the rest by advancing that pointer
+  // (about one LDS read per block instead of a gallop + bisect each). An odd run length
+  // (17 at 16,384 indices) keeps a wave's reads on distinct LDS banks.
   {
+    const uint32_t run = ((n + LAYOUT_NT - 1) / LAYOUT_NT) | 1u;  // run * LAYOUT_NT >= n
+    const uint32_t j0 = threadIdx.x * run, j1 = min(j0 + run, n);
+    uint32_t qp = 0;
 #pragma unroll 1
-    for (uint32_t j = threadIdx.x; j < n; j += LAYOUT_NT) {
+    for (uint32_t j = j0; j < j1; j++) {
       const uint32_t lim = s_excl[j] + page_size;
-      uint32_t qp = j + 1;  // first q' > j with excl[q'] > lim (n + 1: none)
-      if (qp <= n && s_excl[qp] <= lim) {
-        uint32_t lo = qp, hi = qp + 1, step = 1;  // excl[lo] <= lim
-        while (hi <= n && s_excl[hi] <= lim) {
-          lo = hi;
-          step <<= 1;
-          hi = lo + step;
+      if (j == j0) {
+        qp = j + 1;  // first q' > j with excl[q'] > lim (n + 1: none)
+        if (qp <= n && s_excl[qp] <= lim) {
+          uint32_t lo = qp, hi = qp + 1, step = 1;  // excl[lo] <= lim
+          while (hi <= n && s_excl[hi] <= lim) {
+            lo = hi;
+            step <<= 1;
+            hi = lo + step;
+          }
+          if (hi > n + 1) hi = n + 1;
+          while (hi - lo > 1) {  // excl[lo] <= lim < excl[hi] (hi == n + 1: past the end)
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_excl[mid] <= lim) lo = mid; else hi = mid;
+          }
+          qp = hi;
         }
-        if (hi > n + 1) hi = n + 1;
-        while (hi - lo > 1) {  // excl[lo] <= lim < excl[hi] (hi == n + 1: past the end)
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_excl[mid] <= lim) lo = mid; else hi = mid;
-        }
-        qp = hi;
+      } else {
+        // blocks in [j, next(j - 1)) fit under lim(j - 1) <= lim(j): start there
+        qp = max(qp, j + 1);
+        while (qp <= n && s_excl[qp] <= lim) qp++;
       }
       s_jA[j] = (uint16_t)(qp - 1);  // block qp-1 is the first that does not fit (n: none)
     }
