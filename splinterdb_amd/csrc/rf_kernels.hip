@@ -1034,8 +1034,10 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
     }
   }
   if (err) atomicOr(&s_err, err);
+  DBG_PHASE_K(4, 5);  // thread 0's sizes loaded (no barrier)
   uint32_t total;
   block_excl_scan_kmajor<LAYOUT_NT, PER>(sz, s_wt, &total);  // sz becomes the exclusive prefix
+  DBG_PHASE_K(4, 6);
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = k * LAYOUT_NT + threadIdx.x;

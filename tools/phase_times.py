@@ -37,8 +37,9 @@ if KID == 1:
              5: "dedupe+compact", 6: "write out", 7: "index bounds", 8: "uniq+end"}
     order = [15, 0, 1, 2, 3, 4, 5, 6, 7, 8]
 elif KID == 4:
-    names = {15: "entry", 0: "sizes+scan", 1: "next()", 2: "doubling", 3: "pages+slots", 8: "quirk+end"}
-    order = [15, 0, 1, 2, 3, 8]
+    names = {15: "entry", 5: "size loads (t0)", 6: "scan", 0: "excl store", 1: "next()", 2: "doubling",
+             3: "pages+slots", 8: "quirk+end"}
+    order = [15, 5, 6, 0, 1, 2, 3, 8]
 elif KID == 3:
     names = {15: "entry", 0: "metadata", 1: "fill", 2: "entry runs", 3: "store", 4: "line scan",
              8: "line write"}
