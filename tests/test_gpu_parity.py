@@ -472,3 +472,24 @@ def test_var_keys_long_and_empty_wave_windows(oracle, shift):
     b.probe_var_keys(dev(data2), dev(offs), torch.zeros(n, dtype=torch.int32, device="cuda:0"), n, found)
     torch.cuda.synchronize()
     assert (found.cpu().numpy().view(np.uint64) == of.lookup_hashes(oracle.hash_var(data2, offs))).all()
+
+
+def test_sparse_blocks_at_max_indices(oracle):
+    """16,384 indices (8M-fingerprint geometry) holding a few thousand distinct fingerprints:
+    nearly every block is an empty ~40 B encoding, ~100 blocks per page, so K5's next() runs
+    (17 blocks per thread at this index count) each start inside a page much longer than the
+    run and advance their pointer across it."""
+    cfg = E.routing_config_init()
+    ocfg = oracle.make_config()
+    rng = np.random.default_rng(11)
+    for distinct in (1, 2000, 60000):
+        base = rng.integers(0, 1 << 32, size=distinct, dtype=np.uint64).astype(np.uint32)
+        h = base[rng.integers(0, distinct, size=8_000_000)].astype(np.uint32)
+        b = E.FilterBatch(cfg, [h.size], [5])
+        b.build_hashes(dev(h))
+        img = b.image(0)
+        of = oracle.filter_add(ocfg, h, value=5)
+        assert img.num_indices == 16384
+        assert (img.num_unique, img.num_pages) == (of.num_unique, of.num_pages), distinct
+        assert (img.pages == of.pages()).all(), distinct
+        assert (img.slots == of.slots()[: of.num_indices]).all(), distinct
