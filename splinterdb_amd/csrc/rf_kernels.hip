@@ -779,17 +779,20 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     __syncthreads();
   }
   DBG_PHASE(4);
-  // dedupe + compaction: thread t owns the contiguous run [t*PER, t*PER + PER)
+  // dedupe + compaction: thread t owns the contiguous run [t*drun, t*drun + drun), drun =
+  // ceil(n / SORT_NT) made odd (lanes drun words apart fall on distinct LDS banks) and
+  // capped at PER: every thread takes a share of a small bucket, not half of them PER each
+  const uint32_t drun = min((uint32_t)PER, ((n + SORT_NT - 1) / SORT_NT) | 1u);
   uint32_t keep_mask = 0, cnt = 0;
   EntT w[PER];
-  const uint32_t i0 = threadIdx.x * PER;
+  const uint32_t i0 = threadIdx.x * drun;
   const EntT prev0 = (i0 > 0 && i0 <= n) ? s_b[i0 - 1] : EntT(0);
   {
     EntT prev = prev0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const uint32_t i = i0 + k;
-      if (i < n) {
+      if ((uint32_t)k < drun && i < n) {
         w[k] = s_b[i];
         const bool drop = (i > 0) && ent_drop(w[k], prev);
         if (!drop) { keep_mask |= 1u << k; cnt++; }
@@ -813,7 +816,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t i = i0 + k;
-    if (i < n) {
+    if ((uint32_t)k < drun && i < n) {
       const uint32_t e = ent_e(w[k]);
       const uint32_t li = index_of(e), fp = e >> P.vs;
       if (keep_mask & (1u << k)) {
