@@ -1360,7 +1360,7 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   const uint32_t IS = 1u << lis, rvs = P.rvs;
   // (A) metadata + entry offsets (2 blocks per thread)
   uint32_t cj[2], oj[2], sum = 0;
-  if (threadIdx.x < MAX_PAGE / 16) s_wm[threadIdx.x] = 0;
+  for (uint32_t i = threadIdx.x; i < MAX_PAGE / 16; i += ASM_NT) s_wm[i] = 0;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const uint32_t j = threadIdx.x * 2 + q;
@@ -1403,12 +1403,19 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   }
   __syncthreads();
   // block of word w (the block holding byte 4w) = block starts in words <= w: thread t
-  // owns words 4t..4t+3, so one exclusive scan of the per-thread mark counts
+  // owns the QPT 16-byte quads t*QPT.. (words 4 * quad ..), so one exclusive scan of the
+  // per-thread mark counts
   const uint32_t nwp = page_size / 4;
-  const uint32_t mw = 4 * threadIdx.x < nwp ? s_wm[threadIdx.x] : 0u;
+  constexpr uint32_t QPT = (MAX_PAGE / 16 + ASM_NT - 1) / ASM_NT;
+  uint32_t mwq[QPT], msum = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < QPT; q++) {
+    const uint32_t qd = threadIdx.x * QPT + q;
+    mwq[q] = 4 * qd < nwp ? s_wm[qd] : 0u;
+    msum += (mwq[q] & 0xffu) + ((mwq[q] >> 8) & 0xffu) + ((mwq[q] >> 16) & 0xffu) + (mwq[q] >> 24);
+  }
   uint32_t mtot;
-  const uint32_t jw0 = block_excl_scan<ASM_NT>((mw & 0xffu) + ((mw >> 8) & 0xffu) + ((mw >> 16) & 0xffu) + (mw >> 24),
-                                              s_tmp, &mtot);
+  const uint32_t jw0 = block_excl_scan<ASM_NT>(msum, s_tmp, &mtot);
   const uint32_t* base = sorted32 + P.e_first;
   const uint32_t nruns = (ne + ASM_RUN - 1) / ASM_RUN;
   // a run's entries: independent loads, all in flight together
@@ -1445,13 +1452,18 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
   // the first run's loads are issued before the fill, so they land while it runs
   uint32_t ev0[ASM_RUN];
   if (threadIdx.x < nruns) load_run(threadIdx.x, ev0);
-  // (B) fill: thread t builds words 4t..4t+3 (bytes 16t..16t+15) and stores them at once
-  if (4 * threadIdx.x < nwp) {
-    uint32_t x4[4], jw = jw0;
+  // (B) fill: thread t builds its quads' words (16 bytes each) and stores each quad at once
+  uint32_t jw = jw0;
+#pragma unroll
+  for (uint32_t q = 0; q < QPT; q++) {
+  const uint32_t qd = threadIdx.x * QPT + q;
+  const uint32_t mw = mwq[q];
+  if (4 * qd < nwp) {
+    uint32_t x4[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       jw += (mw >> (8 * k)) & 0xffu;
-      const uint32_t w = 4 * threadIdx.x + k;
+      const uint32_t w = 4 * qd + k;
       uint32_t j = jw, x = 0;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -1464,7 +1476,8 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
       }
       x4[k] = x;
     }
-    reinterpret_cast<v4u*>(s_pg)[threadIdx.x] = v4u{x4[0], x4[1], x4[2], x4[3]};
+    reinterpret_cast<v4u*>(s_pg)[qd] = v4u{x4[0], x4[1], x4[2], x4[3]};
+  }
   }
   if (threadIdx.x < 4) s_pg[page_size / 4 + threadIdx.x] = 0;
   __syncthreads();

@@ -23,7 +23,7 @@ constexpr int SORT_CAP = 9216;   // entries per coarse bucket held in LDS (means
 constexpr int BIG_NT = 1024;
 constexpr int BIG_GRID = 64;
 constexpr int LAYOUT_NT = 1024;
-constexpr int ASM_NT = 256;
+constexpr int ASM_NT = 128;
 constexpr uint32_t ASM_MAXB_HOST = 128;  // = ASM_MAXB in rf_kernels.hip (blocks per page in LDS)
 constexpr uint32_t ASM_GT_HOST = 1024;   // = ASM_GT (group-start table entries per page)
 
