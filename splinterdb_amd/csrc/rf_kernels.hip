@@ -1333,13 +1333,17 @@ __global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restric
                                                      uint8_t* __restrict__ pages, uint4* __restrict__ lines,
                                                      uint32_t lis, uint32_t page_size) {
   __shared__ __attribute__((aligned(16))) uint32_t s_pg[MAX_PAGE / 4 + 4];
-  __shared__ uint16_t s_gs[ASM_GT];  // per block: bit after each line group's last terminator
   __shared__ uint32_t s_wpre[ASM_MAXB];
   __shared__ uint32_t s_off[ASM_MAXB + 1];
   __shared__ uint32_t s_c[ASM_MAXB];
   __shared__ uint32_t s_est[ASM_MAXB + 1];
   __shared__ uint32_t s_src[ASM_MAXB];
-  __shared__ uint16_t s_rblk[ASM_MAXE / ASM_RUN];  // block of each run's first entry
+  // s_rblk (block of each run's first entry, phases A-C) and s_gs (per block: bit after each
+  // line group's last terminator, phase E) share one array: 2 KiB less LDS per page lets
+  // 14 pages, not 13, run on a CU
+  __shared__ uint16_t s_rg[ASM_MAXE / ASM_RUN > ASM_GT ? ASM_MAXE / ASM_RUN : ASM_GT];
+  uint16_t* const s_rblk = s_rg;
+  uint16_t* const s_gs = s_rg;
   __shared__ uint32_t s_wm[MAX_PAGE / 16];  // byte w: a block j >= 1 starts in word w
   __shared__ uint32_t s_tmp[ASM_NT / WAVE + 1];
   DBG_PHASE_K(3, 15);
