@@ -1322,7 +1322,7 @@ __device__ __forceinline__ uint64_t lds_bits64(const uint32_t* s_pg, uint32_t bi
 // with one atomic: adjacent lanes share at most a window edge. (D) 16-byte stores.
 // Measured before: entry-parallel single-bit atomics (~19 LDS conflict cycles per LDS
 // instruction), and a byte-serial gather per 16-byte chunk (3.6x slower again).
-__global__ __launch_bounds__(ASM_NT) void k_assemble(const FilterPlan* __restrict__ plans,
+__global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) void k_assemble(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ pg_filter,
                                                      const uint32_t* __restrict__ idx_cnt,
                                                      const uint32_t* __restrict__ idx_start,
