@@ -68,6 +68,8 @@ def parse():
                    help="also time routed probes: each rank probes keys of every rank's filters, "
                         "moved to the owner by all-to-all (route.py); reported beside value")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    p.add_argument("--digest-out", default="",
+                   help="write each rank's per-filter image SHA-256s to <path>.rank<r> (tests)")
     return p.parse_args()
 
 
@@ -149,8 +151,36 @@ def cpu_baseline_var(args, cfg_lis, w, F, n):
     }
 
 
+def launch_ranks(args):
+    """`--gpus N` is the number of ranks, one per GPU. Under torchrun (WORLD_SIZE set) it
+    must agree with WORLD_SIZE. Without it, N > 1 starts the N ranks here: a child
+    torch.distributed.run on 127.0.0.1, started before this process makes any HIP call (no
+    exec from a process that touched the GPU). Returns the children's exit status, or None
+    when this process is itself the (only) rank."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+        return None
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.gpus == 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    spawned = launch_ranks(args)
+    if spawned is not None:
+        sys.exit(spawned)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -250,11 +280,32 @@ def main():
     slot_bytes = sum(i.num_indices for i in infos) * 8
     unique = sum(i.num_unique for i in infos)
     verified = ok and all(i.error == 0 for i in infos)
-    if not var and rank == 0 and me.key_begin == 0 and n == 8_000_000 and args.log_index_size == 8:
+    # image bytes against the committed golden SHA-256s (tests/golden/sha256.json, made by
+    # oracle/gen_golden.py) for every filter of this rank that has one: C2's filter 0, and
+    # the sampled C3/C4 filters k of the 2^20-key layout (ids [k 2^20, (k+1) 2^20))
+    sha_checked = []
+    if not var and args.log_index_size == 8:
         with open(os.path.join(ROOT, "tests", "golden", "sha256.json")) as fh:
-            want = json.load(fh)["seq_n8000000_lis8"]["pages_sha256"]
-        img = batch.image(0)
-        verified = verified and hashlib.sha256(img.pages.tobytes()).hexdigest() == want
+            gold = json.load(fh)
+        for f in range(F):
+            g = me.filter_begin + f
+            key = ("seq_n8000000_lis8" if n == 8_000_000 and g == 0 else
+                   f"seq_n{n}_lis8_k{g}" if n == 1 << 20 else None)
+            if key in gold:
+                img = batch.image(f)
+                good = (hashlib.sha256(img.pages.tobytes()).hexdigest() == gold[key]["pages_sha256"] and
+                        hashlib.sha256(img.slots.tobytes()).hexdigest() == gold[key]["slots_sha256"])
+                verified = verified and good
+                sha_checked.append(g)
+    if args.digest_out:
+        # per-filter image digests of this rank (the multi-rank tests compare them with a
+        # single-process build of the same filters)
+        dig = {}
+        for f in range(F):
+            img = batch.image(f)
+            dig[me.filter_begin + f] = hashlib.sha256(img.pages.tobytes() + img.slots.tobytes()).hexdigest()
+        with open(f"{args.digest_out}.rank{rank}", "w") as fh:
+            json.dump(dig, fh)
 
     # ---- end-to-end (PCIe-inclusive) rate, reported beside `value` (never as it) ------
     # keys H2D from pinned host memory -> build -> probe -> found_values + page images +
@@ -404,6 +455,7 @@ def main():
                      "traffic": traffic},
         "kernels": kern,
         "verified": verified,
+        "sha_checked_filters": sha_checked,
     }
     if routed is not None:
         out["routed_probe"] = routed

@@ -220,6 +220,9 @@ def gen_filters():
     print("filters.npz:", len(out), "arrays")
 
 
+SHARD_SAMPLE = (0, 1, 77, 255, 256, 511, 768, 1023)  # filters of C3 (0-255) and C4 (0-1023)
+
+
 def gen_sha():
     res = {}
     for n, lis in ((1000000, 8), (8000000, 8), (1048576, 8)):
@@ -233,6 +236,15 @@ def gen_sha():
         cfg = O.make_config()
         f = O.filter_add(cfg, O.hash_fixed(K.random_keys(n).reshape(-1), 24))
         res[f"rand24_n{n}_lis8"] = {
+            "pages_sha256": hashlib.sha256(f.pages().tobytes()).hexdigest(),
+            "slots_sha256": hashlib.sha256(f.slots()[: f.num_indices].tobytes()).hexdigest(),
+            "num_unique": f.num_unique, "num_pages": f.num_pages}
+    # C3 / C4 filters: filter k of the 2^20-key layout holds sequential ids [k 2^20, (k+1) 2^20)
+    cfg = O.make_config()
+    for k in SHARD_SAMPLE:
+        n = 1 << 20
+        f = O.filter_add(cfg, O.hash_fixed(K.seq_keys(k * n, n).reshape(-1), 24))
+        res[f"seq_n{n}_lis8_k{k}"] = {
             "pages_sha256": hashlib.sha256(f.pages().tobytes()).hexdigest(),
             "slots_sha256": hashlib.sha256(f.slots()[: f.num_indices].tobytes()).hexdigest(),
             "num_unique": f.num_unique, "num_pages": f.num_pages}

@@ -1,0 +1,656 @@
+/*
+ * ref_harness.c -- TEST INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * Drives the reference's OWN routing filter -- vmware/splinterdb src/routing_filter.c,
+ * src/mini_allocator.c, src/clockcache.c, src/rc_allocator.c, src/PackedArray.c, compiled
+ * unmodified from /root/reference by oracle/Makefile into oracle/_ref/libref_rf.so -- so
+ * that the oracle restatement (rf_oracle.c) and the GPU images can be checked against
+ * filters the reference itself built, byte for byte.
+ *
+ * The reference's storage device sits behind its abstract IO interface (io_ops,
+ * src/platform_linux/platform_io.h:92-110). Its one implementation, laio.c, needs libaio,
+ * which this image lacks, so laio.c and platform_io.c are NOT compiled; this file provides
+ * an in-memory device behind the same interface instead (an anonymous mapping the size of
+ * the configured disk), plus the two non-virtual helpers platform_io.c would provide
+ * (io_config_valid, io_read_bootstrap). No libaio stand-in exists. The cache is sized to
+ * hold every page, so nothing is ever written back to the device (the tests assert it) and
+ * every filter page is a fresh cache page; the only device reads are incremental adds'
+ * prefetch of the old filter's extents (mini_prefetch, src/routing_filter.c:356).
+ *
+ * Everything else -- routing_filter_add / _lookup / _lookup_async / _estimate_unique_fp,
+ * the clockcache the pages live in, the mini_allocator that assigns their addresses -- is
+ * the reference's code. rfr_filter_image() reads a built filter back through cache_get
+ * (src/cache.h:268) into this repo's relocatable image form: data pages in placement order,
+ * slot = data_page_no * page_size + offset (the reference stores absolute disk addresses,
+ * src/routing_filter.c:620).
+ */
+#define _GNU_SOURCE
+#include "platform.h"
+#include "routing_filter.h"
+#include "clockcache.h"
+#include "rc_allocator.h"
+#include "splinterdb/default_data_config.h"
+
+#include <pthread.h>
+#include <stdatomic.h>
+#include <sys/mman.h>
+#include <sys/uio.h>
+#include <time.h>
+
+/* ---- in-memory device behind io_ops --------------------------------------------------- */
+typedef struct mem_io {
+   io_handle  super;
+   io_config *cfg;
+   uint8     *disk;
+   uint64     size;
+   _Atomic uint64 reads, writes;
+} mem_io;
+
+static platform_status
+mem_rw(mem_io *io, void *buf, uint64 bytes, uint64 addr, int wr)
+{
+   if (addr > io->size || bytes > io->size - addr) {
+      return STATUS_IO_ERROR;
+   }
+   if (wr) {
+      memcpy(io->disk + addr, buf, bytes);
+      atomic_fetch_add(&io->writes, 1);
+   } else {
+      memcpy(buf, io->disk + addr, bytes);
+      atomic_fetch_add(&io->reads, 1);
+   }
+   return STATUS_OK;
+}
+
+static platform_status
+mem_read(io_handle *io, void *buf, uint64 bytes, uint64 addr)
+{
+   return mem_rw((mem_io *)io, buf, bytes, addr, 0);
+}
+
+static platform_status
+mem_write(io_handle *io, void *buf, uint64 bytes, uint64 addr)
+{
+   return mem_rw((mem_io *)io, buf, bytes, addr, 1);
+}
+
+#define MEM_ASYNC_MAX_PAGES 32 /* pages_per_extent (laio.c appends at most one extent) */
+typedef struct mem_async_state {
+   io_async_state    super;
+   mem_io           *io;
+   io_async_cmd      cmd;
+   uint64            addr;
+   uint64            iovlen;
+   platform_status   rc;
+   struct iovec      iov[MEM_ASYNC_MAX_PAGES];
+} mem_async_state;
+_Static_assert(sizeof(mem_async_state) <= IO_ASYNC_STATE_BUFFER_SIZE, "async state too large");
+
+static platform_status
+mem_async_append_page(io_async_state *s, void *buf)
+{
+   mem_async_state *m = (mem_async_state *)s;
+   if (m->iovlen == MEM_ASYNC_MAX_PAGES) {
+      return STATUS_LIMIT_EXCEEDED;
+   }
+   m->iov[m->iovlen].iov_base = buf;
+   m->iov[m->iovlen].iov_len  = m->io->cfg->page_size;
+   m->iovlen++;
+   return STATUS_OK;
+}
+
+/* completes at once: an immediate ASYNC_STATUS_DONE is a legal outcome of io_async_run */
+static async_status
+mem_async_run(io_async_state *s)
+{
+   mem_async_state *m = (mem_async_state *)s;
+   uint64           a = m->addr;
+   for (uint64 k = 0; k < m->iovlen && SUCCESS(m->rc); k++) {
+      m->rc = mem_rw(m->io, m->iov[k].iov_base, m->iov[k].iov_len, a, m->cmd == io_async_pwritev);
+      a += m->iov[k].iov_len;
+   }
+   return ASYNC_STATUS_DONE;
+}
+
+static platform_status
+mem_async_result(io_async_state *s)
+{
+   return ((mem_async_state *)s)->rc;
+}
+
+static const struct iovec *
+mem_async_iovec(io_async_state *s, uint64 *iovlen)
+{
+   mem_async_state *m = (mem_async_state *)s;
+   *iovlen            = m->iovlen;
+   return m->iov;
+}
+
+static void
+mem_async_deinit(io_async_state *s)
+{
+   (void)s;
+}
+
+static io_async_state_ops mem_async_ops = {
+   .append_page = mem_async_append_page,
+   .run         = mem_async_run,
+   .get_result  = mem_async_result,
+   .get_iovec   = mem_async_iovec,
+   .deinit      = mem_async_deinit,
+};
+
+static platform_status
+mem_async_init(io_async_state   *state,
+               io_handle        *io,
+               io_async_cmd      cmd,
+               uint64            addr,
+               async_callback_fn callback,
+               void             *callback_arg)
+{
+   mem_async_state *m = (mem_async_state *)state;
+   (void)callback;
+   (void)callback_arg;
+   m->super.ops = &mem_async_ops;
+   m->io        = (mem_io *)io;
+   m->cmd       = cmd;
+   m->addr      = addr;
+   m->iovlen    = 0;
+   m->rc        = STATUS_OK;
+   return STATUS_OK;
+}
+
+static void
+mem_noop_cleanup(io_handle *io, uint64 count)
+{
+   (void)io;
+   (void)count;
+}
+
+static void
+mem_noop(io_handle *io)
+{
+   (void)io;
+}
+
+static io_ops mem_io_ops = {
+   .read             = mem_read,
+   .write            = mem_write,
+   .async_state_init = mem_async_init,
+   .cleanup          = mem_noop_cleanup,
+   .wait_all         = mem_noop,
+};
+
+/* the two non-virtual io helpers of platform_io.c (not compiled: it includes laio.h) */
+platform_status
+io_config_valid(io_config *cfg)
+{
+   if (cfg->page_size != 4096 && cfg->page_size != 8192) {
+      return STATUS_BAD_PARAM;
+   }
+   if (cfg->extent_size % cfg->page_size != 0) {
+      return STATUS_BAD_PARAM;
+   }
+   return STATUS_OK;
+}
+
+platform_status
+io_read_bootstrap(const char *filename, void *buf, uint64 bytes, uint64 addr)
+{
+   (void)filename;
+   (void)buf;
+   (void)bytes;
+   (void)addr;
+   return STATUS_NOTSUP; /* only used to mount an existing disk, never here */
+}
+
+/* ---- one reference filter stack: heap, device, allocator, clockcache, configs --------- */
+typedef struct rfr_stack {
+   platform_heap_id  hid;
+   io_config         io_cfg;
+   allocator_config  al_cfg;
+   clockcache_config cc_cfg;
+   mem_io            io;
+   rc_allocator      al;
+   clockcache        cc;
+   data_config       data_cfg;
+   routing_config    rcfg;
+} rfr_stack;
+
+static _Atomic int g_registered_main = 0;
+
+rfr_stack *
+rfr_create(uint32 fingerprint_size, uint32 log_index_size, uint64 cache_mib, uint64 disk_mib)
+{
+   if (!atomic_exchange(&g_registered_main, 1)) {
+      platform_register_thread();
+   }
+   rfr_stack *s = calloc(1, sizeof(*s));
+   if (!s) {
+      return NULL;
+   }
+   platform_status rc = platform_heap_create(platform_get_module_id(), 1024 * MiB, FALSE, &s->hid);
+   if (!SUCCESS(rc)) {
+      free(s);
+      return NULL;
+   }
+   io_config_init(&s->io_cfg, 4096, 4096 * 32, O_RDWR | O_CREAT, 0600, 256, "rfr-memory-device");
+   const uint64 disk = disk_mib * MiB;
+   s->io.super.ops   = &mem_io_ops;
+   s->io.cfg         = &s->io_cfg;
+   s->io.size        = disk;
+   s->io.disk        = mmap(NULL, disk, PROT_READ | PROT_WRITE,
+                     MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+   if (s->io.disk == MAP_FAILED) {
+      free(s);
+      return NULL;
+   }
+   allocator_config_init(&s->al_cfg, &s->io_cfg, disk);
+   rc = rc_allocator_init(&s->al, &s->al_cfg, &s->io.super, s->hid, platform_get_module_id());
+   if (!SUCCESS(rc)) {
+      munmap(s->io.disk, disk);
+      free(s);
+      return NULL;
+   }
+   clockcache_config_init(&s->cc_cfg, &s->io_cfg, cache_mib * MiB, "", FALSE);
+   rc = clockcache_init(&s->cc, &s->cc_cfg, &s->io.super, (allocator *)&s->al, "rfr", s->hid,
+                        platform_get_module_id());
+   if (!SUCCESS(rc)) {
+      rc_allocator_deinit(&s->al);
+      munmap(s->io.disk, disk);
+      free(s);
+      return NULL;
+   }
+   default_data_config_init(&s->data_cfg);
+   /* splinterdb.c:270-276 / tests/functional/test.h: hash argument ignored, seed 42 */
+   routing_config_init(&s->rcfg, (cache_config *)&s->cc_cfg, &s->data_cfg, fingerprint_size,
+                       log_index_size, NULL, 42);
+   return s;
+}
+
+void
+rfr_destroy(rfr_stack *s)
+{
+   if (!s) {
+      return;
+   }
+   clockcache_deinit(&s->cc);
+   rc_allocator_deinit(&s->al);
+   munmap(s->io.disk, s->io.size);
+   platform_heap_destroy(&s->hid);
+   free(s);
+}
+
+/* device traffic: writes = pages the clockcache wrote back (evicted or flushed); reads =
+ * pages read in (incremental adds prefetch the old filter's extents, mini_prefetch,
+ * src/routing_filter.c:356, which includes pages never allocated -- zeros on the device) */
+uint64
+rfr_device_io_count(rfr_stack *s, int writes)
+{
+   return writes ? atomic_load(&s->io.writes) : atomic_load(&s->io.reads);
+}
+
+uint64
+rfr_max_fingerprints(rfr_stack *s)
+{
+   return routing_filter_max_fingerprints((cache_config *)&s->cc_cfg, &s->rcfg);
+}
+
+/* routing_filter_add; fps is mutated (shifted + sorted), as the reference does */
+int
+rfr_filter_add(rfr_stack      *s,
+               routing_filter *old_filter,
+               routing_filter *filter,
+               uint32         *fps,
+               uint64          n,
+               uint16          value)
+{
+   routing_filter empty = NULL_ROUTING_FILTER;
+   memset(filter, 0, sizeof(*filter));
+   platform_status rc = routing_filter_add(
+      (cache *)&s->cc, &s->rcfg, old_filter ? old_filter : &empty, filter, fps, n, value);
+   return rc.r;
+}
+
+/* one 4 KiB page of the cache into dst (cache_get / cache_unget, src/cache.h:268-311) */
+static void
+read_page(rfr_stack *s, uint64 addr, uint8 *dst)
+{
+   page_handle *pg = cache_get((cache *)&s->cc, addr, TRUE, PAGE_TYPE_FILTER);
+   memcpy(dst, pg->data, s->io_cfg.page_size);
+   cache_unget((cache *)&s->cc, pg);
+}
+
+/*
+ * The filter as a relocatable image: the index slots of the index extent at filter->addr
+ * (slot i at page i / addrs_per_page, src/routing_filter.c:178-198), their data pages in
+ * order of first use (blocks are placed in index order, :599-620), each copied out whole.
+ * Returns the number of indices (0 = NULL filter); *num_pages = data pages. pages must
+ * hold max_pages * page_size bytes, slots num_indices entries.
+ */
+uint32
+rfr_filter_image(rfr_stack      *s,
+                 routing_filter *f,
+                 uint8          *pages,
+                 uint32          max_pages,
+                 uint64         *slots,
+                 uint32         *num_pages)
+{
+   *num_pages = 0;
+   if (f->addr == 0) {
+      return 0;
+   }
+   const uint64 ps  = s->io_cfg.page_size;
+   const uint32 lis = s->rcfg.log_index_size;
+   uint32       lnb = 31 - __builtin_clz(f->num_fingerprints);
+   if (lnb < lis) {
+      lnb = lis;
+   }
+   const uint32 num_indices    = 1u << (lnb - lis);
+   const uint64 addrs_per_page = ps / sizeof(uint64);
+   uint8       *ipage          = malloc(ps);
+   uint64       cur_ipage      = UINT64_MAX;
+   uint64       last_page      = UINT64_MAX;
+   uint32       np             = 0;
+   for (uint32 i = 0; i < num_indices; i++) {
+      const uint64 ip = f->addr + (i / addrs_per_page) * ps;
+      if (ip != cur_ipage) {
+         read_page(s, ip, ipage);
+         cur_ipage = ip;
+      }
+      const uint64 hdr  = ((uint64 *)ipage)[i % addrs_per_page];
+      const uint64 page = hdr - hdr % ps;
+      if (page != last_page) {
+         if (np == max_pages) {
+            free(ipage);
+            return 0;
+         }
+         read_page(s, page, pages + (uint64)np * ps);
+         last_page = page;
+         np++;
+      }
+      slots[i] = (uint64)(np - 1) * ps + hdr % ps;
+   }
+   free(ipage);
+   *num_pages = np;
+   return num_indices;
+}
+
+/* routing_filter_lookup of n fixed-length keys (key i = keys[i*key_len ..]) */
+void
+rfr_lookup_keys(rfr_stack      *s,
+                routing_filter *f,
+                const uint8    *keys,
+                uint32          key_len,
+                uint64          n,
+                uint64         *found)
+{
+   for (uint64 i = 0; i < n; i++) {
+      key             k  = key_create(FALSE, key_len, keys + i * key_len);
+      platform_status rc = routing_filter_lookup((cache *)&s->cc, &s->rcfg, f, k, &found[i]);
+      if (!SUCCESS(rc)) {
+         found[i] = UINT64_MAX;
+      }
+   }
+}
+
+/* variable-length keys: key i = bytes[offs[i] .. offs[i+1]) */
+void
+rfr_lookup_var_keys(rfr_stack      *s,
+                    routing_filter *f,
+                    const uint8    *bytes,
+                    const uint64   *offs,
+                    uint64          n,
+                    uint64         *found)
+{
+   for (uint64 i = 0; i < n; i++) {
+      key             k  = key_create(FALSE, offs[i + 1] - offs[i], bytes + offs[i]);
+      platform_status rc = routing_filter_lookup((cache *)&s->cc, &s->rcfg, f, k, &found[i]);
+      if (!SUCCESS(rc)) {
+         found[i] = UINT64_MAX;
+      }
+   }
+}
+
+void
+rfr_hash_var_keys(rfr_stack *s, const uint8 *bytes, const uint64 *offs, uint64 n, uint32 *out)
+{
+   for (uint64 i = 0; i < n; i++) {
+      key k  = key_create(FALSE, offs[i + 1] - offs[i], bytes + offs[i]);
+      out[i] = data_key_hash(&s->data_cfg, k, s->rcfg.seed);
+   }
+}
+
+/* the same through the coroutine, routing_filter_lookup_async (:895-972), driven to
+ * completion by polling; returns the number of ASYNC_STATUS_RUNNING yields seen */
+uint64
+rfr_lookup_keys_async(rfr_stack      *s,
+                      routing_filter *f,
+                      const uint8    *keys,
+                      uint32          key_len,
+                      uint64          n,
+                      uint64         *found)
+{
+   uint64 yields = 0;
+   for (uint64 i = 0; i < n; i++) {
+      routing_filter_lookup_async_state st;
+      key k = key_create(FALSE, key_len, keys + i * key_len);
+      routing_filter_lookup_async_state_init(
+         &st, (cache *)&s->cc, &s->rcfg, *f, k, &found[i], NULL, NULL);
+      while (routing_filter_lookup_async(&st) != ASYNC_STATUS_DONE) {
+         yields++;
+         cache_cleanup((cache *)&s->cc);
+      }
+      if (!SUCCESS(st.__async_result)) {
+         found[i] = UINT64_MAX;
+      }
+   }
+   return yields;
+}
+
+int
+rfr_estimate_unique_fp(rfr_stack *s, routing_filter *filters, uint64 num, uint32 *out)
+{
+   return routing_filter_estimate_unique_fp((cache *)&s->cc, &s->rcfg, s->hid, filters, num, out).r;
+}
+
+uint32
+rfr_estimate_unique_keys_from_count(rfr_stack *s, uint64 num_unique)
+{
+   return routing_filter_estimate_unique_keys_from_count(&s->rcfg, num_unique);
+}
+
+uint32
+rfr_estimate_unique_keys(rfr_stack *s, routing_filter *f)
+{
+   return routing_filter_estimate_unique_keys(f, &s->rcfg);
+}
+
+uint64
+rfr_space_use_bytes(rfr_stack *s, routing_filter *f)
+{
+   return routing_filter_space_use_bytes((cache *)&s->cc, f);
+}
+
+void
+rfr_dec_ref(rfr_stack *s, routing_filter *f)
+{
+   routing_filter_dec_ref((cache *)&s->cc, f);
+}
+
+/* the header inlines, as the reference's compiler builds them (src/routing_filter.h:94-111) */
+uint16
+rfr_get_next_value(uint64 found_values, uint16 last_value)
+{
+   return routing_filter_get_next_value(found_values, last_value);
+}
+
+int
+rfr_is_value_found(uint64 found_values, uint16 value)
+{
+   return routing_filter_is_value_found(found_values, value) ? 1 : 0;
+}
+
+/* XXH32 through the reference's data_config (data_key_hash, src/data_internal.h:673-683) */
+void
+rfr_hash_keys(rfr_stack *s, const uint8 *keys, uint32 key_len, uint64 n, uint32 *out)
+{
+   for (uint64 i = 0; i < n; i++) {
+      key k  = key_create(FALSE, key_len, keys + i * key_len);
+      out[i] = data_key_hash(&s->data_cfg, k, s->rcfg.seed);
+   }
+}
+
+/* ---- CPU baseline: the reference's own build and lookup, P threads ------------------- */
+/* One routing_filter_add per filter, filters handed to P registered threads as SplinterDB's
+ * TASK_TYPE_NORMAL workers do (src/trunk.c:3932, :4168). hash_keys: 1 = hash the filter's
+ * keys first (btree_pack + add, trunk semantics), 0 = keys already are 32-bit hashes
+ * (filter_test semantics, tests/functional/filter_test.c:185-205). */
+typedef struct rfr_bench {
+   rfr_stack      *s;
+   const uint8    *keys;
+   uint32          key_len;
+   int             hash_keys;
+   const uint64   *start;
+   const uint32   *count;
+   uint32          nf;
+   uint16          value;
+   routing_filter *keep;
+   _Atomic uint32  next;
+   _Atomic int     err;
+   /* probe */
+   const uint32   *filter_id;
+   uint64          n;
+   uint64         *found;
+} rfr_bench;
+
+static double
+now_s(void)
+{
+   struct timespec ts;
+   clock_gettime(CLOCK_MONOTONIC, &ts);
+   return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static void *
+build_worker(void *arg)
+{
+   rfr_bench *b = arg;
+   platform_register_thread();
+   for (;;) {
+      uint32 f = atomic_fetch_add(&b->next, 1);
+      if (f >= b->nf) {
+         break;
+      }
+      uint32  n   = b->count[f];
+      uint32 *fps = malloc((size_t)n * 4 + 4);
+      if (b->hash_keys) {
+         for (uint32 i = 0; i < n; i++) {
+            key k  = key_create(FALSE, b->key_len, b->keys + (b->start[f] + i) * b->key_len);
+            fps[i] = data_key_hash(&b->s->data_cfg, k, b->s->rcfg.seed);
+         }
+      } else {
+         memcpy(fps, (const uint32 *)b->keys + b->start[f], (size_t)n * 4);
+      }
+      routing_filter  empty = NULL_ROUTING_FILTER;
+      platform_status rc    = routing_filter_add(
+         (cache *)&b->s->cc, &b->s->rcfg, &empty, &b->keep[f], fps, n, b->value);
+      if (!SUCCESS(rc)) {
+         atomic_store(&b->err, rc.r);
+      }
+      free(fps);
+   }
+   platform_deregister_thread();
+   return NULL;
+}
+
+static void *
+probe_worker(void *arg)
+{
+   rfr_bench *b = arg;
+   platform_register_thread();
+   const uint64 chunk = 4096;
+   for (;;) {
+      uint64 s = (uint64)atomic_fetch_add(&b->next, 1) * chunk;
+      if (s >= b->n) {
+         break;
+      }
+      uint64 e = s + chunk < b->n ? s + chunk : b->n;
+      for (uint64 i = s; i < e; i++) {
+         key k = key_create(FALSE, b->key_len, b->keys + i * b->key_len);
+         routing_filter_lookup(
+            (cache *)&b->s->cc, &b->s->rcfg, &b->keep[b->filter_id[i]], k, &b->found[i]);
+      }
+   }
+   platform_deregister_thread();
+   return NULL;
+}
+
+static double
+run_threads(rfr_bench *b, int threads, void *(*fn)(void *))
+{
+   if (threads < 1) {
+      threads = 1;
+   }
+   pthread_t *th = malloc(sizeof(pthread_t) * threads);
+   double     t0 = now_s();
+   for (int t = 0; t < threads; t++) {
+      pthread_create(&th[t], NULL, fn, b);
+   }
+   for (int t = 0; t < threads; t++) {
+      pthread_join(th[t], NULL);
+   }
+   double t1 = now_s();
+   free(th);
+   return t1 - t0;
+}
+
+/* seconds, or -1 on a failed add; keep[f] = the built filters (caller releases them) */
+double
+rfr_bench_build(rfr_stack      *s,
+                const uint8    *keys,
+                uint32          key_len,
+                int             hash_keys,
+                const uint64   *key_start,
+                const uint32   *key_count,
+                uint32          num_filters,
+                uint16          value,
+                int             threads,
+                routing_filter *keep)
+{
+   rfr_bench b;
+   memset(&b, 0, sizeof(b));
+   b.s         = s;
+   b.keys      = keys;
+   b.key_len   = key_len;
+   b.hash_keys = hash_keys;
+   b.start     = key_start;
+   b.count     = key_count;
+   b.nf        = num_filters;
+   b.value     = value;
+   b.keep      = keep;
+   double t    = run_threads(&b, threads, build_worker);
+   return atomic_load(&b.err) ? -1.0 : t;
+}
+
+double
+rfr_bench_probe(rfr_stack      *s,
+                routing_filter *keep,
+                const uint8    *keys,
+                uint32          key_len,
+                const uint32   *filter_id,
+                uint64          n,
+                int             threads,
+                uint64         *found)
+{
+   rfr_bench b;
+   memset(&b, 0, sizeof(b));
+   b.s         = s;
+   b.keys      = keys;
+   b.key_len   = key_len;
+   b.keep      = keep;
+   b.filter_id = filter_id;
+   b.n         = n;
+   b.found     = found;
+   return run_threads(&b, threads, probe_worker);
+}

@@ -1,0 +1,218 @@
+"""ctypes binding of the reference's OWN routing filter (TEST INFRASTRUCTURE ONLY).
+
+oracle/_ref/libref_rf.so is vmware/splinterdb's src/routing_filter.c and the page stack it
+runs on (clockcache, mini_allocator, rc_allocator, PackedArray), compiled unmodified from
+/root/reference by oracle/Makefile, with ref_harness.c's in-memory device behind the
+reference's io_ops interface. Only tests/, oracle/gen_ref_golden.py and bench.py's
+cpu_baseline leg use it, as the checker / the CPU baseline. The library is built in this
+container and travels to the GPU box as a built file; where it is absent, `available()`
+is False and its users skip or fall back to the restatement.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_ref", "libref_rf.so")
+
+
+class RoutingFilter(ctypes.Structure):
+    """routing_filter (src/routing_filter.h:66-72), ONDISK = packed: 28 bytes."""
+    _pack_ = 1
+    _fields_ = [("addr", ctypes.c_uint64), ("meta_head", ctypes.c_uint64),
+                ("num_fingerprints", ctypes.c_uint32), ("num_unique", ctypes.c_uint32),
+                ("value_size", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(RoutingFilter) == 28
+
+_lib = None
+
+
+def available():
+    return os.path.exists(LIB_PATH)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        RF = ctypes.POINTER(RoutingFilter)
+        L.rfr_create.restype = vp
+        L.rfr_create.argtypes = [u32, u32, u64, u64]
+        L.rfr_destroy.argtypes = [vp]
+        L.rfr_destroy.restype = None
+        L.rfr_device_io_count.restype = u64
+        L.rfr_device_io_count.argtypes = [vp, i32]
+        L.rfr_max_fingerprints.restype = u64
+        L.rfr_max_fingerprints.argtypes = [vp]
+        L.rfr_filter_add.restype = i32
+        L.rfr_filter_add.argtypes = [vp, RF, RF, vp, u64, u16]
+        L.rfr_filter_image.restype = u32
+        L.rfr_filter_image.argtypes = [vp, RF, vp, u32, vp, ctypes.POINTER(u32)]
+        L.rfr_lookup_keys.argtypes = [vp, RF, vp, u32, u64, vp]
+        L.rfr_lookup_keys.restype = None
+        L.rfr_lookup_keys_async.argtypes = [vp, RF, vp, u32, u64, vp]
+        L.rfr_lookup_keys_async.restype = u64
+        L.rfr_estimate_unique_fp.restype = i32
+        L.rfr_estimate_unique_fp.argtypes = [vp, vp, u64, ctypes.POINTER(u32)]
+        L.rfr_estimate_unique_keys_from_count.restype = u32
+        L.rfr_estimate_unique_keys_from_count.argtypes = [vp, u64]
+        L.rfr_estimate_unique_keys.restype = u32
+        L.rfr_estimate_unique_keys.argtypes = [vp, RF]
+        L.rfr_space_use_bytes.restype = u64
+        L.rfr_space_use_bytes.argtypes = [vp, RF]
+        L.rfr_dec_ref.argtypes = [vp, RF]
+        L.rfr_dec_ref.restype = None
+        L.rfr_get_next_value.restype = u16
+        L.rfr_get_next_value.argtypes = [u64, u16]
+        L.rfr_is_value_found.restype = i32
+        L.rfr_is_value_found.argtypes = [u64, u16]
+        L.rfr_hash_keys.argtypes = [vp, vp, u32, u64, vp]
+        L.rfr_hash_keys.restype = None
+        L.rfr_lookup_var_keys.argtypes = [vp, RF, vp, vp, u64, vp]
+        L.rfr_lookup_var_keys.restype = None
+        L.rfr_hash_var_keys.argtypes = [vp, vp, vp, u64, vp]
+        L.rfr_hash_var_keys.restype = None
+        L.rfr_bench_build.restype = ctypes.c_double
+        L.rfr_bench_build.argtypes = [vp, vp, u32, i32, vp, vp, u32, u16, i32, RF]
+        L.rfr_bench_probe.restype = ctypes.c_double
+        L.rfr_bench_probe.argtypes = [vp, RF, vp, u32, vp, u64, i32, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Image:
+    """A reference-built filter read back as a relocatable image (this repo's form)."""
+
+    def __init__(self, desc, pages, slots):
+        self.desc = desc
+        self.num_fingerprints = desc.num_fingerprints
+        self.num_unique = desc.num_unique
+        self.value_size = desc.value_size
+        self.pages = pages
+        self.slots = slots
+        self.num_pages = pages.size // 4096
+        self.num_indices = slots.size
+
+
+class Stack:
+    """One reference filter stack (heap, in-memory device, rc_allocator, clockcache,
+    routing_config with seed 42 and the default data_config)."""
+
+    def __init__(self, fingerprint_size=26, log_index_size=8, cache_mib=2048, disk_mib=16384):
+        self.lis = log_index_size
+        self.fps = fingerprint_size
+        self.h = lib().rfr_create(fingerprint_size, log_index_size, cache_mib, disk_mib)
+        if not self.h:
+            raise RuntimeError("rfr_create failed")
+
+    def close(self):
+        if self.h:
+            lib().rfr_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def device_writes(self):
+        """pages the cache wrote to the device: 0 while every page stays cached, so every
+        filter page is a fresh cache page (unwritten bytes zero, SURVEY finding 4)"""
+        return int(lib().rfr_device_io_count(self.h, 1))
+
+    def device_reads(self):
+        return int(lib().rfr_device_io_count(self.h, 0))
+
+    def max_fingerprints(self):
+        return int(lib().rfr_max_fingerprints(self.h))
+
+    def add(self, hashes, value=0, old=None):
+        """routing_filter_add over a COPY of hashes (the reference mutates its input)."""
+        fps = np.array(hashes, dtype=np.uint32, copy=True)
+        out = RoutingFilter()
+        rc = lib().rfr_filter_add(self.h, ctypes.byref(old) if old is not None else None,
+                                  ctypes.byref(out), _p(fps) if fps.size else None, fps.size, value)
+        if rc:
+            raise RuntimeError(f"routing_filter_add: platform_status {rc}")
+        return out
+
+    def image(self, desc):
+        if desc.addr == 0:
+            return None
+        lnb = max(int(desc.num_fingerprints).bit_length() - 1, self.lis)
+        ni = 1 << (lnb - self.lis)
+        cap = ni  # at most one data page per index
+        pages = np.zeros(cap * 4096, dtype=np.uint8)
+        slots = np.zeros(ni, dtype=np.uint64)
+        np_ = ctypes.c_uint32(0)
+        got = lib().rfr_filter_image(self.h, ctypes.byref(desc), _p(pages), cap, _p(slots), ctypes.byref(np_))
+        if got != ni:
+            raise RuntimeError("rfr_filter_image failed")
+        return Image(desc, pages[: np_.value * 4096].copy(), slots)
+
+    def lookup_keys(self, desc, keys, key_len=24, use_async=False):
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = k.size // key_len
+        out = np.zeros(n, dtype=np.uint64)
+        if use_async:
+            lib().rfr_lookup_keys_async(self.h, ctypes.byref(desc), _p(k), key_len, n, _p(out))
+        else:
+            lib().rfr_lookup_keys(self.h, ctypes.byref(desc), _p(k), key_len, n, _p(out))
+        return out
+
+    def lookup_var_keys(self, desc, data, offs):
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        o = np.ascontiguousarray(offs, dtype=np.uint64)
+        out = np.zeros(o.size - 1, dtype=np.uint64)
+        lib().rfr_lookup_var_keys(self.h, ctypes.byref(desc), _p(d), _p(o), o.size - 1, _p(out))
+        return out
+
+    def hash_var_keys(self, data, offs):
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        o = np.ascontiguousarray(offs, dtype=np.uint64)
+        out = np.zeros(o.size - 1, dtype=np.uint32)
+        lib().rfr_hash_var_keys(self.h, _p(d), _p(o), o.size - 1, _p(out))
+        return out
+
+    def hash_keys(self, keys, key_len=24):
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = k.size // key_len
+        out = np.zeros(n, dtype=np.uint32)
+        lib().rfr_hash_keys(self.h, _p(k), key_len, n, _p(out))
+        return out
+
+    def estimate_unique_fp(self, descs):
+        arr = (RoutingFilter * max(1, len(descs)))()
+        for i, d in enumerate(descs):
+            arr[i] = d if d is not None else RoutingFilter()
+        out = ctypes.c_uint32(0)
+        rc = lib().rfr_estimate_unique_fp(self.h, ctypes.addressof(arr), len(descs), ctypes.byref(out))
+        if rc:
+            raise RuntimeError(f"estimate_unique_fp: platform_status {rc}")
+        return out.value
+
+    def estimate_unique_keys_from_count(self, num_unique):
+        return int(lib().rfr_estimate_unique_keys_from_count(self.h, num_unique))
+
+    def space_use_bytes(self, desc):
+        return int(lib().rfr_space_use_bytes(self.h, ctypes.byref(desc)))
+
+    def dec_ref(self, desc):
+        lib().rfr_dec_ref(self.h, ctypes.byref(desc))
+
+
+def get_next_value(found_values, last_value):
+    return int(lib().rfr_get_next_value(found_values, last_value))
+
+
+def is_value_found(found_values, value):
+    return bool(lib().rfr_is_value_found(found_values, value))

@@ -201,6 +201,10 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     p.num_new = num_new[f];
     p.old_region = op ? op->num_fp : 0;
     const uint64_t nfp = (uint64_t)p.num_new + p.old_region;
+    if (nfp > rf_amd_max_fingerprints(cfg)) {  // checked before the u32 descriptor field can wrap
+      delete b;
+      return fail(RF_AMD_EINVAL, "num_fingerprints over routing_filter_max_fingerprints (reference: UB)");
+    }
     p.num_fp = (uint32_t)nfp;
     if (p.num_fp == 0) {
       delete b;
@@ -327,9 +331,14 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     return fail(RF_AMD_ENOMEM, "device allocation failed");
   }
   hipStream_t st = e->stream;
+  // Page bytes the reference never writes are zero on a fresh cache page (SURVEY finding 4);
+  // K6 writes every byte of every page it assembles (block bytes and the zero tail), so
+  // this fill only covers reserved pages a build does not use.
+  HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
   if (const char* pz = getenv("RF_AMD_POISON")) {
-    // test hook: fill every work buffer with a pattern, so that a kernel reading memory it
-    // did not write in this build cannot pass the parity tests by reading stale results
+    // test hook: fill every work buffer -- the page images included, after the zero fill
+    // above -- with a pattern, so that a kernel reading memory it did not write in this
+    // build, or leaving page bytes unwritten, cannot pass the parity tests
     const int v = atoi(pz) & 0xff;
     for (DevBuf* d : {&b->d_ent, &b->d_part, &b->d_sorted, &b->d_cb_start, &b->d_idx_cnt, &b->d_idx_start,
                       &b->d_slots, &b->d_lines, &b->d_page_first, &b->d_pages, &b->d_first_old, &b->d_has_old})
@@ -352,7 +361,6 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   UP(b->d_pg_filter, b->pg_filter);
   UP(b->d_idx_filter, b->idx_filter);
 #undef UP
-  HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
   HIPCHK(hipStreamSynchronize(st));
   *out = b;
   return 0;

@@ -308,10 +308,21 @@ def routing_filter_lookup(cfg: RoutingConfig, filt, key: bytes, engine=None):
     return int(routing_filter_lookup_keys(cfg, filt, arr, engine)[0])
 
 
+def _c_int_shl1(v: int) -> int:
+    """`1 << v` on a 32-bit C int as the reference's x86-64 build evaluates it, widened to
+    uint64: the shift count is taken mod 32 (`shl %cl`), and 1 << 31 is INT_MIN, which
+    sign-extends. (Values >= 31 are UB in C; this is the code gcc emits for them.)"""
+    sh = v & 31
+    return 0xFFFFFFFF80000000 if sh == 31 else 1 << sh
+
+
 def routing_filter_get_next_value(found_values: int, last_value: int) -> int:
-    """src/routing_filter.h:94-105 (the reference builds its mask with an int shift)."""
+    """src/routing_filter.h:94-105: `uint64 mask = (1 << last_value) - 1` is int arithmetic
+    (INT_MIN - 1 wraps to INT_MAX), so last_value >= 31 does not mask the way a 64-bit
+    shift would."""
     if last_value != ROUTING_NOT_FOUND:
-        mask = ((1 << last_value) - 1) & 0xFFFFFFFFFFFFFFFF
+        m = _c_int_shl1(last_value)
+        mask = 0x7FFFFFFF if m == 0xFFFFFFFF80000000 else m - 1
         found_values &= mask
     if found_values == 0:
         return ROUTING_NOT_FOUND
@@ -319,7 +330,8 @@ def routing_filter_get_next_value(found_values: int, last_value: int) -> int:
 
 
 def routing_filter_is_value_found(found_values: int, value: int) -> bool:
-    return (found_values & (1 << value)) != 0
+    """src/routing_filter.h:107-111: `found_values & (1 << value)` with an int shift."""
+    return (found_values & _c_int_shl1(value)) != 0
 
 
 def routing_filter_max_fingerprints(cfg: RoutingConfig) -> int:
