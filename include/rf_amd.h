@@ -128,10 +128,11 @@ uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
  * between them (rf_amd_batch_timings_back: back = 0 is the latest round). */
 int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
 int rf_amd_batch_timings_back(rf_amd_batch *b, uint32_t back, float *ms, uint32_t n);
-/* diagnostics: truncate later probes after 1 = hashing, 2 = the probe-line load
- * (results are then NOT found_values); 0 restores normal probes. Bits 8+: cap the probe
- * kernel at that many waves per SIMD (occupancy experiments). */
-void rf_amd_debug_probe_ablate(uint32_t mode);
+/* diagnostics library only (librf_amd_stamps.so; the product library returns EINVAL for a
+ * nonzero mode): truncate later probes after 1 = hashing, 2 = the probe-line load
+ * (results are then NOT found_values); 0 restores normal probes. Bits 8-15: cap the probe
+ * kernel at that many waves per SIMD; bits 16-23: probes per lane (experiments). */
+int rf_amd_debug_probe_ablate(uint32_t mode);
 /* diagnostics: the batch's device-only probe lines (64 B each). read_lines copies them to
  * host (h_lines == NULL: only *num_lines is set); rebuild_lines re-cuts them from the
  * filter images with the image-upload kernel (k_plines), so a test can check that the

@@ -31,7 +31,9 @@ extern "C" int rf_launch_probe(const LaunchArgs* a, int kind, const void* in0, c
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found);
 
 static thread_local std::string g_err;
-static uint32_t g_probe_ablate = 0;  // diagnostics only (rf_amd_debug_probe_ablate)
+#ifdef RF_PHASE_STAMPS
+static uint32_t g_probe_ablate = 0;  // diagnostics library only (rf_amd_debug_probe_ablate)
+#endif
 static int fail(int rc, const std::string& msg) {
   g_err = msg;
   return rc;
@@ -486,9 +488,11 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   (void)hipGetLastError();
   LaunchArgs a = make_args(b, st);
   a.probe_runs = d_runs;
+#ifdef RF_PHASE_STAMPS
   a.ablate = g_probe_ablate & 0xff;
   a.occ = (g_probe_ablate >> 8) & 0xff;
   a.ppl = (g_probe_ablate >> 16) & 0xff;
+#endif
   int rc = rf_launch_probe(&a, kind, in0, offs, key_len, fid, n, found);
   if (rc) return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
   return 0;
@@ -541,9 +545,17 @@ extern "C" int rf_amd_batch_probe_hashes_runs(rf_amd_batch* b, const uint32_t* d
   return probe_runs(b, IN_HASH, d_hashes, 4, h_counts, d_found, stream);
 }
 
-// Diagnostic: low byte 1 = hash only, 2 = + probe record; 0 = normal probe. Bits 8+: cap
-// the probe kernel at that many waves per SIMD via LDS padding (occupancy experiments).
-extern "C" void rf_amd_debug_probe_ablate(uint32_t mode) { g_probe_ablate = mode; }
+// Diagnostic (diagnostics library only; EINVAL in the product): low byte 1 = hash only,
+// 2 = + probe line load; 0 = normal probe. Bits 8-15: cap the probe kernel at that many
+// waves per SIMD via LDS padding; bits 16-23: probes per lane.
+extern "C" int rf_amd_debug_probe_ablate(uint32_t mode) {
+#ifdef RF_PHASE_STAMPS
+  g_probe_ablate = mode;
+  return 0;
+#else
+  return mode ? fail(RF_AMD_EINVAL, "probe ablation exists only in the diagnostics library") : 0;
+#endif
+}
 
 extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid);
 extern "C" int rf_amd_debug_phase_buffer(void* d_buf, uint32_t kernel) {

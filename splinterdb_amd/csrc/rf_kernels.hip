@@ -301,6 +301,13 @@ __device__ uint32_t g_dbg_kid = 0;
 // Compiled in only for the diagnostics library (RF_PHASE_STAMPS, build.py stamps=True):
 // reading the stamp buffer pointer is a vector load whose wait (vmcnt(0)) would also wait
 // for every load or atomic the kernel has in flight at that point.
+// Probe ablation / occupancy experiments (rf_amd_debug_probe_ablate) exist only in the
+// diagnostics library as well; the product's k_probe has no such branches.
+#ifdef RF_PHASE_STAMPS
+#define RF_DIAG 1
+#else
+#define RF_DIAG 0
+#endif
 #ifdef RF_PHASE_STAMPS
 #define DBG_PHASE_K(kid, k)                                                  \
   do {                                                                       \
@@ -2341,10 +2348,14 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
                                                     uint64_t* __restrict__ found, uint32_t fp_size,
                                                     uint32_t seed, uint32_t lis, uint32_t page_size,
                                                     uint32_t num_filters, uint32_t ablate) {
+#if RF_DIAG
   if constexpr (OCC_LDS > 0) {
     __shared__ uint32_t s_pad[OCC_LDS / 4];
     if (ablate == 0xdead) s_pad[threadIdx.x] = 0;  // keeps the pad allocated
   }
+#else
+  (void)ablate;
+#endif
   const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (PROBE_NT * PPL) + threadIdx.x;
   uint32_t h[PPL], fid[PPL];
   constexpr bool WAVE_KEYS = KIND == IN_KEYS24 && PPL == 1 && OCC_LDS == 0;
@@ -2443,7 +2454,12 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     const uint32_t fp = h[q] >> (32 - fp_size);
     bucket[q] = rem >= 32 ? 0u : fp >> rem;  // index << lis | bucket in index
     remainder[q] = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-    if (!pp[q].w && lgl && ablate != 1) {
+#if RF_DIAG
+    const bool load_line = !pp[q].w && lgl && ablate != 1;
+#else
+    const bool load_line = !pp[q].w && lgl;
+#endif
+    if (load_line) {
       const v4u* lp = reinterpret_cast<const v4u*>(lines + ((uint64_t)pp[q].y + (bucket[q] >> (lgl - 1))) * 4);
 #pragma unroll
       for (int k = 0; k < 4; k++) Q[q][k] = lp[k];
@@ -2459,10 +2475,12 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     uint64_t r = 0;
     if (pp[q].w) {
       r = 0;
+#if RF_DIAG
     } else if (ablate == 1) {  // diagnostic: key stream + hash only
       r = h[q];
     } else if (ablate == 2) {  // diagnostic: + the line load
       r = (uint64_t)Q[q][0].x ^ Q[q][3].w ^ h[q];
+#endif
     } else {
       const uint32_t vs = pp[q].x & 0xff, rvs = (pp[q].x >> 16) & 0xff, lgl = pp[q].x >> 24;
       const uint32_t G = lgl ? 1u << (lgl - 1) : 1u;
@@ -2625,10 +2643,15 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found) {
   const LaunchArgs& a = *pa;
   if (n == 0) return 0;
+#if RF_DIAG
   const int ppl = a.ppl ? (int)a.ppl : PROBE_PPL;
+#else
+  const int ppl = PROBE_PPL;
+#endif
   dim3 g((uint32_t)((n + PROBE_NT * ppl - 1) / (PROBE_NT * ppl))), b(PROBE_NT);
   REC(EV_P_START);
 #define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
+#if RF_DIAG
   if (kind == IN_KEYS24 && (a.occ || a.ppl)) {  // experiment variants: waves/SIMD cap, probes per lane
     const int o = a.occ ? (int)a.occ : 8;
     if (ppl == 2) {
@@ -2640,7 +2663,9 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
       else if (o == 4) PK(IN_KEYS24, 38 * 1024, 1); else if (o == 3) PK(IN_KEYS24, 50 * 1024, 1);
       else PK(IN_KEYS24, 70 * 1024, 1);
     }
-  } else {
+  } else
+#endif
+  {
     // production: no LDS pad (8 waves/SIMD). The line probe is bound by outstanding random
     // line fetches (latency x concurrency): 8 waves 1.14 ms, 6 waves 1.20, 5 1.27, 4 1.41
     // at C2 (tools/line_sigma.py). The record-era probe preferred 6 (L2 thrash).

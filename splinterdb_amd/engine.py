@@ -118,7 +118,6 @@ def load_library(build_if_missing=True):
     L.rf_amd_debug_read_lines.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
     L.rf_amd_debug_rebuild_lines.argtypes = [vp]
     L.rf_amd_debug_phase_buffer.argtypes = [vp, u32]
-    L.rf_amd_debug_probe_ablate.restype = None
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
     L.rf_amd_filter_add.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),
