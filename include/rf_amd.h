@@ -102,6 +102,16 @@ int rf_amd_batch_probe_keys_runs(rf_amd_batch *b, const void *d_keys, uint32_t k
 int rf_amd_batch_probe_hashes_runs(rf_amd_batch *b, const uint32_t *d_hashes, const uint64_t *h_counts,
                                    uint64_t *d_found, void *stream);
 
+/* Host-buffer forms (synchronous; inputs staged through the engine's pinned buffer), for
+ * callers that hold no device memory, e.g. the routing_filter.h shim
+ * (shim/routing_filter_amd.c): build batch b from its keys_total host hashes, and probe n
+ * host hashes (filter h_filter_id[i], or filter 0 when NULL) into h_found. */
+int rf_amd_batch_build_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes);
+int rf_amd_batch_probe_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes, const uint32_t *h_filter_id,
+                                   uint64_t n, uint64_t *h_found);
+/* device-allocation pool of the engine (batch work buffers are recycled across batches) */
+int rf_amd_engine_pool_stats(rf_amd_engine *e, uint64_t *pooled_bytes, uint64_t *hits, uint64_t *misses);
+
 /* synchronising accessors */
 int rf_amd_batch_info(rf_amd_batch *b, uint32_t f, rf_amd_filter_info *out);
 /* copy filter f's image to host: num_pages*page_size bytes and num_indices slots */
@@ -258,6 +268,10 @@ int rf_amd_filter_verify(rf_amd_engine *e, const rf_amd_config *cfg, const rf_am
                          const void *keys, uint32_t key_len, uint64_t n, uint16_t value,
                          uint64_t *num_missing);
 int rf_amd_filter_print(const rf_amd_config *cfg, const rf_amd_image *filter, void *out_file);
+/* the same text with the reference's absolute addresses: the filter's index extent address
+ * and each index slot as stored on the index pages (src/routing_filter.c:1201-1226) */
+int rf_amd_filter_print_abs(const rf_amd_config *cfg, const rf_amd_image *filter, uint64_t filter_addr,
+                            const uint64_t *abs_slots, void *out_file);
 
 /* host-side helpers mirroring routing_filter.h (no GPU work) */
 uint64_t rf_amd_max_fingerprints(const rf_amd_config *cfg);              /* .h:120-127  */

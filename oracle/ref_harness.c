@@ -448,6 +448,82 @@ rfr_lookup_keys_async(rfr_stack      *s,
    return yields;
 }
 
+static void
+count_callback(void *arg)
+{
+   __atomic_fetch_add((uint64 *)arg, 1, __ATOMIC_RELAXED);
+}
+
+/*
+ * n lookups issued as n concurrent coroutine states (the trunk's async lookup pattern):
+ * every state is started once, then all are polled until done. Returns the number of
+ * callbacks fired; *running = states whose first call returned ASYNC_STATUS_RUNNING.
+ * filter_id[i] picks the filter of key i from filters[].
+ */
+uint64
+rfr_lookup_keys_async_many(rfr_stack      *s,
+                           routing_filter *filters,
+                           const uint32   *filter_id,
+                           const uint8    *keys,
+                           uint32          key_len,
+                           uint64          n,
+                           uint64         *found,
+                           uint64         *running)
+{
+   routing_filter_lookup_async_state *st = calloc(n ? n : 1, sizeof(*st));
+   uint64                             cb = 0;
+   *running                              = 0;
+   for (uint64 i = 0; i < n; i++) {
+      key k = key_create(FALSE, key_len, keys + i * key_len);
+      routing_filter_lookup_async_state_init(&st[i], (cache *)&s->cc, &s->rcfg,
+                                             filters[filter_id ? filter_id[i] : 0], k,
+                                             &found[i], count_callback, &cb);
+      if (routing_filter_lookup_async(&st[i]) != ASYNC_STATUS_DONE) {
+         (*running)++;
+      }
+   }
+   for (uint64 i = 0; i < n; i++) {
+      while (routing_filter_lookup_async(&st[i]) != ASYNC_STATUS_DONE) {
+         cache_cleanup((cache *)&s->cc);
+      }
+      if (!SUCCESS(st[i].__async_result)) {
+         found[i] = UINT64_MAX;
+      }
+   }
+   free(st);
+   return cb;
+}
+
+/* the shim's flush counters (weak: absent from the reference's own library) */
+__attribute__((weak)) void
+routing_filter_amd_async_stats(uint64 *batches, uint64 *probes);
+
+int
+rfr_async_stats(uint64 *batches, uint64 *probes)
+{
+   if (!routing_filter_amd_async_stats) {
+      *batches = *probes = 0;
+      return 0;
+   }
+   routing_filter_amd_async_stats(batches, probes);
+   return 1;
+}
+
+/* routing_filter_print of the linked implementation, to stdout */
+void
+rfr_print(rfr_stack *s, routing_filter *f)
+{
+   routing_filter_print((cache *)&s->cc, &s->rcfg, f);
+   fflush(stdout);
+}
+
+/* one raw cache page (all page_size bytes) at a disk address */
+void
+rfr_read_page(rfr_stack *s, uint64 addr, uint8 *dst)
+{
+   read_page(s, addr, dst);
+}
+
 int
 rfr_estimate_unique_fp(rfr_stack *s, routing_filter *filters, uint64 num, uint32 *out)
 {

@@ -15,6 +15,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_ref", "libref_rf.so")
+# the same harness and page stack with shim/routing_filter_amd.c (the MI355X drop-in) in
+# place of routing_filter.c
+SHIM_PATH = os.path.join(HERE, "_ref", "libshim_rf.so")
 
 
 class RoutingFilter(ctypes.Structure):
@@ -27,17 +30,16 @@ class RoutingFilter(ctypes.Structure):
 
 assert ctypes.sizeof(RoutingFilter) == 28
 
-_lib = None
+_libs = {}
 
 
-def available():
-    return os.path.exists(LIB_PATH)
+def available(path=LIB_PATH):
+    return os.path.exists(path)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        L = ctypes.CDLL(LIB_PATH)
+def lib(path=LIB_PATH):
+    if path not in _libs:
+        L = ctypes.CDLL(path)
         vp, u16, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
         RF = ctypes.POINTER(RoutingFilter)
         L.rfr_create.restype = vp
@@ -80,8 +82,16 @@ def lib():
         L.rfr_bench_build.argtypes = [vp, vp, u32, i32, vp, vp, u32, u16, i32, RF]
         L.rfr_bench_probe.restype = ctypes.c_double
         L.rfr_bench_probe.argtypes = [vp, RF, vp, u32, vp, u64, i32, vp]
-        _lib = L
-    return _lib
+        L.rfr_lookup_keys_async_many.restype = u64
+        L.rfr_lookup_keys_async_many.argtypes = [vp, vp, vp, vp, u32, u64, vp, ctypes.POINTER(u64)]
+        L.rfr_async_stats.restype = i32
+        L.rfr_async_stats.argtypes = [ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.rfr_print.argtypes = [vp, RF]
+        L.rfr_print.restype = None
+        L.rfr_read_page.argtypes = [vp, u64, vp]
+        L.rfr_read_page.restype = None
+        _libs[path] = L
+    return _libs[path]
 
 
 def _p(a):
@@ -106,16 +116,18 @@ class Stack:
     """One reference filter stack (heap, in-memory device, rc_allocator, clockcache,
     routing_config with seed 42 and the default data_config)."""
 
-    def __init__(self, fingerprint_size=26, log_index_size=8, cache_mib=2048, disk_mib=16384):
+    def __init__(self, fingerprint_size=26, log_index_size=8, cache_mib=2048, disk_mib=16384, path=LIB_PATH):
+        """path: LIB_PATH (the reference's routing_filter.c) or SHIM_PATH (the drop-in)"""
         self.lis = log_index_size
         self.fps = fingerprint_size
-        self.h = lib().rfr_create(fingerprint_size, log_index_size, cache_mib, disk_mib)
+        self.L = lib(path)
+        self.h = self.L.rfr_create(fingerprint_size, log_index_size, cache_mib, disk_mib)
         if not self.h:
             raise RuntimeError("rfr_create failed")
 
     def close(self):
         if self.h:
-            lib().rfr_destroy(self.h)
+            self.L.rfr_destroy(self.h)
             self.h = None
 
     def __enter__(self):
@@ -127,19 +139,19 @@ class Stack:
     def device_writes(self):
         """pages the cache wrote to the device: 0 while every page stays cached, so every
         filter page is a fresh cache page (unwritten bytes zero, SURVEY finding 4)"""
-        return int(lib().rfr_device_io_count(self.h, 1))
+        return int(self.L.rfr_device_io_count(self.h, 1))
 
     def device_reads(self):
-        return int(lib().rfr_device_io_count(self.h, 0))
+        return int(self.L.rfr_device_io_count(self.h, 0))
 
     def max_fingerprints(self):
-        return int(lib().rfr_max_fingerprints(self.h))
+        return int(self.L.rfr_max_fingerprints(self.h))
 
     def add(self, hashes, value=0, old=None):
         """routing_filter_add over a COPY of hashes (the reference mutates its input)."""
         fps = np.array(hashes, dtype=np.uint32, copy=True)
         out = RoutingFilter()
-        rc = lib().rfr_filter_add(self.h, ctypes.byref(old) if old is not None else None,
+        rc = self.L.rfr_filter_add(self.h, ctypes.byref(old) if old is not None else None,
                                   ctypes.byref(out), _p(fps) if fps.size else None, fps.size, value)
         if rc:
             raise RuntimeError(f"routing_filter_add: platform_status {rc}")
@@ -154,7 +166,7 @@ class Stack:
         pages = np.zeros(cap * 4096, dtype=np.uint8)
         slots = np.zeros(ni, dtype=np.uint64)
         np_ = ctypes.c_uint32(0)
-        got = lib().rfr_filter_image(self.h, ctypes.byref(desc), _p(pages), cap, _p(slots), ctypes.byref(np_))
+        got = self.L.rfr_filter_image(self.h, ctypes.byref(desc), _p(pages), cap, _p(slots), ctypes.byref(np_))
         if got != ni:
             raise RuntimeError("rfr_filter_image failed")
         return Image(desc, pages[: np_.value * 4096].copy(), slots)
@@ -164,30 +176,30 @@ class Stack:
         n = k.size // key_len
         out = np.zeros(n, dtype=np.uint64)
         if use_async:
-            lib().rfr_lookup_keys_async(self.h, ctypes.byref(desc), _p(k), key_len, n, _p(out))
+            self.L.rfr_lookup_keys_async(self.h, ctypes.byref(desc), _p(k), key_len, n, _p(out))
         else:
-            lib().rfr_lookup_keys(self.h, ctypes.byref(desc), _p(k), key_len, n, _p(out))
+            self.L.rfr_lookup_keys(self.h, ctypes.byref(desc), _p(k), key_len, n, _p(out))
         return out
 
     def lookup_var_keys(self, desc, data, offs):
         d = np.ascontiguousarray(data, dtype=np.uint8)
         o = np.ascontiguousarray(offs, dtype=np.uint64)
         out = np.zeros(o.size - 1, dtype=np.uint64)
-        lib().rfr_lookup_var_keys(self.h, ctypes.byref(desc), _p(d), _p(o), o.size - 1, _p(out))
+        self.L.rfr_lookup_var_keys(self.h, ctypes.byref(desc), _p(d), _p(o), o.size - 1, _p(out))
         return out
 
     def hash_var_keys(self, data, offs):
         d = np.ascontiguousarray(data, dtype=np.uint8)
         o = np.ascontiguousarray(offs, dtype=np.uint64)
         out = np.zeros(o.size - 1, dtype=np.uint32)
-        lib().rfr_hash_var_keys(self.h, _p(d), _p(o), o.size - 1, _p(out))
+        self.L.rfr_hash_var_keys(self.h, _p(d), _p(o), o.size - 1, _p(out))
         return out
 
     def hash_keys(self, keys, key_len=24):
         k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
         n = k.size // key_len
         out = np.zeros(n, dtype=np.uint32)
-        lib().rfr_hash_keys(self.h, _p(k), key_len, n, _p(out))
+        self.L.rfr_hash_keys(self.h, _p(k), key_len, n, _p(out))
         return out
 
     def estimate_unique_fp(self, descs):
@@ -195,19 +207,58 @@ class Stack:
         for i, d in enumerate(descs):
             arr[i] = d if d is not None else RoutingFilter()
         out = ctypes.c_uint32(0)
-        rc = lib().rfr_estimate_unique_fp(self.h, ctypes.addressof(arr), len(descs), ctypes.byref(out))
+        rc = self.L.rfr_estimate_unique_fp(self.h, ctypes.addressof(arr), len(descs), ctypes.byref(out))
         if rc:
             raise RuntimeError(f"estimate_unique_fp: platform_status {rc}")
         return out.value
 
     def estimate_unique_keys_from_count(self, num_unique):
-        return int(lib().rfr_estimate_unique_keys_from_count(self.h, num_unique))
+        return int(self.L.rfr_estimate_unique_keys_from_count(self.h, num_unique))
 
     def space_use_bytes(self, desc):
-        return int(lib().rfr_space_use_bytes(self.h, ctypes.byref(desc)))
+        return int(self.L.rfr_space_use_bytes(self.h, ctypes.byref(desc)))
+
+    def lookup_keys_async_many(self, descs, keys, filter_id=None, key_len=24):
+        """len(keys) lookups as concurrent routing_filter_lookup_async states (each started
+        once, then all polled): (found, callbacks fired, states that first returned RUNNING)"""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = k.size // key_len
+        arr = (RoutingFilter * max(1, len(descs)))(*descs)
+        fid = None if filter_id is None else np.ascontiguousarray(filter_id, dtype=np.uint32)
+        out = np.zeros(n, dtype=np.uint64)
+        running = ctypes.c_uint64(0)
+        cb = self.L.rfr_lookup_keys_async_many(self.h, ctypes.addressof(arr), None if fid is None else _p(fid),
+                                               _p(k), key_len, n, _p(out), ctypes.byref(running))
+        return out, int(cb), int(running.value)
+
+    def async_stats(self):
+        b, p = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self.L.rfr_async_stats(ctypes.byref(b), ctypes.byref(p))
+        return int(b.value), int(p.value)
+
+    def print_text(self, desc):
+        """routing_filter_print's output (C stdout captured through a temporary file)"""
+        import sys
+        import tempfile
+        sys.stdout.flush()
+        fd = os.dup(1)
+        with tempfile.TemporaryFile() as tmp:
+            os.dup2(tmp.fileno(), 1)
+            try:
+                self.L.rfr_print(self.h, ctypes.byref(desc))
+            finally:
+                os.dup2(fd, 1)
+                os.close(fd)
+            tmp.seek(0)
+            return tmp.read().decode()
+
+    def read_page(self, addr):
+        out = np.zeros(4096, dtype=np.uint8)
+        self.L.rfr_read_page(self.h, addr, _p(out))
+        return out
 
     def dec_ref(self, desc):
-        lib().rfr_dec_ref(self.h, ctypes.byref(desc))
+        self.L.rfr_dec_ref(self.h, ctypes.byref(desc))
 
 
 def get_next_value(found_values, last_value):

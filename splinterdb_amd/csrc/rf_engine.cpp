@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -46,20 +48,86 @@ static int fail(int rc, const std::string& msg) {
                   std::string(#x) + ": " + hipGetErrorString(_e));                    \
   } while (0)
 
+// Device allocations of an engine's batches are recycled through a pool: SplinterDB builds
+// a new set of filters on every compaction, so in steady state rf_amd_batch_create finds
+// its ~25 work buffers here instead of calling hipMalloc. Sizes are rounded up to classes
+// of 1/8 of a power of two (at most 12.5 % slack); a block returns to the pool when its
+// batch is destroyed (after a device synchronize, so no kernel still uses it) unless the
+// pool already holds RF_AMD_POOL_MIB (default 32768) MiB.
+struct DevPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free_blocks;
+  size_t pooled = 0, limit = 0;
+  uint64_t hits = 0, misses = 0;
+  static size_t size_class(size_t bytes) {
+    if (bytes <= 4096) return 4096;
+    const int lg = 63 - __builtin_clzll((unsigned long long)bytes);
+    const size_t step = (size_t)1 << (lg - 3);
+    return (bytes + step - 1) / step * step;
+  }
+  void* take(size_t cls) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = free_blocks.find(cls);
+    if (it == free_blocks.end()) {
+      misses++;
+      return nullptr;
+    }
+    void* p = it->second;
+    free_blocks.erase(it);
+    pooled -= cls;
+    hits++;
+    return p;
+  }
+  bool give(void* p, size_t cls) {
+    std::lock_guard<std::mutex> g(mu);
+    if (pooled + cls > limit) return false;
+    free_blocks.emplace(cls, p);
+    pooled += cls;
+    return true;
+  }
+  void drain() {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& kv : free_blocks) (void)hipFree(kv.second);
+    free_blocks.clear();
+    pooled = 0;
+  }
+};
+
+// host-buffer entry points stage through these (rf_amd_batch_*_host): pinned host memory
+// and a device buffer per engine, grown on demand, one caller at a time
+struct HostStage {
+  std::mutex mu;
+  void* h = nullptr;
+  void* d = nullptr;
+  size_t cap = 0;
+};
+
 struct rf_amd_engine {
   int device;
   hipStream_t stream;
+  DevPool pool;
+  HostStage stage;
 };
 
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+  DevPool* pool = nullptr;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p && !(pool && pool->give(p, n))) (void)hipFree(p);
+    p = nullptr;
   }
-  int alloc(size_t bytes) {
-    n = bytes ? bytes : 16;
+  int alloc(size_t bytes, DevPool* from = nullptr) {
+    release();
+    pool = from;
+    n = from ? DevPool::size_class(bytes ? bytes : 16) : (bytes ? bytes : 16);
+    if (from && (p = from->take(n)) != nullptr) return 0;
     hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess && from) {  // the pool may hold what this needs: give it back, retry
+      from->drain();
+      e = hipMalloc(&p, n);
+    }
     if (e != hipSuccess) {
       p = nullptr;
       return fail(RF_AMD_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -104,7 +172,12 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
     return fail(RF_AMD_ENODEV, "no HIP device: the routing-filter engine has no CPU fallback");
   if (device < 0 || device >= n) return fail(RF_AMD_EINVAL, "bad device ordinal");
   HIPCHK(hipSetDevice(device));
-  auto* e = new rf_amd_engine{device, nullptr};
+  auto* e = new rf_amd_engine();
+  e->device = device;
+  {
+    const char* lim = getenv("RF_AMD_POOL_MIB");
+    e->pool.limit = (size_t)(lim ? atoll(lim) : 32768) << 20;
+  }
   // a BLOCKING stream: ordered with the legacy null stream that torch and most callers use
   if (hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess) {
     delete e;
@@ -119,6 +192,9 @@ extern "C" void rf_amd_engine_destroy(rf_amd_engine* e) {
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
   (void)hipStreamDestroy(e->stream);
+  e->pool.drain();
+  if (e->stage.h) (void)hipHostFree(e->stage.h);
+  if (e->stage.d) (void)hipFree(e->stage.d);
   delete e;
 }
 
@@ -298,35 +374,36 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   b->NL = line_base;
   const size_t esz = b->wide ? 8 : 4;
   int rc = 0;
-  rc |= b->d_plans.alloc(sizeof(FilterPlan) * num_filters);
-  rc |= b->d_pplans.alloc(16ull * num_filters);
-  rc |= b->d_outs.alloc(sizeof(FilterOut) * num_filters);
-  rc |= b->d_ent.alloc(esz * b->E + 64);
-  rc |= b->d_part.alloc(esz * b->E + 64);
-  if (b->wide) rc |= b->d_sorted.alloc(4 * b->E + 64);
-  rc |= b->d_cb_count.alloc(4 * b->CB);
-  rc |= b->d_cb_start.alloc(4 * b->CB);
-  rc |= b->d_cb_cursor.alloc(4 * b->CB);
-  rc |= b->d_cb_filter.alloc(4 * b->CB);
-  rc |= b->d_overflow.alloc(4 * (b->CB + 1));
-  rc |= b->d_spill.alloc(4);
-  rc |= b->d_idx_cnt.alloc(4 * b->I);
-  rc |= b->d_idx_start.alloc(4 * b->I);
-  rc |= b->d_slots.alloc(8 * b->I);
-  rc |= b->d_lines.alloc(64ull * b->NL + 64);
-  rc |= b->d_idx_filter.alloc(4ull * b->I);
-  rc |= b->d_page_first.alloc(4 * b->PF);
-  rc |= b->d_pg_filter.alloc(4 * b->PS);
-  rc |= b->d_pages.alloc((size_t)b->PS * P + 256);
-  rc |= b->d_tile_filter.alloc(4 * b->tile_filter.size());
-  rc |= b->d_tile_start.alloc(4 * b->tile_start.size());
-  rc |= b->d_old_tile_filter.alloc(4 * b->old_tile_filter.size());
-  rc |= b->d_old_tile_start.alloc(4 * b->old_tile_start.size());
+  DevPool* pool = &e->pool;
+  rc |= b->d_plans.alloc(sizeof(FilterPlan) * num_filters, pool);
+  rc |= b->d_pplans.alloc(16ull * num_filters, pool);
+  rc |= b->d_outs.alloc(sizeof(FilterOut) * num_filters, pool);
+  rc |= b->d_ent.alloc(esz * b->E + 64, pool);
+  rc |= b->d_part.alloc(esz * b->E + 64, pool);
+  if (b->wide) rc |= b->d_sorted.alloc(4 * b->E + 64, pool);
+  rc |= b->d_cb_count.alloc(4 * b->CB, pool);
+  rc |= b->d_cb_start.alloc(4 * b->CB, pool);
+  rc |= b->d_cb_cursor.alloc(4 * b->CB, pool);
+  rc |= b->d_cb_filter.alloc(4 * b->CB, pool);
+  rc |= b->d_overflow.alloc(4 * (b->CB + 1), pool);
+  rc |= b->d_spill.alloc(4, pool);
+  rc |= b->d_idx_cnt.alloc(4 * b->I, pool);
+  rc |= b->d_idx_start.alloc(4 * b->I, pool);
+  rc |= b->d_slots.alloc(8 * b->I, pool);
+  rc |= b->d_lines.alloc(64ull * b->NL + 64, pool);
+  rc |= b->d_idx_filter.alloc(4ull * b->I, pool);
+  rc |= b->d_page_first.alloc(4 * b->PF, pool);
+  rc |= b->d_pg_filter.alloc(4 * b->PS, pool);
+  rc |= b->d_pages.alloc((size_t)b->PS * P + 256, pool);
+  rc |= b->d_tile_filter.alloc(4 * b->tile_filter.size(), pool);
+  rc |= b->d_tile_start.alloc(4 * b->tile_start.size(), pool);
+  rc |= b->d_old_tile_filter.alloc(4 * b->old_tile_filter.size(), pool);
+  rc |= b->d_old_tile_start.alloc(4 * b->old_tile_start.size(), pool);
   if (b->wide) {
-    rc |= b->d_old_cnt.alloc(4 * MAX_INDICES);
-    rc |= b->d_old_pos.alloc(4 * MAX_INDICES);
-    rc |= b->d_first_old.alloc(4 * b->I);
-    rc |= b->d_has_old.alloc(4 * b->I);
+    rc |= b->d_old_cnt.alloc(4 * MAX_INDICES, pool);
+    rc |= b->d_old_pos.alloc(4 * MAX_INDICES, pool);
+    rc |= b->d_first_old.alloc(4 * b->I, pool);
+    rc |= b->d_has_old.alloc(4 * b->I, pool);
   }
   if (rc) {
     delete b;
@@ -371,8 +448,19 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
 extern "C" void rf_amd_batch_destroy(rf_amd_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->eng->device);
-  (void)hipStreamSynchronize(b->eng->stream);
+  // work on a caller's stream may still read the batch: its blocks go back to the pool only
+  // once the device is idle (what hipFree would have waited for)
+  (void)hipDeviceSynchronize();
   delete b;
+}
+
+extern "C" int rf_amd_engine_pool_stats(rf_amd_engine* e, uint64_t* pooled_bytes, uint64_t* hits, uint64_t* misses) {
+  if (!e) return fail(RF_AMD_EINVAL, "null engine");
+  std::lock_guard<std::mutex> g(e->pool.mu);
+  if (pooled_bytes) *pooled_bytes = e->pool.pooled;
+  if (hits) *hits = e->pool.hits;
+  if (misses) *misses = e->pool.misses;
+  return 0;
 }
 
 extern "C" uint32_t rf_amd_batch_num_filters(const rf_amd_batch* b) { return b ? b->F : 0; }
@@ -424,6 +512,10 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.events = b->events.empty() ? nullptr : reinterpret_cast<void**>(b->events.data() + (size_t)b->ev_set * NUM_EVENTS);
   return a;
 }
+
+static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
+                    const uint32_t* fid, uint64_t n, uint64_t* found, void* stream,
+                    const uint64_t* d_runs = nullptr);
 
 static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
                     void* stream) {
@@ -478,9 +570,81 @@ extern "C" int rf_amd_batch_build_hashes(rf_amd_batch* b, const uint32_t* d_hash
   return do_build(b, IN_HASH, d_hashes, nullptr, 4, stream);
 }
 
+// the engine's host staging area, grown to `bytes`; the caller holds e->stage.mu
+static int stage_reserve(rf_amd_engine* e, size_t bytes) {
+  HostStage& s = e->stage;
+  if (s.cap >= bytes) return 0;
+  if (s.h) (void)hipHostFree(s.h);
+  if (s.d) (void)hipFree(s.d);
+  s.h = s.d = nullptr;
+  s.cap = 0;
+  const size_t c = std::max<size_t>(bytes, (size_t)1 << 20);
+  if (hipHostMalloc(&s.h, c, hipHostMallocDefault) != hipSuccess) {
+    s.h = nullptr;
+    return fail(RF_AMD_ENOMEM, "pinned staging allocation failed");
+  }
+  if (hipMalloc(&s.d, c) != hipSuccess) {
+    (void)hipHostFree(s.h);
+    s.h = nullptr;
+    return fail(RF_AMD_ENOMEM, "device staging allocation failed");
+  }
+  s.cap = c;
+  return 0;
+}
+
+// Host-buffer forms for callers that hold no device memory (the routing_filter.h shim,
+// shim/routing_filter_amd.c): inputs are staged through the engine's pinned buffer on the
+// engine stream, and the call returns once the results are complete.
+extern "C" int rf_amd_batch_build_hashes_host(rf_amd_batch* b, const uint32_t* h_hashes) {
+  if (!b) return fail(RF_AMD_EINVAL, "null batch");
+  if (b->keys_total && !h_hashes) return fail(RF_AMD_EINVAL, "null hashes");
+  rf_amd_engine* e = b->eng;
+  HIPCHK(hipSetDevice(e->device));
+  std::lock_guard<std::mutex> g(e->stage.mu);
+  const size_t bytes = 4ull * b->keys_total;
+  if (int rc = stage_reserve(e, bytes + 16)) return rc;
+  if (bytes) {
+    memcpy(e->stage.h, h_hashes, bytes);
+    HIPCHK(hipMemcpyAsync(e->stage.d, e->stage.h, bytes, hipMemcpyHostToDevice, e->stream));
+  }
+  if (int rc = do_build(b, IN_HASH, e->stage.d, nullptr, 4, e->stream)) return rc;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+extern "C" int rf_amd_batch_probe_hashes_host(rf_amd_batch* b, const uint32_t* h_hashes, const uint32_t* h_filter_id,
+                                              uint64_t n, uint64_t* h_found) {
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "probe on an unbuilt batch");
+  if (n == 0) return 0;
+  if (!h_hashes || !h_found) return fail(RF_AMD_EINVAL, "null probe buffer");
+  rf_amd_engine* e = b->eng;
+  HIPCHK(hipSetDevice(e->device));
+  std::lock_guard<std::mutex> g(e->stage.mu);
+  // [hashes 4n | filter ids 4n | found 8n], found 8-byte aligned
+  if (int rc = stage_reserve(e, 16ull * n + 16)) return rc;
+  uint8_t* hh = static_cast<uint8_t*>(e->stage.h);
+  uint8_t* dd = static_cast<uint8_t*>(e->stage.d);
+  const size_t o_fid = 4 * n, o_found = (8 * n + 7) & ~7ull;
+  memcpy(hh, h_hashes, 4 * n);
+  if (h_filter_id) {
+    memcpy(hh + o_fid, h_filter_id, 4 * n);
+    HIPCHK(hipMemcpyAsync(dd, hh, 8 * n, hipMemcpyHostToDevice, e->stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(dd, hh, 4 * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemsetAsync(dd + o_fid, 0, 4 * n, e->stream));
+  }
+  if (int rc = do_probe(b, IN_HASH, dd, nullptr, 4, reinterpret_cast<const uint32_t*>(dd + o_fid), n,
+                        reinterpret_cast<uint64_t*>(dd + o_found), e->stream))
+    return rc;
+  HIPCHK(hipMemcpyAsync(hh + o_found, dd + o_found, 8 * n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  memcpy(h_found, hh + o_found, 8 * n);
+  return 0;
+}
+
 static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
                     const uint32_t* fid, uint64_t n, uint64_t* found, void* stream,
-                    const uint64_t* d_runs = nullptr) {
+                    const uint64_t* d_runs) {
   if (!b || !b->built) return fail(RF_AMD_EINVAL, "probe on an unbuilt batch");
   if (n && (!in0 || !(fid || d_runs) || !found)) return fail(RF_AMD_EINVAL, "null probe buffer");
   HIPCHK(hipSetDevice(b->eng->device));
@@ -741,13 +905,14 @@ static int batch_import(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t F, 
   b->I = (uint32_t)idx_total;
   b->NL = lines_total;
   const size_t page_bytes = (size_t)pages_total * cfg->page_size;
-  int rc = b->d_plans.alloc(sizeof(FilterPlan) * F);
-  rc |= b->d_pplans.alloc(16ull * F);
-  rc |= b->d_pages.alloc(page_bytes + 256);
-  rc |= b->d_slots.alloc(8ull * idx_total);
-  rc |= b->d_lines.alloc(64ull * b->NL + 64);
-  rc |= b->d_idx_filter.alloc(4ull * idx_total);
-  rc |= b->d_outs.alloc(sizeof(FilterOut) * F);
+  DevPool* pool = &e->pool;
+  int rc = b->d_plans.alloc(sizeof(FilterPlan) * F, pool);
+  rc |= b->d_pplans.alloc(16ull * F, pool);
+  rc |= b->d_pages.alloc(page_bytes + 256, pool);
+  rc |= b->d_slots.alloc(8ull * idx_total, pool);
+  rc |= b->d_lines.alloc(64ull * b->NL + 64, pool);
+  rc |= b->d_idx_filter.alloc(4ull * idx_total, pool);
+  rc |= b->d_outs.alloc(sizeof(FilterOut) * F, pool);
   if (rc) {
     delete b;
     return fail(RF_AMD_ENOMEM, "device allocation failed");
@@ -1298,7 +1463,21 @@ extern "C" int rf_amd_filter_verify(rf_amd_engine* e, const rf_amd_config* cfg, 
 }
 
 // ---- routing_filter_print (src/routing_filter.c:1185-1286): debug text, host only ----------
+static int print_filter(const rf_amd_config* cfg, const rf_amd_image* filter, uint64_t filter_addr,
+                        const uint64_t* abs_slots, void* out_file);
+
 extern "C" int rf_amd_filter_print(const rf_amd_config* cfg, const rf_amd_image* filter, void* out_file) {
+  return print_filter(cfg, filter, 0, nullptr, out_file);
+}
+
+extern "C" int rf_amd_filter_print_abs(const rf_amd_config* cfg, const rf_amd_image* filter, uint64_t filter_addr,
+                                       const uint64_t* abs_slots, void* out_file) {
+  if (!abs_slots) return fail(RF_AMD_EINVAL, "null absolute slots");
+  return print_filter(cfg, filter, filter_addr, abs_slots, out_file);
+}
+
+static int print_filter(const rf_amd_config* cfg, const rf_amd_image* filter, uint64_t filter_addr,
+                        const uint64_t* abs_slots, void* out_file) {
   if (int rc = check_cfg(cfg)) return rc;
   if (!filter || !filter->pages || !filter->slots) return fail(RF_AMD_EINVAL, "null filter");
   FILE* fo = out_file ? (FILE*)out_file : stdout;
@@ -1310,9 +1489,10 @@ extern "C" int rf_amd_filter_print(const rf_amd_config* cfg, const rf_amd_image*
   auto bit = [&](uint64_t bp) { return (pg[bp >> 3] >> (bp & 7)) & 1u; };
   fprintf(fo, "********************************************************************************\n");
   fprintf(fo, "***   filter INDEX\n");
-  fprintf(fo, "***   filter_addr: %lu\n", (unsigned long)0);
+  fprintf(fo, "***   filter_addr: %lu\n", (unsigned long)filter_addr);
   fprintf(fo, "--------------------------------------------------------------------------------\n");
-  for (uint32_t i = 0; i < num_indices; i++) fprintf(fo, "index 0x%x: %lu\n", i, (unsigned long)filter->slots[i]);
+  for (uint32_t i = 0; i < num_indices; i++)
+    fprintf(fo, "index 0x%x: %lu\n", i, (unsigned long)(abs_slots ? abs_slots[i] : filter->slots[i]));
   for (uint32_t i = 0; i < num_indices; i++) {
     const uint64_t h = filter->slots[i];
     const uint32_t c = (uint32_t)pg[h] | ((uint32_t)pg[h + 1] << 8);

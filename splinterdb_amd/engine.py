@@ -45,6 +45,8 @@ EXPORTED = [
     "rf_amd_lookup_async_free", "rf_amd_filter_verify", "rf_amd_filter_print",
     "rf_amd_hash_keys", "rf_amd_hash_var_keys",
     "rf_amd_batch_export", "rf_amd_batch_import", "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
+    "rf_amd_batch_build_hashes_host", "rf_amd_batch_probe_hashes_host", "rf_amd_engine_pool_stats",
+    "rf_amd_filter_print_abs",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -158,6 +160,10 @@ def load_library(build_if_missing=True):
     L.rf_amd_route_probes.argtypes = [vp, vp, vp, u64, vp, u32, u32, vp, vp, vp, ctypes.POINTER(u64), vp]
     L.rf_amd_batch_probe_pairs.argtypes = [vp, vp, u64, vp, vp]
     L.rf_amd_unroute_found.argtypes = [vp, vp, vp, u64, vp, vp]
+    L.rf_amd_batch_build_hashes_host.argtypes = [vp, vp]
+    L.rf_amd_batch_probe_hashes_host.argtypes = [vp, vp, vp, u64, vp]
+    L.rf_amd_engine_pool_stats.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    L.rf_amd_filter_print_abs.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), u64, vp, vp]
     _lib = L
     return L
 
