@@ -509,12 +509,17 @@ rfr_async_stats(uint64 *batches, uint64 *probes)
    return 1;
 }
 
-/* routing_filter_print of the linked implementation, to stdout */
+/* routing_filter_print of the linked implementation, with platform_default_log pointed at
+ * stdout for the call (the library's default is /dev/null, platform_log.c:15-24) */
 void
 rfr_print(rfr_stack *s, routing_filter *f)
 {
+   platform_log_handle *info = platform_get_stdout_stream();
+   fflush(stdout);
+   platform_set_log_streams(stdout, stderr);
    routing_filter_print((cache *)&s->cc, &s->rcfg, f);
    fflush(stdout);
+   platform_set_log_streams(info, stderr);
 }
 
 /* one raw cache page (all page_size bytes) at a disk address */

@@ -35,7 +35,7 @@
  * one returns ENODEV (there is no CPU fallback).
  *
  * Device residency. Each filter this process builds stays on the GPU (a probe-only batch:
- * pages, slots, probe lines) in a registry keyed by its index-extent address, so lookups
+ * pages, slots, probe lines) in a registry keyed by (cache, index-extent address), so lookups
  * and later incremental adds never re-read it; a filter not in the registry (built before
  * a restart) is read back through cache_get once and imported. dec_ref drops the device
  * copy when the reference's refcount reaches zero.
@@ -110,8 +110,9 @@ num_indices_of(const routing_config *cfg, uint32 num_fingerprints)
    return 1u << (lnb - cfg->log_index_size);
 }
 
-/* ---- registry of device-resident filters, keyed by index-extent address --------------- */
+/* ---- registry of device-resident filters, keyed by (cache, index-extent address) -------- */
 typedef struct resident_filter {
+   const cache            *cc;
    uint64                  addr;
    rf_amd_batch           *batch;
    struct resident_filter *next;
@@ -122,18 +123,18 @@ static resident_filter *g_registry[REGISTRY_BUCKETS];
 static pthread_mutex_t  g_registry_mu = PTHREAD_MUTEX_INITIALIZER;
 
 static uint64
-registry_bucket(uint64 addr)
+registry_bucket(const cache *cc, uint64 addr)
 {
-   return (addr >> 12) * 0x9E3779B97F4A7C15ull >> 52;
+   return ((addr >> 12) ^ (uint64)(uintptr_t)cc) * 0x9E3779B97F4A7C15ull >> 52;
 }
 
 static rf_amd_batch *
-registry_find(uint64 addr)
+registry_find(const cache *cc, uint64 addr)
 {
    rf_amd_batch *b = NULL;
    pthread_mutex_lock(&g_registry_mu);
-   for (resident_filter *r = g_registry[registry_bucket(addr)]; r; r = r->next) {
-      if (r->addr == addr) {
+   for (resident_filter *r = g_registry[registry_bucket(cc, addr)]; r; r = r->next) {
+      if (r->cc == cc && r->addr == addr) {
          b = r->batch;
          break;
       }
@@ -142,22 +143,35 @@ registry_find(uint64 addr)
    return b;
 }
 
-/* inserts b unless addr is present; returns the registered batch (b's caller destroys b
- * when another thread registered first) */
+/*
+ * Registers b for (cc, addr). replace = 0 (a filter imported from the cache): an entry
+ * present already wins and is returned (the caller destroys b). replace = 1 (a filter just
+ * built at addr): any entry there is stale -- its pages were freed and reallocated without
+ * our dec_ref seeing it reach zero -- and is destroyed.
+ */
 static rf_amd_batch *
-registry_insert(uint64 addr, rf_amd_batch *b)
+registry_insert(const cache *cc, uint64 addr, rf_amd_batch *b, int replace)
 {
+   rf_amd_batch *stale = NULL;
    pthread_mutex_lock(&g_registry_mu);
-   resident_filter **head = &g_registry[registry_bucket(addr)];
+   resident_filter **head = &g_registry[registry_bucket(cc, addr)];
    for (resident_filter *r = *head; r; r = r->next) {
-      if (r->addr == addr) {
-         rf_amd_batch *have = r->batch;
+      if (r->cc == cc && r->addr == addr) {
+         if (!replace) {
+            rf_amd_batch *have = r->batch;
+            pthread_mutex_unlock(&g_registry_mu);
+            return have;
+         }
+         stale    = r->batch;
+         r->batch = b;
          pthread_mutex_unlock(&g_registry_mu);
-         return have;
+         rf_amd_batch_destroy(stale);
+         return b;
       }
    }
    resident_filter *r = malloc(sizeof(*r));
    platform_assert(r != NULL);
+   r->cc    = cc;
    r->addr  = addr;
    r->batch = b;
    r->next  = *head;
@@ -167,12 +181,12 @@ registry_insert(uint64 addr, rf_amd_batch *b)
 }
 
 static void
-registry_drop(uint64 addr)
+registry_drop(const cache *cc, uint64 addr)
 {
    rf_amd_batch *b = NULL;
    pthread_mutex_lock(&g_registry_mu);
-   for (resident_filter **pp = &g_registry[registry_bucket(addr)]; *pp; pp = &(*pp)->next) {
-      if ((*pp)->addr == addr) {
+   for (resident_filter **pp = &g_registry[registry_bucket(cc, addr)]; *pp; pp = &(*pp)->next) {
+      if ((*pp)->cc == cc && (*pp)->addr == addr) {
          resident_filter *r = *pp;
          *pp                = r->next;
          b                  = r->batch;
@@ -256,7 +270,7 @@ rf_read_image(cache                *cc,
 static platform_status
 resident(cache *cc, const routing_config *cfg, const routing_filter *f, rf_amd_batch **out)
 {
-   *out = registry_find(f->addr);
+   *out = registry_find(cc, f->addr);
    if (*out) {
       return STATUS_OK;
    }
@@ -276,7 +290,7 @@ resident(cache *cc, const routing_config *cfg, const routing_filter *f, rf_amd_b
    if (r) {
       return status_of(r);
    }
-   *out = registry_insert(f->addr, b);
+   *out = registry_insert(cc, f->addr, b, 0);
    if (*out != b) {
       rf_amd_batch_destroy(b);
    }
@@ -410,9 +424,7 @@ routing_filter_add(cache                *cc,
    if (rf_amd_batch_image_ptrs(b, 0, &d_pages, &d_slots) == 0
        && rf_amd_batch_import(e, &c, 1, &one, d_pages, d_slots, 1, &keep) == 0)
    {
-      if (registry_insert(filter->addr, keep) != keep) {
-         rf_amd_batch_destroy(keep);
-      }
+      registry_insert(cc, filter->addr, keep, 1);
    }
    rf_amd_batch_destroy(b);
    return STATUS_OK;
@@ -574,7 +586,7 @@ routing_filter_dec_ref(cache *cc, routing_filter *filter)
       return;
    }
    if (mini_dec_ref(cc, filter->meta_head, PAGE_TYPE_FILTER) == 0) {
-      registry_drop(filter->addr); /* the pages are gone: so is the device copy */
+      registry_drop(cc, filter->addr); /* the pages are gone: so is the device copy */
    }
 }
 
@@ -677,9 +689,10 @@ routing_filter_print(cache *cc, routing_config *cfg, routing_filter *filter)
    if (!SUCCESS(rf_read_image(cc, cfg, filter, &img, &abs_slots))) {
       return;
    }
-   rf_amd_config c = amd_config(cfg);
-   fflush(stdout);
-   rf_amd_filter_print_abs(&c, &img, filter->addr, abs_slots, stdout);
+   rf_amd_config c   = amd_config(cfg);
+   FILE         *out = platform_get_stdout_stream(); /* platform_default_log's stream */
+   fflush(out);
+   rf_amd_filter_print_abs(&c, &img, filter->addr, abs_slots, out);
    free(abs_slots);
    rf_amd_image_free(&img);
 }
