@@ -590,6 +590,7 @@ rfr_hash_keys(rfr_stack *s, const uint8 *keys, uint32 key_len, uint64 n, uint32 
 typedef struct rfr_bench {
    rfr_stack      *s;
    const uint8    *keys;
+   const uint64   *offs; /* variable-length keys: key i = keys[offs[i] .. offs[i+1]) */
    uint32          key_len;
    int             hash_keys;
    const uint64   *start;
@@ -627,7 +628,9 @@ build_worker(void *arg)
       uint32 *fps = malloc((size_t)n * 4 + 4);
       if (b->hash_keys) {
          for (uint32 i = 0; i < n; i++) {
-            key k  = key_create(FALSE, b->key_len, b->keys + (b->start[f] + i) * b->key_len);
+            const uint64 j = b->start[f] + i;
+            key          k = b->offs ? key_create(FALSE, b->offs[j + 1] - b->offs[j], b->keys + b->offs[j])
+                                     : key_create(FALSE, b->key_len, b->keys + j * b->key_len);
             fps[i] = data_key_hash(&b->s->data_cfg, k, b->s->rcfg.seed);
          }
       } else {
@@ -658,7 +661,8 @@ probe_worker(void *arg)
       }
       uint64 e = s + chunk < b->n ? s + chunk : b->n;
       for (uint64 i = s; i < e; i++) {
-         key k = key_create(FALSE, b->key_len, b->keys + i * b->key_len);
+         key k = b->offs ? key_create(FALSE, b->offs[i + 1] - b->offs[i], b->keys + b->offs[i])
+                         : key_create(FALSE, b->key_len, b->keys + i * b->key_len);
          routing_filter_lookup(
             (cache *)&b->s->cc, &b->s->rcfg, &b->keep[b->filter_id[i]], k, &b->found[i]);
       }
@@ -690,6 +694,7 @@ run_threads(rfr_bench *b, int threads, void *(*fn)(void *))
 double
 rfr_bench_build(rfr_stack      *s,
                 const uint8    *keys,
+                const uint64   *offs,
                 uint32          key_len,
                 int             hash_keys,
                 const uint64   *key_start,
@@ -703,6 +708,7 @@ rfr_bench_build(rfr_stack      *s,
    memset(&b, 0, sizeof(b));
    b.s         = s;
    b.keys      = keys;
+   b.offs      = offs;
    b.key_len   = key_len;
    b.hash_keys = hash_keys;
    b.start     = key_start;
@@ -718,6 +724,7 @@ double
 rfr_bench_probe(rfr_stack      *s,
                 routing_filter *keep,
                 const uint8    *keys,
+                const uint64   *offs,
                 uint32          key_len,
                 const uint32   *filter_id,
                 uint64          n,
@@ -728,6 +735,7 @@ rfr_bench_probe(rfr_stack      *s,
    memset(&b, 0, sizeof(b));
    b.s         = s;
    b.keys      = keys;
+   b.offs      = offs;
    b.key_len   = key_len;
    b.keep      = keep;
    b.filter_id = filter_id;

@@ -78,10 +78,10 @@ def lib(path=LIB_PATH):
         L.rfr_lookup_var_keys.restype = None
         L.rfr_hash_var_keys.argtypes = [vp, vp, vp, u64, vp]
         L.rfr_hash_var_keys.restype = None
+        L.rfr_bench_build.argtypes = [vp, vp, vp, u32, i32, vp, vp, u32, u16, i32, RF]
         L.rfr_bench_build.restype = ctypes.c_double
-        L.rfr_bench_build.argtypes = [vp, vp, u32, i32, vp, vp, u32, u16, i32, RF]
         L.rfr_bench_probe.restype = ctypes.c_double
-        L.rfr_bench_probe.argtypes = [vp, RF, vp, u32, vp, u64, i32, vp]
+        L.rfr_bench_probe.argtypes = [vp, RF, vp, vp, u32, vp, u64, i32, vp]
         L.rfr_lookup_keys_async_many.restype = u64
         L.rfr_lookup_keys_async_many.argtypes = [vp, vp, vp, vp, u32, u64, vp, ctypes.POINTER(u64)]
         L.rfr_async_stats.restype = i32
@@ -256,6 +256,34 @@ class Stack:
         out = np.zeros(4096, dtype=np.uint8)
         self.L.rfr_read_page(self.h, addr, _p(out))
         return out
+
+    def bench_build(self, data, key_len, starts, counts, threads, hash_keys=True, offs=None, value=0):
+        """routing_filter_add of len(counts) filters (filter f = keys starts[f] ..
+        starts[f] + counts[f] - 1) on `threads` registered threads, one filter per task as the
+        trunk's TASK_TYPE_NORMAL workers run them. data = keys (hash_keys=True: each filter's
+        keys are hashed first, trunk semantics) or u32 hashes (hash_keys=False, filter_test
+        semantics). Returns (seconds, descriptors)."""
+        d = np.ascontiguousarray(data)
+        st = np.ascontiguousarray(starts, dtype=np.uint64)
+        ct = np.ascontiguousarray(counts, dtype=np.uint32)
+        keep = (RoutingFilter * max(1, ct.size))()
+        o = None if offs is None else np.ascontiguousarray(offs, dtype=np.uint64)
+        t = self.L.rfr_bench_build(self.h, _p(d), None if o is None else _p(o), key_len, 1 if hash_keys else 0,
+                                   _p(st), _p(ct), ct.size, value, threads, keep)
+        if t < 0:
+            raise RuntimeError("routing_filter_add failed in the bench")
+        return t, keep
+
+    def bench_probe(self, keep, data, key_len, filter_id, threads, offs=None):
+        """routing_filter_lookup of every key (key i in filter filter_id[i]) on `threads`
+        threads. Returns (seconds, found_values)."""
+        d = np.ascontiguousarray(data)
+        fid = np.ascontiguousarray(filter_id, dtype=np.uint32)
+        o = None if offs is None else np.ascontiguousarray(offs, dtype=np.uint64)
+        found = np.zeros(fid.size, dtype=np.uint64)
+        t = self.L.rfr_bench_probe(self.h, keep, _p(d), None if o is None else _p(o), key_len, _p(fid), fid.size,
+                                   threads, _p(found))
+        return t, found
 
     def dec_ref(self, desc):
         self.L.rfr_dec_ref(self.h, ctypes.byref(desc))
