@@ -2251,6 +2251,21 @@ __device__ __forceinline__ uint32_t select32(uint32_t x, uint32_t r) {
   return pos;
 }
 
+// bit 0 of every rvs-bit field of a 64-bit word (rvs in [1, 32]): sum of 2^(k rvs) for
+// k < 64 / rvs, by doubling the pattern
+__device__ __forceinline__ uint64_t field_ones64(uint32_t rvs) {
+  uint64_t L = 1;
+  uint32_t w = rvs;  // width covered so far
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    if (w < 64) {
+      L |= L << w;
+      w <<= 1;
+    }
+  }
+  return L;
+}
+
 // Line probe, decode half (format above): bucket j of the line's group, line bytes in Q.
 // Returns false when the image must be walked instead (overflowed line, or a bucket too
 // large for the 96-bit remainder window).
@@ -2297,6 +2312,32 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
   const uint32_t w2 = o == 0 ? W[2] : (o == 1 ? W[3] : (o == 2 ? W[4] : W[5]));
   const uint64_t wl = (uint64_t)w1 << 32 | w0;
   const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
+  const uint32_t nb = c * rvs, rem = rvs - vs;
+  if (nb <= 64 && rem > 0) {
+    // all c entries at once (SWAR): W holds them as c fields of rvs bits, remainder part
+    // [vs, rvs) of each. Y keeps each field's remainder part XOR the probe's; a field
+    // matches iff its part of Y is zero: adding the all-ones low part MH carries into the
+    // part's top bit H exactly when the low bits are nonzero (no carry leaves a field).
+    const uint64_t W = off ? (wl >> off) | ((uint64_t)w2 << (64 - off)) : wl;
+    const uint64_t L = field_ones64(rvs);  // bit 0 of every rvs-bit field
+    const uint64_t valid = nb == 64 ? ~0ull : (1ull << nb) - 1;
+    const uint64_t M = ((L << rvs) - (L << vs)) & valid;  // remainder part of each field
+    const uint64_t H = (L << (rvs - 1)) & valid;          // top bit of each remainder part
+    const uint64_t MH = M & ~H;
+    const uint64_t Y = (W ^ ((uint64_t)(remainder << vs) * L)) & M;
+    uint64_t Z = H & ~((((Y & MH) + MH) | Y) & H);  // top bits of the matching fields
+    if (vs == 0) {
+      found = Z ? 1ull : 0ull;
+    } else {
+      while (Z) {  // one pass per match (usually 0 or 1)
+        const uint32_t p = (uint32_t)__builtin_ctzll(Z) + 1 - rvs;  // the field's first bit
+        const uint32_t val = (uint32_t)(W >> p) & vmask;
+        if (val < 64) found |= 1ull << val;
+        Z &= Z - 1;
+      }
+    }
+    return true;
+  }
   const uint32_t rvmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
   for (uint32_t k = 0; k < c; k++) {
     const uint32_t qb = off + k * rvs;  // < 96

@@ -1,0 +1,67 @@
+"""A/B of librf_amd builds in ONE process, interleaved rounds: probe (and build) kernel
+times at C2 (8 x 8M, probes grouped by filter) and C3 (256 x 2^20), plus result identity.
+usage: python tools/ab_probe2.py libA.so libB.so ...   (prints one JSON line)"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from splinterdb_amd import engine as E  # noqa: E402
+from splinterdb_amd import keys as K  # noqa: E402
+
+vp = ctypes.c_void_p
+dev = torch.device("cuda", 0)
+cfg = E.RfConfig(26, 8, 42, 4096, 32)
+shapes = {"c2": (8, 8_000_000), "c3": (256, 1 << 20)}
+out = {}
+for shape, (F, n) in shapes.items():
+    N = F * n
+    keys = K.seq_keys_torch(0, N, 24, dev)
+    counts = (ctypes.c_uint64 * F)(*([n] * F))
+    libs = []
+    for path in sys.argv[1:]:
+        L = ctypes.CDLL(os.path.abspath(path))
+        L.rf_amd_engine_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        L.rf_amd_batch_create.argtypes = [vp, ctypes.POINTER(E.RfConfig), ctypes.c_uint32, vp, vp, vp, vp,
+                                          ctypes.POINTER(vp)]
+        L.rf_amd_batch_build_keys.argtypes = [vp, vp, ctypes.c_uint32, vp]
+        L.rf_amd_batch_probe_keys_runs.argtypes = [vp, vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), vp, vp]
+        L.rf_amd_batch_set_timing.argtypes = [vp, ctypes.c_int]
+        L.rf_amd_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32]
+        L.rf_amd_batch_destroy.argtypes = [vp]
+        e = vp()
+        assert L.rf_amd_engine_create(0, ctypes.byref(e)) == 0
+        nn = np.full(F, n, dtype=np.uint32)
+        vals = np.zeros(F, dtype=np.uint16)
+        b = vp()
+        assert L.rf_amd_batch_create(e, ctypes.byref(cfg), F, nn.ctypes.data, vals.ctypes.data, None, None,
+                                     ctypes.byref(b)) == 0
+        assert L.rf_amd_batch_set_timing(b, 1) == 0
+        found = torch.empty(N, dtype=torch.int64, device=dev)
+        libs.append((os.path.basename(os.path.dirname(path)) + "/" + os.path.basename(path), L, b, found, nn, vals))
+    torch.cuda.synchronize()
+    res = {name: {"probe": [], "build": [], "assemble": [], "sort": [], "partition": []} for name, *_ in libs}
+    arr = (ctypes.c_float * 9)()
+    for rnd in range(7):
+        for name, L, b, found, *_ in libs:
+            assert L.rf_amd_batch_build_keys(b, keys.data_ptr(), 24, None) == 0
+            assert L.rf_amd_batch_probe_keys_runs(b, keys.data_ptr(), 24, counts, found.data_ptr(), None) == 0
+            torch.cuda.synchronize()
+            L.rf_amd_batch_timings(b, arr, 9)
+            r = res[name]
+            r["probe"].append(arr[8]); r["build"].append(arr[7]); r["assemble"].append(arr[6])
+            r["sort"].append(arr[3]); r["partition"].append(arr[0])
+    ref = libs[0][3]
+    same = all(torch.equal(ref, x[3]) for x in libs[1:])
+    allfound = bool(((ref & 1) == 1).all())
+    out[shape] = {"identical": same, "all_found": allfound,
+                  **{k: {m: round(float(np.median(v[m][1:])), 4) for m in v} for k, v in res.items()}}
+    for name, L, b, *_ in libs:
+        L.rf_amd_batch_destroy(b)
+    del keys, libs
+    torch.cuda.empty_cache()
+print(json.dumps(out))
