@@ -114,6 +114,8 @@ int rf_amd_engine_pool_stats(rf_amd_engine *e, uint64_t *pooled_bytes, uint64_t 
 
 /* synchronising accessors */
 int rf_amd_batch_info(rf_amd_batch *b, uint32_t f, rf_amd_filter_info *out);
+/* all rf_amd_batch_num_filters(b) infos at once (one synchronisation) */
+int rf_amd_batch_infos(rf_amd_batch *b, rf_amd_filter_info *out);
 /* copy filter f's image to host: num_pages*page_size bytes and num_indices slots */
 int rf_amd_batch_read_image(rf_amd_batch *b, uint32_t f, uint8_t *h_pages,
                             uint64_t pages_bytes, uint64_t *h_slots, uint32_t num_slots);

@@ -15,7 +15,8 @@
  * (io_config_valid, io_read_bootstrap). No libaio stand-in exists. The cache is sized to
  * hold every page, so nothing is ever written back to the device (the tests assert it) and
  * every filter page is a fresh cache page; the only device reads are incremental adds'
- * prefetch of the old filter's extents (mini_prefetch, src/routing_filter.c:356).
+ * prefetch of the old filter's extents (mini_prefetch, src/routing_filter.c:356). Async
+ * requests follow laio's completion protocol (mem_async_run below).
  *
  * Everything else -- routing_filter_add / _lookup / _lookup_async / _estimate_unique_fp,
  * the clockcache the pages live in, the mini_allocator that assigns their addresses -- is
@@ -38,12 +39,16 @@
 #include <time.h>
 
 /* ---- in-memory device behind io_ops --------------------------------------------------- */
+struct mem_async_state;
 typedef struct mem_io {
    io_handle  super;
    io_config *cfg;
    uint8     *disk;
    uint64     size;
    _Atomic uint64 reads, writes;
+   /* submitted requests whose completion callback io_cleanup has not fired yet */
+   pthread_mutex_t         lock;
+   struct mem_async_state *pending;
 } mem_io;
 
 static platform_status
@@ -76,13 +81,17 @@ mem_write(io_handle *io, void *buf, uint64 bytes, uint64 addr)
 
 #define MEM_ASYNC_MAX_PAGES 32 /* pages_per_extent (laio.c appends at most one extent) */
 typedef struct mem_async_state {
-   io_async_state    super;
-   mem_io           *io;
-   io_async_cmd      cmd;
-   uint64            addr;
-   uint64            iovlen;
-   platform_status   rc;
-   struct iovec      iov[MEM_ASYNC_MAX_PAGES];
+   io_async_state          super;
+   mem_io                 *io;
+   io_async_cmd            cmd;
+   uint64                  addr;
+   uint64                  iovlen;
+   platform_status         rc;
+   int                     submitted;
+   async_callback_fn       callback;
+   void                   *callback_arg;
+   struct mem_async_state *next;
+   struct iovec            iov[MEM_ASYNC_MAX_PAGES];
 } mem_async_state;
 _Static_assert(sizeof(mem_async_state) <= IO_ASYNC_STATE_BUFFER_SIZE, "async state too large");
 
@@ -99,17 +108,32 @@ mem_async_append_page(io_async_state *s, void *buf)
    return STATUS_OK;
 }
 
-/* completes at once: an immediate ASYNC_STATUS_DONE is a legal outcome of io_async_run */
+/*
+ * laio's protocol (src/platform_linux/laio.c:338-464): an empty request is DONE at once; a
+ * submitted one returns RUNNING, its completion callback fires from a later io_cleanup
+ * (laio.c:328-336), and the next run returns DONE. Callers such as clockcache's prefetch
+ * (src/clockcache.c:2463-2540) ignore run's result and finish only in that callback. The
+ * copy itself happens at submission; once queued the state belongs to the device.
+ */
 static async_status
 mem_async_run(io_async_state *s)
 {
    mem_async_state *m = (mem_async_state *)s;
-   uint64           a = m->addr;
+   if (m->iovlen == 0 || m->submitted) {
+      return ASYNC_STATUS_DONE;
+   }
+   uint64 a = m->addr;
    for (uint64 k = 0; k < m->iovlen && SUCCESS(m->rc); k++) {
       m->rc = mem_rw(m->io, m->iov[k].iov_base, m->iov[k].iov_len, a, m->cmd == io_async_pwritev);
       a += m->iov[k].iov_len;
    }
-   return ASYNC_STATUS_DONE;
+   m->submitted = 1;
+   mem_io *io   = m->io;
+   pthread_mutex_lock(&io->lock);
+   m->next     = io->pending;
+   io->pending = m;
+   pthread_mutex_unlock(&io->lock);
+   return ASYNC_STATUS_RUNNING;
 }
 
 static platform_status
@@ -149,36 +173,52 @@ mem_async_init(io_async_state   *state,
                void             *callback_arg)
 {
    mem_async_state *m = (mem_async_state *)state;
-   (void)callback;
-   (void)callback_arg;
-   m->super.ops = &mem_async_ops;
-   m->io        = (mem_io *)io;
-   m->cmd       = cmd;
-   m->addr      = addr;
-   m->iovlen    = 0;
-   m->rc        = STATUS_OK;
+   m->super.ops    = &mem_async_ops;
+   m->io           = (mem_io *)io;
+   m->cmd          = cmd;
+   m->addr         = addr;
+   m->iovlen       = 0;
+   m->rc           = STATUS_OK;
+   m->submitted    = 0;
+   m->callback     = callback;
+   m->callback_arg = callback_arg;
+   m->next         = NULL;
    return STATUS_OK;
 }
 
+/* fire up to count completion callbacks (count 0: all), as laio's io_cleanup does */
 static void
-mem_noop_cleanup(io_handle *io, uint64 count)
+mem_cleanup(io_handle *ioh, uint64 count)
 {
-   (void)io;
-   (void)count;
+   mem_io *io = (mem_io *)ioh;
+   for (uint64 done = 0; count == 0 || done < count; done++) {
+      pthread_mutex_lock(&io->lock);
+      mem_async_state *m = io->pending;
+      if (m) {
+         io->pending = m->next;
+      }
+      pthread_mutex_unlock(&io->lock);
+      if (!m) {
+         break;
+      }
+      if (m->callback) {
+         m->callback(m->callback_arg);
+      }
+   }
 }
 
 static void
-mem_noop(io_handle *io)
+mem_wait_all(io_handle *io)
 {
-   (void)io;
+   mem_cleanup(io, 0);
 }
 
 static io_ops mem_io_ops = {
    .read             = mem_read,
    .write            = mem_write,
    .async_state_init = mem_async_init,
-   .cleanup          = mem_noop_cleanup,
-   .wait_all         = mem_noop,
+   .cleanup          = mem_cleanup,
+   .wait_all         = mem_wait_all,
 };
 
 /* the two non-virtual io helpers of platform_io.c (not compiled: it includes laio.h) */
@@ -237,6 +277,7 @@ rfr_create(uint32 fingerprint_size, uint32 log_index_size, uint64 cache_mib, uin
    io_config_init(&s->io_cfg, 4096, 4096 * 32, O_RDWR | O_CREAT, 0600, 256, "rfr-memory-device");
    const uint64 disk = disk_mib * MiB;
    s->io.super.ops   = &mem_io_ops;
+   pthread_mutex_init(&s->io.lock, NULL);
    s->io.cfg         = &s->io_cfg;
    s->io.size        = disk;
    s->io.disk        = mmap(NULL, disk, PROT_READ | PROT_WRITE,
@@ -274,6 +315,7 @@ rfr_destroy(rfr_stack *s)
    if (!s) {
       return;
    }
+   mem_cleanup(&s->io.super, 0); /* complete every outstanding request first */
    clockcache_deinit(&s->cc);
    rc_allocator_deinit(&s->al);
    munmap(s->io.disk, s->io.size);
@@ -600,6 +642,9 @@ typedef struct rfr_bench {
    routing_filter *keep;
    _Atomic uint32  next;
    _Atomic int     err;
+   /* compaction chain: rounds per filter, key ids (f << 32) | (v << 24) | j */
+   uint32          rounds;
+   uint32          chain_n;
    /* probe */
    const uint32   *filter_id;
    uint64          n;
@@ -667,6 +712,51 @@ probe_worker(void *arg)
             (cache *)&b->s->cc, &b->s->rcfg, &b->keep[b->filter_id[i]], k, &b->found[i]);
       }
    }
+   platform_deregister_thread();
+   return NULL;
+}
+
+/* One filter's chain of incremental adds, as the trunk's compactions grow a branch's filter
+ * (src/trunk.c:3821-3835 hashes the packed keys, routing_filter_add merges the old filter,
+ * routing_filter_dec_ref drops the superseded one): round v adds chain_n 24 B keys of ids
+ * (f << 32) | (v << 24) | j under value v. */
+static void *
+chain_worker(void *arg)
+{
+   rfr_bench *b = arg;
+   platform_register_thread();
+   const uint32 n    = b->chain_n;
+   uint8       *keys = calloc((size_t)n, 24);
+   uint32      *fps  = malloc((size_t)n * 4 + 4);
+   for (;;) {
+      uint32 f = atomic_fetch_add(&b->next, 1);
+      if (f >= b->nf) {
+         break;
+      }
+      routing_filter cur = NULL_ROUTING_FILTER;
+      for (uint32 v = 0; v < b->rounds; v++) {
+         for (uint32 j = 0; j < n; j++) {
+            uint64 id = ((uint64)f << 32) | ((uint64)v << 24) | j;
+            memcpy(keys + (size_t)j * 24, &id, 8);
+            fps[j] = data_key_hash(&b->s->data_cfg, key_create(FALSE, 24, keys + (size_t)j * 24),
+                                   b->s->rcfg.seed);
+         }
+         routing_filter  next = NULL_ROUTING_FILTER;
+         platform_status rc   = routing_filter_add(
+            (cache *)&b->s->cc, &b->s->rcfg, &cur, &next, fps, n, (uint16)v);
+         if (!SUCCESS(rc)) {
+            atomic_store(&b->err, rc.r);
+            break;
+         }
+         if (v > 0) {
+            routing_filter_dec_ref((cache *)&b->s->cc, &cur);
+         }
+         cur = next;
+      }
+      b->keep[f] = cur;
+   }
+   free(keys);
+   free(fps);
    platform_deregister_thread();
    return NULL;
 }
@@ -742,4 +832,25 @@ rfr_bench_probe(rfr_stack      *s,
    b.n         = n;
    b.found     = found;
    return run_threads(&b, threads, probe_worker);
+}
+
+/* seconds for num_filters chains of `rounds` incremental adds of n keys each (chain_worker),
+ * or -1 on a failed add; keep[f] = each chain's last filter */
+double
+rfr_bench_chain(rfr_stack      *s,
+                uint32          num_filters,
+                uint32          rounds,
+                uint32          n,
+                int             threads,
+                routing_filter *keep)
+{
+   rfr_bench b;
+   memset(&b, 0, sizeof(b));
+   b.s       = s;
+   b.nf      = num_filters;
+   b.rounds  = rounds;
+   b.chain_n = n;
+   b.keep    = keep;
+   double t  = run_threads(&b, threads, chain_worker);
+   return atomic_load(&b.err) ? -1.0 : t;
 }

@@ -80,6 +80,8 @@ def lib(path=LIB_PATH):
         L.rfr_hash_var_keys.restype = None
         L.rfr_bench_build.argtypes = [vp, vp, vp, u32, i32, vp, vp, u32, u16, i32, RF]
         L.rfr_bench_build.restype = ctypes.c_double
+        L.rfr_bench_chain.argtypes = [vp, u32, u32, u32, i32, RF]
+        L.rfr_bench_chain.restype = ctypes.c_double
         L.rfr_bench_probe.restype = ctypes.c_double
         L.rfr_bench_probe.argtypes = [vp, RF, vp, vp, u32, vp, u64, i32, vp]
         L.rfr_lookup_keys_async_many.restype = u64
@@ -284,6 +286,17 @@ class Stack:
         t = self.L.rfr_bench_probe(self.h, keep, _p(d), None if o is None else _p(o), key_len, _p(fid), fid.size,
                                    threads, _p(found))
         return t, found
+
+    def bench_chain(self, num_filters, rounds, n, threads):
+        """num_filters compaction chains on `threads` threads: round v of filter f hashes n
+        24 B keys of ids (f << 32) | (v << 24) | j and routing_filter_adds them (value v) to
+        the filter of round v-1, dropping the superseded one (oracle/ref_harness.c
+        chain_worker). Returns (seconds, each chain's last filter)."""
+        keep = (RoutingFilter * max(1, num_filters))()
+        t = self.L.rfr_bench_chain(self.h, num_filters, rounds, n, threads, keep)
+        if t < 0:
+            raise RuntimeError("routing_filter_add failed in the chain bench")
+        return t, keep
 
     def dec_ref(self, desc):
         self.L.rfr_dec_ref(self.h, ctypes.byref(desc))

@@ -23,8 +23,7 @@
 using namespace rf;
 
 extern "C" int rf_launch_build(const LaunchArgs* a);
-extern "C" int rf_launch_old_decode(const LaunchArgs* a, uint32_t f, uint32_t old_num_indices,
-                                    uint32_t* d_cnt, uint32_t* d_pos);
+extern "C" int rf_launch_old_decode(const LaunchArgs* a);
 extern "C" int rf_launch_plines(const LaunchArgs* a);
 extern "C" int rf_launch_build_init(void* stream, uint32_t* cb_count, uint32_t* cb_cursor, uint32_t num_cb,
                                     uint32_t* outs_words, uint32_t num_out_words, uint32_t* overflow,
@@ -144,7 +143,8 @@ struct rf_amd_batch {
   uint32_t F = 0;
   bool wide = false;
   std::vector<FilterPlan> plans;
-  std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter, idx_filter;
+  std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter, idx_filter,
+      old_idx_filter;
   uint64_t E = 0, keys_total = 0;
   uint32_t CB = 0, I = 0, PS = 0, PF = 0;
   uint64_t NL = 0;         // probe lines (64 B each)
@@ -154,8 +154,8 @@ struct rf_amd_batch {
   std::vector<uint64_t> runs_host;  // their last uploaded value
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
-      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill;
-  std::vector<uint32_t> old_num_indices;
+      d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill,
+      d_old_idx_filter;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
@@ -255,7 +255,6 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   b->cfg = *cfg;
   b->F = num_filters;
   b->plans.resize(num_filters);
-  b->old_num_indices.assign(num_filters, 0);
   const uint32_t lis = cfg->log_index_size, fps = cfg->fingerprint_size, P = cfg->page_size;
   const uint32_t IS = 1u << lis;
   uint64_t e_first = 0, key_first = 0;
@@ -332,7 +331,8 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       p.npo = p.num_indices / op->num_indices;
       p.old_pages = ob->d_pages.as<uint8_t>() + (uint64_t)op->page_base * P;
       p.old_slots = ob->d_slots.as<uint64_t>() + op->idx_base;
-      b->old_num_indices[f] = op->num_indices;
+      p.old_idx_base = (uint32_t)b->old_idx_filter.size();
+      b->old_idx_filter.insert(b->old_idx_filter.end(), op->num_indices, f);
     }
     for (uint32_t s = 0; s < p.num_new; s += TILE_KEYS) {
       b->tile_filter.push_back(f);
@@ -400,8 +400,9 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   rc |= b->d_old_tile_filter.alloc(4 * b->old_tile_filter.size(), pool);
   rc |= b->d_old_tile_start.alloc(4 * b->old_tile_start.size(), pool);
   if (b->wide) {
-    rc |= b->d_old_cnt.alloc(4 * MAX_INDICES, pool);
-    rc |= b->d_old_pos.alloc(4 * MAX_INDICES, pool);
+    rc |= b->d_old_cnt.alloc(4 * b->old_idx_filter.size(), pool);
+    rc |= b->d_old_pos.alloc(4 * b->old_idx_filter.size(), pool);
+    rc |= b->d_old_idx_filter.alloc(4 * b->old_idx_filter.size(), pool);
     rc |= b->d_first_old.alloc(4 * b->I, pool);
     rc |= b->d_has_old.alloc(4 * b->I, pool);
   }
@@ -439,6 +440,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   UP(b->d_cb_filter, b->cb_filter);
   UP(b->d_pg_filter, b->pg_filter);
   UP(b->d_idx_filter, b->idx_filter);
+  UP(b->d_old_idx_filter, b->old_idx_filter);
 #undef UP
   HIPCHK(hipStreamSynchronize(st));
   *out = b;
@@ -480,6 +482,10 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.old_tile_filter = b->d_old_tile_filter.as<uint32_t>();
   a.old_tile_start = b->d_old_tile_start.as<uint32_t>();
   a.num_old_tiles = (uint32_t)b->old_tile_filter.size();
+  a.old_idx_filter = b->d_old_idx_filter.as<uint32_t>();
+  a.num_old_idx = (uint32_t)b->old_idx_filter.size();
+  a.old_cnt = b->d_old_cnt.as<uint32_t>();
+  a.old_pos = b->d_old_pos.as<uint32_t>();
   a.fp_size = b->cfg.fingerprint_size;
   a.seed = b->cfg.seed;
   a.lis = b->cfg.log_index_size;
@@ -536,13 +542,10 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
                            b->d_overflow.as<uint32_t>(), b->wide ? nullptr : b->d_spill.as<uint32_t>()))
     return fail(RF_AMD_EINVAL, "init kernel launch failed");
   if (b->wide) {
-    HIPCHK(hipMemsetAsync(b->d_ent.p, 0xff, b->d_ent.n, st));
-    for (uint32_t f = 0; f < b->F; f++) {
-      if (!b->old_num_indices[f]) continue;
-      int rc = rf_launch_old_decode(&a, f, b->old_num_indices[f], b->d_old_cnt.as<uint32_t>(),
-                                    b->d_old_pos.as<uint32_t>());
-      if (rc) return fail(RF_AMD_EINVAL, std::string("old decode launch: ") + hipGetErrorString((hipError_t)rc));
-    }
+    // every old filter of the batch decoded by one launch sequence (which also marks the
+    // unused tail of each old region); the new regions are written whole by the hashing pass
+    int rc = rf_launch_old_decode(&a);
+    if (rc) return fail(RF_AMD_EINVAL, std::string("old decode launch: ") + hipGetErrorString((hipError_t)rc));
   }
   int rc = rf_launch_build(&a);
   if (rc) return fail(RF_AMD_EINVAL, std::string("build launch: ") + hipGetErrorString((hipError_t)rc));
@@ -798,6 +801,25 @@ extern "C" int rf_amd_batch_info(rf_amd_batch* b, uint32_t f, rf_amd_filter_info
   out->num_indices = p.num_indices;
   out->num_pages = o.num_pages;
   out->error = o.error;
+  return 0;
+}
+
+// every filter's info with one copy (rf_amd_batch_info per filter synchronises F times)
+extern "C" int rf_amd_batch_infos(rf_amd_batch* b, rf_amd_filter_info* out) {
+  if (!b || !out) return fail(RF_AMD_EINVAL, "bad batch");
+  HIPCHK(hipSetDevice(b->eng->device));
+  std::vector<FilterOut> o(b->F);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost));
+  for (uint32_t f = 0; f < b->F; f++) {
+    const FilterPlan& p = b->plans[f];
+    out[f].num_fingerprints = p.num_fp;
+    out[f].num_unique = o[f].num_unique;
+    out[f].value_size = p.vs;
+    out[f].num_indices = p.num_indices;
+    out[f].num_pages = o[f].num_pages;
+    out[f].error = o[f].error;
+  }
   return 0;
 }
 

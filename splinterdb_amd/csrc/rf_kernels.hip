@@ -1677,27 +1677,61 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_scan_small(const uint32_t* __rest
   }
 }
 
+// Every old index of the batch in one list (filter f's at P.old_idx_base ..): the decode of
+// all old filters is three launches, whatever the number of filters.
 // k_old_counts: per old index, num_remainders from its header -> cnt
-__global__ void k_old_counts(const FilterPlan* __restrict__ plans, uint32_t f,
-                             uint32_t* __restrict__ cnt) {
-  const FilterPlan& P = plans[f];
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P.old_num_indices) return;
-  const uint64_t s = P.old_slots[i];
-  cnt[i] = (uint32_t)P.old_pages[s] | ((uint32_t)P.old_pages[s + 1] << 8);
+__global__ void k_old_counts(const FilterPlan* __restrict__ plans, const uint32_t* __restrict__ old_idx_filter,
+                             uint32_t num_old_idx, uint32_t* __restrict__ cnt) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= num_old_idx) return;
+  const FilterPlan& P = plans[old_idx_filter[g]];
+  const uint64_t s = P.old_slots[g - P.old_idx_base];
+  cnt[g] = (uint32_t)P.old_pages[s] | ((uint32_t)P.old_pages[s + 1] << 8);
+}
+
+// one workgroup per filter: exclusive scan of its old indices' counts -> pos (filter-relative),
+// and the sentinel (~0) on the entry slots past the decoded entries (old_region counts the old
+// filter's num_fingerprints, duplicates included; k_old_count / k_scatter skip sentinels)
+__global__ __launch_bounds__(LAYOUT_NT) void k_old_scan(const FilterPlan* __restrict__ plans,
+                                                        const uint32_t* __restrict__ cnt,
+                                                        uint32_t* __restrict__ pos, uint64_t* __restrict__ ent) {
+  __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
+  const FilterPlan& P = plans[blockIdx.x];
+  const uint32_t n = P.old_num_indices;
+  if (n == 0) return;
+  constexpr int PER = MAX_INDICES / LAYOUT_NT;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x * PER + k;
+    v[k] = i < n ? cnt[P.old_idx_base + i] : 0u;
+    sum += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan<LAYOUT_NT>(sum, s_tmp, &total);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const uint32_t i = threadIdx.x * PER + k;
+    if (i < n) pos[P.old_idx_base + i] = run;
+    run += v[k];
+  }
+  uint64_t* tail = ent + P.e_first + P.num_new;
+  for (uint32_t j = total + threadIdx.x; j < P.old_region; j += LAYOUT_NT) tail[j] = ~0ull;
 }
 
 // k_old_decode: one wave per old index. Entry k of the block: bucket offset = number of
 // 1-bits before its 0-bit in the encoding (routing_get_bucket_counts, :281-306); value
 // bits re-widened to the new value_size (:536-543). Written as (e << 1) | 0 (old flag).
-__global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict__ plans, uint32_t f,
-                                                    const uint32_t* __restrict__ pos,
+__global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict__ plans,
+                                                    const uint32_t* __restrict__ old_idx_filter,
+                                                    uint32_t num_old_idx, const uint32_t* __restrict__ pos,
                                                     uint64_t* __restrict__ ent, uint32_t lis,
                                                     uint32_t fp_size) {
-  const FilterPlan& P = plans[f];
-  const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  if (wid >= P.old_num_indices) return;
+  if (g >= num_old_idx) return;  // uniform per wave
+  const FilterPlan& P = plans[old_idx_filter[g]];
+  const uint32_t wid = g - P.old_idx_base;  // old index within its filter
   const uint32_t index_size = 1u << lis;
   const uint64_t hdr = P.old_slots[wid];
   const uint8_t* pg = P.old_pages;
@@ -1706,7 +1740,7 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
   const uint64_t ebit = (hdr + 2) * 8;
   const uint64_t rbit = (hdr + 2 + enc) * 8;
   const uint32_t total_bits = c + index_size;
-  uint64_t* out = ent + P.e_first + P.num_new + pos[wid];
+  uint64_t* out = ent + P.e_first + P.num_new + pos[g];
   const uint32_t old_vmask = (uint32_t)((1ull << P.old_vs) - 1);
   // walk the encoding 64 bits per lane-step: each lane takes one 64-bit chunk per round
   uint32_t zeros_before = 0, ones_before = 0;
@@ -2665,17 +2699,19 @@ extern "C" int rf_launch_plines(const LaunchArgs* pa) {
   return 0;
 }
 
-extern "C" int rf_launch_old_decode(const LaunchArgs* pa, uint32_t f, uint32_t old_num_indices,
-                                    uint32_t* d_cnt, uint32_t* d_pos) {
+extern "C" int rf_launch_old_decode(const LaunchArgs* pa) {
   const LaunchArgs& a = *pa;
-  hipLaunchKernelGGL(k_old_counts, dim3((old_num_indices + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a.plans, f,
-                     d_cnt);
+  if (a.num_old_idx == 0) return 0;
+  hipLaunchKernelGGL(k_old_counts, dim3((a.num_old_idx + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a.plans,
+                     a.old_idx_filter, a.num_old_idx, a.old_cnt);
   CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, d_cnt, d_pos, old_num_indices);
+  hipLaunchKernelGGL(k_old_scan, dim3(a.num_filters), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, a.plans, a.old_cnt,
+                     a.old_pos, (uint64_t*)a.ent);
   CHECK_LAUNCH();
   const uint32_t waves_per_block = 256 / WAVE;
-  hipLaunchKernelGGL(k_old_decode, dim3((old_num_indices + waves_per_block - 1) / waves_per_block), dim3(256),
-                     0, (hipStream_t)a.stream, a.plans, f, d_pos, (uint64_t*)a.ent, a.lis, a.fp_size);
+  hipLaunchKernelGGL(k_old_decode, dim3((a.num_old_idx + waves_per_block - 1) / waves_per_block), dim3(256), 0,
+                     (hipStream_t)a.stream, a.plans, a.old_idx_filter, a.num_old_idx, a.old_pos, (uint64_t*)a.ent,
+                     a.lis, a.fp_size);
   CHECK_LAUNCH();
   return 0;
 }

@@ -48,6 +48,8 @@ struct FilterPlan {
   uint32_t lines_asm;  // 1: K6 cuts this filter's lines from its LDS page images; 0: k_plines
   // old filter (incremental add)
   uint32_t old_num_indices, old_vs, old_rvs, npo;  // npo = new indices per old index
+  uint32_t old_idx_base;  // first of this filter's old indices in the batch's old-index list
+  uint32_t pad0;
   const uint8_t* old_pages;
   const uint64_t* old_slots;
 };
@@ -83,6 +85,10 @@ struct LaunchArgs {
   const uint32_t* old_tile_filter;
   const uint32_t* old_tile_start;
   uint32_t num_old_tiles;
+  const uint32_t* old_idx_filter;  // incremental adds: filter of each old index of the batch
+  uint32_t num_old_idx;
+  uint32_t* old_cnt;  // per old index: entries (num_remainders), then their start
+  uint32_t* old_pos;
   const void* in0;
   const uint64_t* offs;
   uint32_t key_len, fp_size, seed, lis, page_size;

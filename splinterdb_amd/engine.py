@@ -46,7 +46,7 @@ EXPORTED = [
     "rf_amd_hash_keys", "rf_amd_hash_var_keys",
     "rf_amd_batch_export", "rf_amd_batch_import", "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
     "rf_amd_batch_build_hashes_host", "rf_amd_batch_probe_hashes_host", "rf_amd_engine_pool_stats",
-    "rf_amd_filter_print_abs",
+    "rf_amd_filter_print_abs", "rf_amd_batch_infos",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -164,6 +164,7 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_probe_hashes_host.argtypes = [vp, vp, vp, u64, vp]
     L.rf_amd_engine_pool_stats.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
     L.rf_amd_filter_print_abs.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), u64, vp, vp]
+    L.rf_amd_batch_infos.argtypes = [vp, ctypes.POINTER(RfFilterInfo)]
     _lib = L
     return L
 
@@ -678,6 +679,12 @@ class FilterBatch:
         out = RfFilterInfo()
         _check(load_library().rf_amd_batch_info(self.h, f, ctypes.byref(out)))
         return out
+
+    def infos(self):
+        """every filter's RfFilterInfo (one synchronisation)"""
+        arr = (RfFilterInfo * self.F)()
+        _check(load_library().rf_amd_batch_infos(self.h, arr))
+        return list(arr)
 
     def read_image_async(self, f, h_pages, h_slots, stream=None):
         """D2H of filter f's pages/slots into (pinned) host tensors sized by the caller."""
