@@ -47,7 +47,13 @@ WORKLOADS = {
     "c4": (1024, 1 << 20, "strong", "C4: 2^30 x 24B keys = 1024 filters x 2^20 split by key range, build + full probe"),
     "c5": (8, 1 << 21, "weak", "C5: 16.8M variable-length (8-100 B) keys per GPU = 8 filters x 2^21, build + "
                                "as many probes (90% Zipf(0.99) positives, 10% negatives, shuffled)"),
+    "compaction": (64, (1 << 20) - 1, "weak",
+                   "compaction chains: 64 filters per GPU, each grown by 8 incremental routing_filter_adds of "
+                   "2^20-1 keys (filter_test's basic chain, keys (f << 32) + (v + 1) j, value v); every round = "
+                   "create + build (merging the previous round's filter) + read-back of the pages to pinned host "
+                   "memory + release of the superseded filter"),
 }
+CHAIN_ROUNDS = 8
 
 METRIC = "routing_filter build Mkeys/s + probe Mkeys/s, device-resident, 24B keys"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -58,10 +64,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
+    p.add_argument("--workload", choices=list(WORKLOADS), default="c2",
                    help="c2: 8 x 8,000,000 keys per GPU (weak); c3: 256 x 2^20 per GPU (weak); "
                         "c4: 1024 x 2^20 keys in total, split over the GPUs (strong); "
-                        "c5: 8 x 2^21 variable-length keys per GPU + Zipf probe mix (weak)")
+                        "c5: 8 x 2^21 variable-length keys per GPU + Zipf probe mix (weak); "
+                        "compaction: 64 incremental chains of 8 x (2^20-1) keys per GPU (weak; "
+                        "a step = one whole chain)")
     p.add_argument("--filters", type=int, default=0, help="override filters (per GPU for c2/c3)")
     p.add_argument("--keys-per-filter", type=int, default=0)
     p.add_argument("--log-index-size", type=int, default=8)
@@ -153,6 +161,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     coll_dev = dev if backend == "nccl" else None  # device of the timing reductions
+
+    if args.workload == "compaction":
+        return run_compaction(args, rank, world, dist, dev, coll_dev, backend)
 
     wf, wn, scaling, wdesc = WORKLOADS[args.workload]
     var = args.workload == "c5"
@@ -424,6 +435,184 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     batch.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_compaction(args, rank, world, dist, dev, coll_dev, backend):
+    """Compaction chains (SURVEY.md §8(f) 'incremental adds'): the trunk grows a branch's
+    filter by one routing_filter_add per compaction, merging the previous filter
+    (src/trunk.c:3821-3835, src/routing_filter.c:355-368) and dropping it afterwards
+    (routing_filter_dec_ref). Here F filters per GPU run CHAIN_ROUNDS such rounds in
+    lockstep; round v of filter g adds keys (g << 32) + (v + 1) j, j < n, under value v --
+    for g = 0 exactly tests/functional/filter_test.c:53-82. A round = create the batch (pooled
+    device memory), build it from the device-resident keys with the previous round's
+    batch as old filters, read every filter's pages and index slots back into pinned host
+    buffers (the clockcache pages' stand-in) on a copy stream, and release the superseded
+    batch stream-ordered. The read-back of round v overlaps the build of round v+1. One
+    step = one whole chain; value = new keys / step time, whole job."""
+    F = args.filters or WORKLOADS["compaction"][0]
+    n = args.keys_per_filter or WORKLOADS["compaction"][1]
+    V = CHAIN_ROUNDS
+    g0 = rank * F
+    cfg = E.routing_config_init(fingerprint_size=26, log_index_size=args.log_index_size, seed=42)
+    eng = E.Engine(dev.index)
+    stream = torch.cuda.Stream(device=dev)
+    copy = torch.cuda.Stream(device=dev)
+    st = stream.cuda_stream
+    with torch.cuda.stream(stream):
+        gid = torch.arange(g0, g0 + F, device=dev, dtype=torch.int64)[:, None] << 32
+        j = torch.arange(n, device=dev, dtype=torch.int64)[None, :]
+        keys = [K.ids_keys_torch((gid + (v + 1) * j).reshape(-1), 24) for v in range(V)]
+        found = torch.empty(F * n, dtype=torch.int64, device=dev)
+        del gid, j
+    stream.synchronize()
+    hp = hs = None
+
+    def chain(readback, timing=False):
+        """one chain of V rounds; returns (last batch, per-round wall ms, per-round build ms,
+        per-round infos)"""
+        prev = None
+        walls, builds, infos_all = [], [], []
+        evs = []
+        for v in range(V):
+            t0 = time.perf_counter()
+            b = E.FilterBatch(cfg, [n] * F, [v] * F, old=[(prev, f) for f in range(F)] if prev else None,
+                              engine=eng)
+            if timing:
+                b.set_timing(True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            b.build_keys(keys[v], 24, stream=st)
+            e1.record(stream)
+            evs.append((e0, e1))
+            if prev is not None:
+                stream.wait_stream(copy)  # the previous round's read-back also reads prev
+                prev.close(stream=st)
+            inf = b.infos(stream=st)
+            if readback:
+                copy.wait_stream(stream)
+                for f in range(F):
+                    b.read_image_async(f, hp[f][: inf[f].num_pages * cfg.page_size], hs[f][: inf[f].num_indices],
+                                       copy.cuda_stream)
+            infos_all.append(inf)
+            walls.append((time.perf_counter() - t0) * 1e3)
+            prev = b
+        copy.synchronize()
+        stream.synchronize()
+        builds = [a.elapsed_time(c) for a, c in evs]
+        return prev, walls, builds, infos_all
+
+    # sizing chain (untimed): the last round's filters are the largest
+    last, _, _, inf0 = chain(False)
+    last.close()
+    hp = [torch.empty(i.num_pages * cfg.page_size, dtype=torch.uint8).pin_memory() for i in inf0[-1]]
+    hs = [torch.empty(i.num_indices, dtype=torch.int64).pin_memory() for i in inf0[-1]]
+    for _ in range(max(0, args.warmup)):
+        last, *_ = chain(True)
+        last.close()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    steps = max(1, args.steps)
+    walls, builds = np.zeros(V), np.zeros(V)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        last, w, bt, infos_all = chain(True)
+        walls += w
+        builds += bt
+        if k + 1 < steps:
+            last.close(stream=st)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = S.max_over_ranks(time.perf_counter() - t0, dist, coll_dev)
+    keys_job = S.sum_over_ranks(float(F * n * V), dist, coll_dev)
+    walls /= steps
+    builds /= steps
+
+    # device-only chain (no read-back), beside value
+    torch.cuda.synchronize()
+    td = time.perf_counter()
+    lastd, _, bt_d, _ = chain(False, timing=True)
+    td = time.perf_counter() - td
+    stage_last = lastd.timings(0)
+    lastd.close()
+
+    # ---- verification (outside the timed region) -------------------------------------
+    # every round's keys find their value in the final filters (filter_test.c:100-116)
+    ok = True
+    counts = [n] * F
+    for v in range(V):
+        last.probe_keys_runs(keys[v], 24, counts, found, stream=st)
+        stream.synchronize()
+        ok = ok and bool((((found >> v) & 1) == 1).all().item())
+    final = infos_all[-1]
+    ok = ok and all(i.error == 0 and i.num_fingerprints == V * n for i in final)
+    sha_checked = []
+    if args.log_index_size == 8:
+        with open(os.path.join(ROOT, "tests", "golden", "sha256.json")) as fh:
+            gold = json.load(fh)
+        for f in range(F):
+            key = f"chain_f{g0 + f}_v{V}_n{n}_lis8"
+            if key in gold:
+                img = last.image(f)
+                good = (hashlib.sha256(img.pages.tobytes()).hexdigest() == gold[key]["pages_sha256"] and
+                        hashlib.sha256(img.slots.tobytes()).hexdigest() == gold[key]["slots_sha256"] and
+                        final[f].num_unique == gold[key]["num_unique"])
+                ok = ok and good
+                sha_checked.append(g0 + f)
+    # the read-back landed: the host copy of the last round equals the device image
+    img0 = last.image(0)
+    ok = ok and bool(np.array_equal(hp[0][: img0.pages.size].numpy(), img0.pages))
+    last.close()
+    verified = S.max_over_ranks(0.0 if ok else 1.0, dist, coll_dev) == 0.0
+
+    # roofline of the dominant phase, the last round's incremental build: algorithmic bytes =
+    # new keys (24 B) + the old filters' pages and slots read + the new pages and slots written
+    pg = cfg.page_size
+    old_b = sum(i.num_pages * pg + i.num_indices * 8 for i in infos_all[-2]) if V > 1 else 0
+    new_b = sum(i.num_pages * pg + i.num_indices * 8 for i in final)
+    alg = F * n * 24 + old_b + new_b
+    b_ms = float(builds[-1])
+    achieved = alg / (b_ms * 1e-3) / 1e9
+    readback_bytes = sum(i.num_pages * pg + i.num_indices * 8 for inf in infos_all for i in inf)
+    ms_step = elapsed / steps * 1e3
+    value = keys_job / (elapsed / steps) / 1e6
+    out = {
+        "metric": "routing_filter compaction chain: new keys/s through create + incremental build + page read-back",
+        "value": round(value, 1), "unit": "Mkeys/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: filter_test-format 24 B keys (f << 32) + (v + 1) j, generated in HBM",
+        "config": {"workload": WORKLOADS["compaction"][3], "filters_per_gpu": F, "rounds": V,
+                   "keys_per_round": n, "fingerprints_final": V * n, "fingerprint_size": 26,
+                   "log_index_size": args.log_index_size, "seed": 42,
+                   "parallelism": f"filter shards, {world} rank(s), no data-path collective"},
+        "round_wall_ms": [round(x, 3) for x in walls],
+        "round_build_ms": [round(x, 3) for x in builds],
+        "device_only_chain_ms": round(td * 1e3, 3),
+        "device_only_mkeys_s": round(F * n * V / td / 1e6, 1),
+        "readback_gb_per_chain": round(readback_bytes / 1e9, 3),
+        "readback_gbs": round(readback_bytes / (elapsed / steps) / 1e9, 1),
+        "last_round_stages_ms": {k: round(v, 4) for k, v in stage_last.items() if k != "probe"},
+        "roofline": {"bound": "hbm", "kernel": "incremental build (round 8, all stages)", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "alg_bytes": int(alg)},
+        "verified": verified, "sha_checked_filters": sha_checked,
+        "num_unique_filter0": int(final[0].num_unique),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline as CB
+        cb = CB.chain(args.log_index_size, V, n, threads=args.cpu_threads)
+        if cb is not None:
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu"] = round(value / cb["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

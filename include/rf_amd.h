@@ -74,7 +74,13 @@ int rf_amd_batch_create(rf_amd_engine *e, const rf_amd_config *cfg, uint32_t num
                         const uint32_t *num_new, const uint16_t *value,
                         rf_amd_batch *const *old_batch, const uint32_t *old_index,
                         rf_amd_batch **out);
+/* synchronises the device, then releases the batch's memory (routing_filter_dec_ref's
+ * release of a superseded filter, src/routing_filter.c:1101-1109) */
 void rf_amd_batch_destroy(rf_amd_batch *b);
+/* stream-ordered destroy: the caller has ordered every use of b before the current end of
+ * `stream` (NULL = engine's); the memory becomes reusable once the stream passes that point.
+ * Does not wait. */
+int rf_amd_batch_destroy_on(rf_amd_batch *b, void *stream);
 
 /* inputs are DEVICE pointers; all calls are asynchronous on `stream` (NULL = engine's) */
 int rf_amd_batch_build_keys(rf_amd_batch *b, const void *d_keys, uint32_t key_len,
@@ -114,8 +120,9 @@ int rf_amd_engine_pool_stats(rf_amd_engine *e, uint64_t *pooled_bytes, uint64_t 
 
 /* synchronising accessors */
 int rf_amd_batch_info(rf_amd_batch *b, uint32_t f, rf_amd_filter_info *out);
-/* all rf_amd_batch_num_filters(b) infos at once (one synchronisation) */
-int rf_amd_batch_infos(rf_amd_batch *b, rf_amd_filter_info *out);
+/* all rf_amd_batch_num_filters(b) infos at once: one synchronisation, with `stream` (the
+ * build's stream) or, if NULL, the whole device */
+int rf_amd_batch_infos(rf_amd_batch *b, rf_amd_filter_info *out, void *stream);
 /* copy filter f's image to host: num_pages*page_size bytes and num_indices slots */
 int rf_amd_batch_read_image(rf_amd_batch *b, uint32_t f, uint8_t *h_pages,
                             uint64_t pages_bytes, uint64_t *h_slots, uint32_t num_slots);

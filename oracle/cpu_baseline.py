@@ -190,3 +190,35 @@ def var_keys(lis, w, F, n, threads=0):
         "host": host, "all_cores": dict(threads=P, filters=F, keys_per_filter=n, **rates),
         "build_mkeys_s": rates["hash_build_mkeys_s"], "probe_mkeys_s": rates["probe_mkeys_s"],
     }
+
+
+def chain(lis, rounds, n, threads=0):
+    """bench.py --workload compaction: the reference's own incremental routing_filter_add
+    chains (oracle/ref_harness.c chain_worker: keys generated and hashed per round, old filter
+    merged, superseded filter dec_ref'd), one chain per thread on every usable core, and one
+    chain on one thread."""
+    from oracle import refimpl as R
+    if not R.available():
+        return None
+    cores, host = host_cores()
+    P = threads or cores
+    best = {}
+    for label, nf, th in (("all_cores", P, P), ("single_thread", 1, 1)):
+        t_best = None
+        for _ in range(REPS):
+            with R.Stack(log_index_size=lis, cache_mib=8192, disk_mib=131072) as s:
+                t, keep = s.bench_chain(nf, rounds, n, th)
+                u0 = int(keep[0].num_unique)
+                for f in range(nf):
+                    s.dec_ref(keep[f])
+            t_best = t if t_best is None else min(t_best, t)
+        best[label] = {"threads": th, "chains": nf, "seconds": round(t_best, 3),
+                       "mkeys_s": round(nf * rounds * n / t_best / 1e6, 2),
+                       "ns_per_key": round(t_best / (nf * rounds * n) * 1e9 * th, 1)}
+    return {
+        "value": best["all_cores"]["mkeys_s"], "unit": "Mkeys/s", "cores": P, "kind": "reference",
+        "sample": f"{P} chains (one per thread on {P} threads) of {rounds} incremental routing_filter_adds of "
+                  f"{n} 24 B keys each (keys generated + hashed per round, superseded filter dec_ref'd); "
+                  f"filter 0's num_unique {u0}",
+        "host": host, "all_cores": best["all_cores"], "single_thread": best["single_thread"],
+    }

@@ -253,6 +253,33 @@ def gen_sha():
     print("sha256.json:", list(res))
 
 
+CHAIN_SAMPLE = (0, 1, 63)
+CHAIN_ROUNDS, CHAIN_N = 8, (1 << 20) - 1
+
+
+def gen_chain_sha():
+    """Compaction chains (bench.py --workload compaction): filter f after CHAIN_ROUNDS
+    incremental routing_filter_adds of CHAIN_N keys of ids (f << 32) + (v + 1) * j, value v,
+    built by the REFERENCE itself (oracle/_ref/libref_rf.so, oracle/ref_harness.c
+    chain_worker). Merged into sha256.json."""
+    from oracle import refimpl as R
+    path = os.path.join(GOLD, "sha256.json")
+    with open(path) as fh:
+        res = json.load(fh)
+    with R.Stack(log_index_size=8, cache_mib=4096, disk_mib=65536) as s:
+        _, keep = s.bench_chain(max(CHAIN_SAMPLE) + 1, CHAIN_ROUNDS, CHAIN_N, 8)
+        for f in CHAIN_SAMPLE:
+            img = s.image(keep[f])
+            res[f"chain_f{f}_v{CHAIN_ROUNDS}_n{CHAIN_N}_lis8"] = {
+                "pages_sha256": hashlib.sha256(img.pages.tobytes()).hexdigest(),
+                "slots_sha256": hashlib.sha256(img.slots.tobytes()).hexdigest(),
+                "num_fingerprints": int(keep[f].num_fingerprints), "num_unique": int(keep[f].num_unique),
+                "num_pages": int(img.pages.size // 4096), "source": "reference"}
+    with open(path, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print("sha256.json chains:", CHAIN_SAMPLE)
+
+
 if __name__ == "__main__":
     os.makedirs(GOLD, exist_ok=True)
     O.build()
@@ -263,3 +290,4 @@ if __name__ == "__main__":
     gen_packedarray()
     gen_filters()
     gen_sha()
+    gen_chain_sha()

@@ -642,7 +642,7 @@ typedef struct rfr_bench {
    routing_filter *keep;
    _Atomic uint32  next;
    _Atomic int     err;
-   /* compaction chain: rounds per filter, key ids (f << 32) | (v << 24) | j */
+   /* compaction chain: rounds per filter, key ids (f << 32) + (v + 1) * j */
    uint32          rounds;
    uint32          chain_n;
    /* probe */
@@ -719,7 +719,8 @@ probe_worker(void *arg)
 /* One filter's chain of incremental adds, as the trunk's compactions grow a branch's filter
  * (src/trunk.c:3821-3835 hashes the packed keys, routing_filter_add merges the old filter,
  * routing_filter_dec_ref drops the superseded one): round v adds chain_n 24 B keys of ids
- * (f << 32) | (v << 24) | j under value v. */
+ * (f << 32) + (v + 1) * j under value v -- for f = 0 exactly filter_test's basic chain
+ * (tests/functional/filter_test.c:55-78, keys (i + 1) * j). */
 static void *
 chain_worker(void *arg)
 {
@@ -736,7 +737,7 @@ chain_worker(void *arg)
       routing_filter cur = NULL_ROUTING_FILTER;
       for (uint32 v = 0; v < b->rounds; v++) {
          for (uint32 j = 0; j < n; j++) {
-            uint64 id = ((uint64)f << 32) | ((uint64)v << 24) | j;
+            uint64 id = ((uint64)f << 32) + (uint64)(v + 1) * j;
             memcpy(keys + (size_t)j * 24, &id, 8);
             fps[j] = data_key_hash(&b->s->data_cfg, key_create(FALSE, 24, keys + (size_t)j * 24),
                                    b->s->rcfg.seed);

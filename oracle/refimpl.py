@@ -289,7 +289,7 @@ class Stack:
 
     def bench_chain(self, num_filters, rounds, n, threads):
         """num_filters compaction chains on `threads` threads: round v of filter f hashes n
-        24 B keys of ids (f << 32) | (v << 24) | j and routing_filter_adds them (value v) to
+        24 B keys of ids (f << 32) + (v + 1) * j and routing_filter_adds them (value v) to
         the filter of round v-1, dropping the superseded one (oracle/ref_harness.c
         chain_worker). Returns (seconds, each chain's last filter)."""
         keep = (RoutingFilter * max(1, num_filters))()

@@ -51,11 +51,18 @@ static int fail(int rc, const std::string& msg) {
 // a new set of filters on every compaction, so in steady state rf_amd_batch_create finds
 // its ~25 work buffers here instead of calling hipMalloc. Sizes are rounded up to classes
 // of 1/8 of a power of two (at most 12.5 % slack); a block returns to the pool when its
-// batch is destroyed (after a device synchronize, so no kernel still uses it) unless the
-// pool already holds RF_AMD_POOL_MIB (default 32768) MiB.
+// batch is destroyed unless the pool already holds RF_AMD_POOL_MIB (default 32768) MiB.
+// rf_amd_batch_destroy synchronises the device first; rf_amd_batch_destroy_on instead
+// parks the blocks behind an event on the caller's stream (stream-ordered release, as
+// hipFreeAsync): they become reusable once that event has completed.
 struct DevPool {
   std::mutex mu;
   std::multimap<size_t, void*> free_blocks;
+  struct Parked {
+    hipEvent_t ev;
+    std::vector<std::pair<void*, size_t>> blocks;  // size 0: not pooled, hipFree when released
+  };
+  std::vector<Parked> parked;
   size_t pooled = 0, limit = 0;
   uint64_t hits = 0, misses = 0;
   static size_t size_class(size_t bytes) {
@@ -64,8 +71,32 @@ struct DevPool {
     const size_t step = (size_t)1 << (lg - 3);
     return (bytes + step - 1) / step * step;
   }
+  void give_locked(void* p, size_t cls) {
+    if (cls == 0 || pooled + cls > limit) {
+      (void)hipFree(p);
+      return;
+    }
+    free_blocks.emplace(cls, p);
+    pooled += cls;
+  }
+  // parked blocks whose event has completed (wait: every parked block) go to free_blocks
+  void reap_locked(bool wait) {
+    for (size_t i = 0; i < parked.size();) {
+      Parked& k = parked[i];
+      if (wait) (void)hipEventSynchronize(k.ev);
+      if (!wait && hipEventQuery(k.ev) != hipSuccess) {
+        i++;
+        continue;
+      }
+      for (auto& b : k.blocks) give_locked(b.first, b.second);
+      (void)hipEventDestroy(k.ev);
+      parked[i] = std::move(parked.back());
+      parked.pop_back();
+    }
+  }
   void* take(size_t cls) {
     std::lock_guard<std::mutex> g(mu);
+    if (!parked.empty()) reap_locked(false);
     auto it = free_blocks.find(cls);
     if (it == free_blocks.end()) {
       misses++;
@@ -84,8 +115,13 @@ struct DevPool {
     pooled += cls;
     return true;
   }
+  void park(Parked&& k) {
+    std::lock_guard<std::mutex> g(mu);
+    parked.push_back(std::move(k));
+  }
   void drain() {
     std::lock_guard<std::mutex> g(mu);
+    reap_locked(true);
     for (auto& kv : free_blocks) (void)hipFree(kv.second);
     free_blocks.clear();
     pooled = 0;
@@ -162,6 +198,13 @@ struct rf_amd_batch {
   ~rf_amd_batch() {
     for (auto ev : events) (void)hipEventDestroy(ev);
   }
+  std::vector<DevBuf*> bufs() {
+    return {&d_runs, &d_plans, &d_outs, &d_ent, &d_part, &d_sorted, &d_cb_count, &d_cb_start, &d_cb_cursor,
+            &d_cb_filter, &d_overflow, &d_idx_cnt, &d_idx_start, &d_slots, &d_page_first, &d_pg_filter,
+            &d_pages, &d_tile_filter, &d_tile_start, &d_old_tile_filter, &d_old_tile_start, &d_old_cnt,
+            &d_old_pos, &d_first_old, &d_has_old, &d_pplans, &d_lines, &d_idx_filter, &d_spill,
+            &d_old_idx_filter};
+  }
 };
 
 extern "C" const char* rf_amd_last_error(void) { return g_err.c_str(); }
@@ -190,7 +233,7 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
 extern "C" void rf_amd_engine_destroy(rf_amd_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
-  (void)hipStreamSynchronize(e->stream);
+  (void)hipDeviceSynchronize();
   (void)hipStreamDestroy(e->stream);
   e->pool.drain();
   if (e->stage.h) (void)hipHostFree(e->stage.h);
@@ -454,6 +497,31 @@ extern "C" void rf_amd_batch_destroy(rf_amd_batch* b) {
   // once the device is idle (what hipFree would have waited for)
   (void)hipDeviceSynchronize();
   delete b;
+}
+
+// stream-ordered destroy: every use of the batch is ordered before the current end of
+// `stream`; its device blocks are parked behind an event recorded there and reused (or
+// freed) once it completes. Returns without waiting.
+extern "C" int rf_amd_batch_destroy_on(rf_amd_batch* b, void* stream) {
+  if (!b) return 0;
+  HIPCHK(hipSetDevice(b->eng->device));
+  hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  DevPool::Parked k{};
+  hipError_t he = hipEventCreateWithFlags(&k.ev, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventRecord(k.ev, st);
+  if (he != hipSuccess) {  // fall back to the synchronising destroy
+    if (k.ev) (void)hipEventDestroy(k.ev);
+    rf_amd_batch_destroy(b);
+    return 0;
+  }
+  for (DevBuf* d : b->bufs()) {
+    if (!d->p) continue;
+    k.blocks.emplace_back(d->p, d->pool == &b->eng->pool ? d->n : 0);
+    d->p = nullptr;
+  }
+  b->eng->pool.park(std::move(k));
+  delete b;
+  return 0;
 }
 
 extern "C" int rf_amd_engine_pool_stats(rf_amd_engine* e, uint64_t* pooled_bytes, uint64_t* hits, uint64_t* misses) {
@@ -805,12 +873,18 @@ extern "C" int rf_amd_batch_info(rf_amd_batch* b, uint32_t f, rf_amd_filter_info
 }
 
 // every filter's info with one copy (rf_amd_batch_info per filter synchronises F times)
-extern "C" int rf_amd_batch_infos(rf_amd_batch* b, rf_amd_filter_info* out) {
+extern "C" int rf_amd_batch_infos(rf_amd_batch* b, rf_amd_filter_info* out, void* stream) {
   if (!b || !out) return fail(RF_AMD_EINVAL, "bad batch");
   HIPCHK(hipSetDevice(b->eng->device));
   std::vector<FilterOut> o(b->F);
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost));
+  if (stream) {  // the build was issued on `stream`: wait for it alone
+    HIPCHK(hipMemcpyAsync(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost,
+                          (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  } else {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost));
+  }
   for (uint32_t f = 0; f < b->F; f++) {
     const FilterPlan& p = b->plans[f];
     out[f].num_fingerprints = p.num_fp;

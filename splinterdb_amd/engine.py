@@ -46,7 +46,7 @@ EXPORTED = [
     "rf_amd_hash_keys", "rf_amd_hash_var_keys",
     "rf_amd_batch_export", "rf_amd_batch_import", "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
     "rf_amd_batch_build_hashes_host", "rf_amd_batch_probe_hashes_host", "rf_amd_engine_pool_stats",
-    "rf_amd_filter_print_abs", "rf_amd_batch_infos",
+    "rf_amd_filter_print_abs", "rf_amd_batch_infos", "rf_amd_batch_destroy_on",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -164,7 +164,8 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_probe_hashes_host.argtypes = [vp, vp, vp, u64, vp]
     L.rf_amd_engine_pool_stats.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
     L.rf_amd_filter_print_abs.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), u64, vp, vp]
-    L.rf_amd_batch_infos.argtypes = [vp, ctypes.POINTER(RfFilterInfo)]
+    L.rf_amd_batch_infos.argtypes = [vp, ctypes.POINTER(RfFilterInfo), vp]
+    L.rf_amd_batch_destroy_on.argtypes = [vp, vp]
     _lib = L
     return L
 
@@ -208,6 +209,12 @@ class Engine:
         _check(L.rf_amd_engine_create(device, ctypes.byref(h)))
         self.h = h
         self.device = device
+
+    def pool_stats(self):
+        """device-memory pool of the engine's batches: bytes held, hits, misses"""
+        v = [ctypes.c_uint64() for _ in range(3)]
+        _check(load_library().rf_amd_engine_pool_stats(self.h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("pooled_bytes", "hits", "misses"), (x.value for x in v)))
 
     def close(self):
         if self.h:
@@ -595,9 +602,15 @@ class FilterBatch:
         infos = [self.info(f) for f in range(self.F)]
         return infos, sum(i.num_pages for i in infos) * self.cfg.page_size, sum(i.num_indices for i in infos)
 
-    def close(self):
+    def close(self, stream=None):
+        """release the batch; with `stream`, stream-ordered (rf_amd_batch_destroy_on: every
+        use of the batch must be ordered before the stream's current end), else after a
+        device synchronisation"""
         if getattr(self, "h", None):
-            load_library().rf_amd_batch_destroy(self.h)
+            if stream is not None:
+                _check(load_library().rf_amd_batch_destroy_on(self.h, _stream(stream)))
+            else:
+                load_library().rf_amd_batch_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -680,10 +693,11 @@ class FilterBatch:
         _check(load_library().rf_amd_batch_info(self.h, f, ctypes.byref(out)))
         return out
 
-    def infos(self):
-        """every filter's RfFilterInfo (one synchronisation)"""
+    def infos(self, stream=None):
+        """every filter's RfFilterInfo (one synchronisation: with `stream`, the build's
+        stream, or the whole device)"""
         arr = (RfFilterInfo * self.F)()
-        _check(load_library().rf_amd_batch_infos(self.h, arr))
+        _check(load_library().rf_amd_batch_infos(self.h, arr, _stream(stream)))
         return list(arr)
 
     def read_image_async(self, f, h_pages, h_slots, stream=None):

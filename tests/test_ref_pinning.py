@@ -127,6 +127,8 @@ def test_sha_fixtures_are_reference_images(stacks):
         sh = json.load(fh)
     s = stacks()
     for key, want in sh.items():
+        if key.startswith("chain_"):
+            continue  # made by the reference itself: test_chain_fixtures_match_oracle
         if key.startswith("rand24_n"):
             n = int(key.split("_n")[1].split("_")[0])
             keys = K.random_keys(n)
@@ -139,6 +141,28 @@ def test_sha_fixtures_are_reference_images(stacks):
         assert (img.num_unique, img.num_pages) == (want["num_unique"], want["num_pages"]), key
         assert hashlib.sha256(img.pages.tobytes()).hexdigest() == want["pages_sha256"], key
         assert hashlib.sha256(img.slots.tobytes()).hexdigest() == want["slots_sha256"], key
+
+
+def test_chain_fixtures_match_oracle(oracle):
+    """the compaction-chain SHA-256s (bench.py --workload compaction; made by the reference's
+    own incremental adds, oracle/gen_golden.py gen_chain_sha) equal the oracle restatement's
+    chains: filter g, round v adds keys (g << 32) + (v + 1) j under value v"""
+    with open(os.path.join(GOLD, "sha256.json")) as fh:
+        sh = json.load(fh)
+    cfg = oracle.make_config()
+    chains = {k: v for k, v in sh.items() if k.startswith("chain_")}
+    assert chains
+    for key, want in chains.items():
+        g = int(key.split("_f")[1].split("_")[0])
+        V = int(key.split("_v")[1].split("_")[0])
+        n = int(key.split("_n")[1].split("_")[0])
+        filt = None
+        for v in range(V):
+            ids = (np.uint64(g) << np.uint64(32)) + np.uint64(v + 1) * np.arange(n, dtype=np.uint64)
+            filt = oracle.filter_add(cfg, oracle.hash_fixed(K.ids_keys(ids).reshape(-1), 24), value=v, old=filt)
+        assert (filt.num_unique, filt.num_pages) == (want["num_unique"], want["num_pages"]), key
+        assert hashlib.sha256(filt.pages().tobytes()).hexdigest() == want["pages_sha256"], key
+        assert hashlib.sha256(filt.slots()[: filt.num_indices].tobytes()).hexdigest() == want["slots_sha256"], key
 
 
 def test_filter_test_basic_chain_matches_oracle(stacks, oracle):
