@@ -24,6 +24,7 @@ using namespace rf;
 
 extern "C" int rf_launch_build(const LaunchArgs* a);
 extern "C" int rf_launch_old_decode(const LaunchArgs* a);
+extern "C" int rf_launch_wave_tab(void* stream, const uint64_t* runs, uint32_t nf, uint64_t n, uint32_t* tab);
 extern "C" int rf_launch_plines(const LaunchArgs* a);
 extern "C" int rf_launch_build_init(void* stream, uint32_t* cb_count, uint32_t* cb_cursor, uint32_t num_cb,
                                     uint32_t* outs_words, uint32_t num_out_words, uint32_t* overflow,
@@ -186,7 +187,7 @@ struct rf_amd_batch {
   uint64_t NL = 0;         // probe lines (64 B each)
   bool plines_needed = false;  // some filter's lines come from k_plines
   uint32_t line_lmax = 0;  // max probe lines per index
-  DevBuf d_runs;                    // probe run bounds (rf_amd_batch_probe_*_runs)
+  DevBuf d_runs, d_wave_tab;        // probe run bounds (rf_amd_batch_probe_*_runs), their wave table
   std::vector<uint64_t> runs_host;  // their last uploaded value
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
@@ -199,7 +200,7 @@ struct rf_amd_batch {
     for (auto ev : events) (void)hipEventDestroy(ev);
   }
   std::vector<DevBuf*> bufs() {
-    return {&d_runs, &d_plans, &d_outs, &d_ent, &d_part, &d_sorted, &d_cb_count, &d_cb_start, &d_cb_cursor,
+    return {&d_runs, &d_wave_tab, &d_plans, &d_outs, &d_ent, &d_part, &d_sorted, &d_cb_count, &d_cb_start, &d_cb_cursor,
             &d_cb_filter, &d_overflow, &d_idx_cnt, &d_idx_start, &d_slots, &d_page_first, &d_pg_filter,
             &d_pages, &d_tile_filter, &d_tile_start, &d_old_tile_filter, &d_old_tile_start, &d_old_cnt,
             &d_old_pos, &d_first_old, &d_has_old, &d_pplans, &d_lines, &d_idx_filter, &d_spill,
@@ -723,6 +724,7 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   (void)hipGetLastError();
   LaunchArgs a = make_args(b, st);
   a.probe_runs = d_runs;
+  a.wave_tab = d_runs ? b->d_wave_tab.as<uint32_t>() : nullptr;
 #ifdef RF_PHASE_STAMPS
   a.ablate = g_probe_ablate & 0xff;
   a.occ = (g_probe_ablate >> 8) & 0xff;
@@ -761,10 +763,14 @@ static int probe_runs(rf_amd_batch* b, int kind, const void* in0, uint32_t key_l
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(b->eng->device));
   if (runs != b->runs_host) {
-    if (!b->d_runs.p && b->d_runs.alloc(8ull * (b->F + 1))) return RF_AMD_ENOMEM;
+    if (!b->d_runs.p && b->d_runs.alloc(8ull * (b->F + 1), &b->eng->pool)) return RF_AMD_ENOMEM;
     hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
     HIPCHK(hipStreamSynchronize(st));  // earlier probes may still read the old bounds
+    const uint64_t nw = (n + 63) / 64;
+    if (b->d_wave_tab.n < 4 * nw && b->d_wave_tab.alloc(4 * nw, &b->eng->pool)) return RF_AMD_ENOMEM;
     HIPCHK(hipMemcpy(b->d_runs.p, runs.data(), 8ull * (b->F + 1), hipMemcpyHostToDevice));
+    if (rf_launch_wave_tab(st, b->d_runs.as<uint64_t>(), b->F, n, b->d_wave_tab.as<uint32_t>()))
+      return fail(RF_AMD_EINVAL, "wave table launch failed");
     b->runs_host = runs;
   }
   return do_probe(b, kind, in0, nullptr, key_len, nullptr, n, d_found, stream, b->d_runs.as<uint64_t>());

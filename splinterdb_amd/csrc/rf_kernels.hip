@@ -2410,6 +2410,51 @@ __device__ __forceinline__ uint32_t run_filter(const uint64_t* __restrict__ runs
   return lo;
 }
 
+// Wave table of per-filter probe runs: entry w = (filter of probe 64 w) << 7 | the number of
+// the wave's leading probes in that filter's run (64: the whole wave). Built by k_wave_tab
+// whenever the run bounds change, so a probe wave finds its filter with ONE scalar load
+// instead of a binary search of dependent loads over the run bounds.
+__global__ __launch_bounds__(256) void k_wave_tab(const uint64_t* __restrict__ runs, uint32_t nf, uint64_t n,
+                                                  uint32_t* __restrict__ tab) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = w * WAVE;
+  if (i >= n) return;
+  uint32_t lo = 0, hi = nf;  // largest lo with runs[lo] <= i
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (runs[mid] <= i) lo = mid; else hi = mid;
+  }
+  const uint64_t left = runs[lo + 1] - i;  // runs[nf] = n
+  tab[w] = lo << 7 | (uint32_t)min<uint64_t>(left, WAVE);
+}
+
+// filter of probe i (lane `lane` of its wave) from the wave table; lanes past the wave's
+// first run boundary step forward over the run bounds
+__device__ __forceinline__ uint32_t tab_filter(const uint32_t* __restrict__ tab, const uint64_t* __restrict__ runs,
+                                               uint32_t nf, uint64_t i) {
+  const uint64_t w = i / WAVE;
+  const uint64_t wu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32)) << 32) |
+                      __builtin_amdgcn_readfirstlane((uint32_t)w);
+  const uint32_t t = tab[wu];  // wave-uniform address: a scalar load
+  uint32_t lo = t >> 7;
+  if ((uint32_t)(i & (WAVE - 1)) >= (t & 127u))
+    while (lo + 1 < nf && runs[lo + 1] <= i) lo++;
+  return lo;
+}
+
+// the probe plan of filter fid; when the whole wave probes one filter (the usual case with
+// per-filter runs) it is one scalar load
+__device__ __forceinline__ uint4 load_pplan(const uint4* __restrict__ pplans, uint32_t fid, uint32_t nf) {
+  const uint32_t fs = __builtin_amdgcn_readfirstlane(fid);
+  if (__builtin_amdgcn_ballot_w64(fid != fs) == 0) {
+    if (fs >= nf) return make_uint4(0, 0, 0, 1);
+    // constant address space: a uniform address there is always a scalar (SMEM) load
+    typedef __attribute__((address_space(4))) const uint4 cuint4;
+    return reinterpret_cast<cuint4*>(reinterpret_cast<uintptr_t>(pplans))[fs];
+  }
+  return fid < nf ? pplans[fid] : make_uint4(0, 0, 0, 1);
+}
+
 template <int KIND, int OCC_LDS = 0, int PPL = 1>
 __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
                                                     const FilterPlan* __restrict__ plans,
@@ -2419,7 +2464,8 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
                                                     const void* __restrict__ in0,
                                                     const uint64_t* __restrict__ offs, uint32_t key_len,
                                                     const uint32_t* __restrict__ filter_id,
-                                                    const uint64_t* __restrict__ runs, uint64_t n,
+                                                    const uint64_t* __restrict__ runs,
+                                                    const uint32_t* __restrict__ wave_tab, uint64_t n,
                                                     uint64_t* __restrict__ found, uint32_t fp_size,
                                                     uint32_t seed, uint32_t lis, uint32_t page_size,
                                                     uint32_t num_filters, uint32_t ablate) {
@@ -2433,6 +2479,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
 #endif
   const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (PROBE_NT * PPL) + threadIdx.x;
   uint32_t h[PPL], fid[PPL];
+  uint4 pp[PPL];
   constexpr bool WAVE_KEYS = KIND == IN_KEYS24 && PPL == 1 && OCC_LDS == 0;
   if constexpr (WAVE_KEYS) {
     // 24-byte keys: the wave's 64 keys (1,536 contiguous bytes) are read with 16-byte
@@ -2443,8 +2490,10 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     const uint64_t wf = i0 - lane;
     fid[0] = 0xffffffffu;
     h[0] = 0;
+    pp[0] = make_uint4(0, 0, 0, 1);
     if (wf < n) {  // uniform per wave
-      if (i0 < n) fid[0] = runs ? run_filter(runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
+      if (i0 < n) fid[0] = runs ? tab_filter(wave_tab, runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
+      pp[0] = load_pplan(pplans, fid[0], num_filters);  // in flight with the key loads
       if (((uintptr_t)in0 & 15) == 0) {
         v4u* sw = s_keys[threadIdx.x / WAVE];
         const uint32_t bytes = (uint32_t)min<uint64_t>(WAVE, n - wf) * 24;
@@ -2492,10 +2541,11 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     h[0] = 0;
     uint64_t o0 = 0, o1 = 0;
     if (i0 < n) {
-      fid[0] = runs ? run_filter(runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
+      fid[0] = runs ? tab_filter(wave_tab, runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
       o0 = offs[i0];
       o1 = offs[i0 + 1];
     }
+    pp[0] = load_pplan(pplans, fid[0], num_filters);
     uint64_t w0 = 0, w1 = 0;
     h[0] = wave_hash_var<VCAP, true>(static_cast<const uint8_t*>(in0), o0, o1, i0 < n,
                                      s_vk[threadIdx.x / WAVE], seed, &w0, &w1);
@@ -2513,18 +2563,18 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
         fid[q] = (uint32_t)(pr >> 32);
         h[q] = (uint32_t)pr;
       } else {
-        fid[q] = runs ? run_filter(runs, num_filters, i) : __builtin_nontemporal_load(filter_id + i);
+        fid[q] = runs ? (PPL == 1 ? tab_filter(wave_tab, runs, num_filters, i) : run_filter(runs, num_filters, i))
+                      : __builtin_nontemporal_load(filter_id + i);
         h[q] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
       }
     }
+    pp[q] = load_pplan(pplans, fid[q], num_filters);
   }
-  uint4 pp[PPL];
   uint32_t bucket[PPL], remainder[PPL];
   v4u Q[PPL][4];
 #pragma unroll
   for (int q = 0; q < PPL; q++) {
     // unknown filter, or one whose build failed (k_layout sets pp.w): nothing found
-    pp[q] = fid[q] < num_filters ? pplans[fid[q]] : make_uint4(0, 0, 0, 1);
     const uint32_t rem = (pp[q].x >> 8) & 0xff, lgl = pp[q].x >> 24;
     const uint32_t fp = h[q] >> (32 - fp_size);
     bucket[q] = rem >= 32 ? 0u : fp >> rem;  // index << lis | bucket in index
@@ -2716,6 +2766,14 @@ extern "C" int rf_launch_old_decode(const LaunchArgs* pa) {
   return 0;
 }
 
+extern "C" int rf_launch_wave_tab(void* stream, const uint64_t* runs, uint32_t nf, uint64_t n, uint32_t* tab) {
+  const uint64_t nw = (n + WAVE - 1) / WAVE;
+  if (nw == 0) return 0;
+  hipLaunchKernelGGL(k_wave_tab, dim3((uint32_t)((nw + 255) / 256)), dim3(256), 0, (hipStream_t)stream, runs, nf, n, tab);
+  CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, const uint64_t* offs,
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found) {
   const LaunchArgs& a = *pa;
@@ -2727,7 +2785,7 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
 #endif
   dim3 g((uint32_t)((n + PROBE_NT * ppl - 1) / (PROBE_NT * ppl))), b(PROBE_NT);
   REC(EV_P_START);
-#define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
+#define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, a.wave_tab, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
 #if RF_DIAG
   if (kind == IN_KEYS24 && (a.occ || a.ppl)) {  // experiment variants: waves/SIMD cap, probes per lane
     const int o = a.occ ? (int)a.occ : 8;

@@ -122,6 +122,7 @@ struct LaunchArgs {
   uint32_t occ;     // probe occupancy experiment (0 = normal)
   uint32_t ppl;     // probe probes-per-lane experiment (0 = production)
   const uint64_t* probe_runs;  // probes grouped by filter: runs[f] <= i < runs[f+1] (nullptr: per-probe ids)
+  const uint32_t* wave_tab;    // with probe_runs: per 64-probe wave, filter << 7 | leading probes in it
   void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)
 };
 
