@@ -2318,11 +2318,10 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
   }
   const uint32_t s = p1 - j;
   // c = entries of bucket j = zeros from p1 up to terminator j
-  const uint32_t q = p1 >> 5, sh = p1 & 31;
-  const uint64_t lo = q == 0 ? ((uint64_t)d1 << 32 | d0)
-                             : (q == 1 ? ((uint64_t)d2 << 32 | d1) : (q == 2 ? ((uint64_t)d3 << 32 | d2) : d3));
-  const uint32_t hi = q == 0 ? d2 : (q == 1 ? d3 : 0u);
-  const uint64_t y = (lo >> sh) | (sh ? (uint64_t)hi << (64 - sh) : 0ull);
+  // (p1 <= 128: the encoding has j + 1 <= G terminators in 128 bits)
+  const uint64_t e0 = (uint64_t)d1 << 32 | d0, e1 = (uint64_t)d3 << 32 | d2;
+  const uint64_t y = p1 >= 128 ? 0ull
+                     : (p1 >= 64 ? e1 >> (p1 - 64) : (e0 >> p1) | (p1 ? e1 << (64 - p1) : 0ull));
   if (y == 0) return false;
   const uint32_t c = (uint32_t)__builtin_ctzll(y);
   found = 0;
@@ -2448,11 +2447,52 @@ __device__ __forceinline__ uint4 load_pplan(const uint4* __restrict__ pplans, ui
   const uint32_t fs = __builtin_amdgcn_readfirstlane(fid);
   if (__builtin_amdgcn_ballot_w64(fid != fs) == 0) {
     if (fs >= nf) return make_uint4(0, 0, 0, 1);
+#if __HIP_DEVICE_COMPILE__
     // constant address space: a uniform address there is always a scalar (SMEM) load
-    typedef __attribute__((address_space(4))) const uint4 cuint4;
-    return reinterpret_cast<cuint4*>(reinterpret_cast<uintptr_t>(pplans))[fs];
+    typedef __attribute__((address_space(4))) const uint32_t cu32;
+    const cu32* c = reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(pplans + fs));
+    return make_uint4(c[0], c[1], c[2], c[3]);
+#else
+    return pplans[fs];
+#endif
   }
   return fid < nf ? pplans[fid] : make_uint4(0, 0, 0, 1);
+}
+
+// The line half of one probe once its hash and probe plan P are known: bucket, remainder,
+// the probe line and its decode. Returns false when the image must be walked instead
+// (overflowed line, a bucket too large for the window, or a filter without lines). When the
+// whole wave probes one filter, k_probe passes P as wave-uniform values, so everything
+// derived from the plan alone (widths, masks, the SWAR field pattern) is computed once per
+// wave in scalar registers.
+__device__ __forceinline__ bool probe_line(const uint4 P, uint32_t h, const uint4* __restrict__ lines,
+                                           uint32_t fp_size, uint64_t& r) {
+  const uint32_t vs = P.x & 0xff, rem = (P.x >> 8) & 0xff, rvs = (P.x >> 16) & 0xff, lgl = P.x >> 24;
+  r = 0;
+  if (P.w) return true;  // unknown filter, or its build failed: nothing found
+  if (!lgl) return false;
+  const uint32_t fp = h >> (32 - fp_size);
+  const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;  // index << lis | bucket in index
+  const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+  const v4u* lp = reinterpret_cast<const v4u*>(lines + ((uint64_t)P.y + (bucket >> (lgl - 1))) * 4);
+  v4u Q[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) Q[k] = lp[k];
+  return line_decode(Q, bucket & ((1u << (lgl - 1)) - 1), remainder, vs, rvs, r);
+}
+
+// the image walk of one probe (probe_stream from its index slot)
+__device__ __forceinline__ uint64_t probe_walk(const uint4 P, uint32_t h, uint32_t fid,
+                                               const FilterPlan* __restrict__ plans,
+                                               const uint8_t* __restrict__ pages, const uint64_t* __restrict__ slots,
+                                               uint32_t fp_size, uint32_t lis, uint32_t page_size) {
+  const uint32_t vs = P.x & 0xff, rem = (P.x >> 8) & 0xff, rvs = (P.x >> 16) & 0xff;
+  const uint32_t fp = h >> (32 - fp_size);
+  const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
+  const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+  const uint64_t hdr = slots[P.z + (bucket >> lis)];
+  const uint8_t* pg = pages + (uint64_t)plans[fid].page_base * page_size;
+  return probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, pg, hdr, lis);
 }
 
 template <int KIND, int OCC_LDS = 0, int PPL = 1>
@@ -2570,6 +2610,24 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     }
     pp[q] = load_pplan(pplans, fid[q], num_filters);
   }
+#if !RF_DIAG
+  if constexpr (PPL == 1) {
+    if (i0 >= n) return;
+    const uint32_t fs = __builtin_amdgcn_readfirstlane(fid[0]);
+    uint64_t r;
+    bool ok;
+    if (__builtin_amdgcn_ballot_w64(fid[0] != fs) == 0) {
+      const uint4 U = make_uint4(__builtin_amdgcn_readfirstlane(pp[0].x), __builtin_amdgcn_readfirstlane(pp[0].y),
+                                 __builtin_amdgcn_readfirstlane(pp[0].z), __builtin_amdgcn_readfirstlane(pp[0].w));
+      ok = probe_line(U, h[0], lines, fp_size, r);
+    } else {
+      ok = probe_line(pp[0], h[0], lines, fp_size, r);
+    }
+    if (!ok) r = probe_walk(pp[0], h[0], fid[0], plans, pages, slots, fp_size, lis, page_size);
+    __builtin_nontemporal_store(r, found + i0);
+    return;
+  }
+#endif
   uint32_t bucket[PPL], remainder[PPL];
   v4u Q[PPL][4];
 #pragma unroll

@@ -58,7 +58,14 @@ for shape, (F, n) in shapes.items():
     ref = libs[0][3]
     same = all(torch.equal(ref, x[3]) for x in libs[1:])
     allfound = bool(((ref & 1) == 1).all())
-    out[shape] = {"identical": same, "all_found": allfound,
+    diff = {}
+    for name, _, _, fo, *_ in libs[1:]:
+        bad = torch.nonzero(ref != fo).flatten()
+        if bad.numel():
+            sel = bad[:12]
+            diff[name] = {"count": int(bad.numel()), "idx": sel.tolist(), "want": ref[sel].tolist(),
+                          "got": fo[sel].tolist(), "lanes_in_wave": (sel % 64).tolist()}
+    out[shape] = {"identical": same, "all_found": allfound, "diff": diff,
                   **{k: {m: round(float(np.median(v[m][1:])), 4) for m in v} for k, v in res.items()}}
     for name, L, b, *_ in libs:
         L.rf_amd_batch_destroy(b)
