@@ -179,6 +179,8 @@ struct rf_amd_batch {
   rf_amd_config cfg{};
   uint32_t F = 0;
   bool wide = false;
+  bool flag32 = false;      // wide build with 32-bit flagged entries (every fp_size + vs <= 31)
+  uint64_t old_total = 0;   // flag32: decoded old entries reserved (sum of old num_fingerprints)
   std::vector<FilterPlan> plans;
   std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter, idx_filter,
       old_idx_filter;
@@ -192,7 +194,7 @@ struct rf_amd_batch {
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
       d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill,
-      d_old_idx_filter;
+      d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
@@ -204,7 +206,7 @@ struct rf_amd_batch {
             &d_cb_filter, &d_overflow, &d_idx_cnt, &d_idx_start, &d_slots, &d_page_first, &d_pg_filter,
             &d_pages, &d_tile_filter, &d_tile_start, &d_old_tile_filter, &d_old_tile_start, &d_old_cnt,
             &d_old_pos, &d_first_old, &d_has_old, &d_pplans, &d_lines, &d_idx_filter, &d_spill,
-            &d_old_idx_filter};
+            &d_old_idx_filter, &d_old32, &d_old_tot, &d_ob_lo, &d_ob_n};
   }
 };
 
@@ -376,6 +378,8 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       p.old_pages = ob->d_pages.as<uint8_t>() + (uint64_t)op->page_base * P;
       p.old_slots = ob->d_slots.as<uint64_t>() + op->idx_base;
       p.old_idx_base = (uint32_t)b->old_idx_filter.size();
+      p.old_first = b->old_total;
+      b->old_total += p.old_region;
       b->old_idx_filter.insert(b->old_idx_filter.end(), op->num_indices, f);
     }
     for (uint32_t s = 0; s < p.num_new; s += TILE_KEYS) {
@@ -405,6 +409,11 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       e_first += (uint64_t)SORT_CAP << p.cbits;
     }
   }
+  if (b->wide) {
+    // 32-bit entries when (e << 1) | flag fits: fp_size + value_size <= 31 in every filter
+    b->flag32 = getenv("RF_AMD_WIDE64") == nullptr;
+    for (const auto& p : b->plans) b->flag32 = b->flag32 && fps + p.vs <= 31;
+  }
   b->E = e_first;
   b->keys_total = key_first;
   b->CB = cb_base;
@@ -416,7 +425,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     return fail(RF_AMD_EINVAL, "batch too large (probe lines > 2^32)");
   }
   b->NL = line_base;
-  const size_t esz = b->wide ? 8 : 4;
+  const size_t esz = (b->wide && !b->flag32) ? 8 : 4;
   int rc = 0;
   DevPool* pool = &e->pool;
   rc |= b->d_plans.alloc(sizeof(FilterPlan) * num_filters, pool);
@@ -449,6 +458,12 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     rc |= b->d_old_idx_filter.alloc(4 * b->old_idx_filter.size(), pool);
     rc |= b->d_first_old.alloc(4 * b->I, pool);
     rc |= b->d_has_old.alloc(4 * b->I, pool);
+    if (b->flag32) {
+      rc |= b->d_old32.alloc(4 * b->old_total + 64, pool);
+      rc |= b->d_old_tot.alloc(4 * b->F, pool);
+      rc |= b->d_ob_lo.alloc(4 * b->CB, pool);
+      rc |= b->d_ob_n.alloc(4 * b->CB, pool);
+    }
   }
   if (rc) {
     delete b;
@@ -465,7 +480,8 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     // build, or leaving page bytes unwritten, cannot pass the parity tests
     const int v = atoi(pz) & 0xff;
     for (DevBuf* d : {&b->d_ent, &b->d_part, &b->d_sorted, &b->d_cb_start, &b->d_idx_cnt, &b->d_idx_start,
-                      &b->d_slots, &b->d_lines, &b->d_page_first, &b->d_pages, &b->d_first_old, &b->d_has_old})
+                      &b->d_slots, &b->d_lines, &b->d_page_first, &b->d_pages, &b->d_first_old, &b->d_has_old,
+                      &b->d_old32, &b->d_old_tot, &b->d_ob_lo, &b->d_ob_n})
       if (d->p) HIPCHK(hipMemsetAsync(d->p, v, d->n, st));
   }
 #define UP(buf, vec) \
@@ -555,6 +571,11 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.num_old_idx = (uint32_t)b->old_idx_filter.size();
   a.old_cnt = b->d_old_cnt.as<uint32_t>();
   a.old_pos = b->d_old_pos.as<uint32_t>();
+  a.flag32 = b->flag32 ? 1u : 0u;
+  a.old32 = b->d_old32.as<uint32_t>();
+  a.old_tot = b->d_old_tot.as<uint32_t>();
+  a.ob_lo = b->d_ob_lo.as<uint32_t>();
+  a.ob_n = b->d_ob_n.as<uint32_t>();
   a.fp_size = b->cfg.fingerprint_size;
   a.seed = b->cfg.seed;
   a.lis = b->cfg.log_index_size;

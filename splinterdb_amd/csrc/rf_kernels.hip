@@ -96,7 +96,7 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
 // ======================================================================================
 // K1: hash + coarse-bucket histogram
 // ======================================================================================
-template <int KIND, typename EntT>
+template <int KIND, typename EntT, bool FL = (sizeof(EntT) == 8)>
 __global__ __launch_bounds__(TILE_NT) void k_hash_count(const FilterPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ tile_filter,
                                                         const uint32_t* __restrict__ tile_start,
@@ -119,8 +119,8 @@ __global__ __launch_bounds__(TILE_NT) void k_hash_count(const FilterPlan* __rest
   for (uint32_t j = threadIdx.x; j < count; j += TILE_NT) {
     const uint32_t h = hash_key<KIND>(in0, offs, key_len, seed, P.key_first + start + j);
     const uint32_t e = ((h >> (32 - fp_size)) << P.vs) | P.value;
-    if constexpr (sizeof(EntT) == 8) {
-      ent[P.e_first + start + j] = ((uint64_t)e << 1) | 1ull;  // new entry: flag 1
+    if constexpr (FL) {
+      ent[P.e_first + start + j] = (EntT)(((EntT)e << 1) | EntT(1));  // new entry: flag 1
     } else {
       ent[P.e_first + start + j] = e;
     }
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256) void k_cb_scan(const FilterPlan* __restrict__ 
 // ======================================================================================
 // K3: scatter entries into coarse buckets
 // ======================================================================================
-template <typename EntT>
+template <typename EntT, bool FL = (sizeof(EntT) == 8)>
 __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ tile_filter,
                                                      const uint32_t* __restrict__ tile_start,
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
   const uint32_t esh = fp_size + P.vs - P.cbits;
   auto cb_of = [&](EntT x) -> uint32_t {
     uint32_t e;
-    if constexpr (sizeof(EntT) == 8) e = (uint32_t)(x >> 1);
+    if constexpr (FL) e = (uint32_t)(x >> 1);
     else e = x;
     return P.cbits ? (e >> esh) : 0u;
   };
@@ -504,16 +504,18 @@ __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(4))) vo
 // ======================================================================================
 // K4: per coarse bucket sort / dedupe / index counts
 // ======================================================================================
-template <typename EntT>
+// Entries: e = (fp << vs) | value, or, in incremental builds (FL), (e << 1) | new-flag --
+// 64-bit, or 32-bit when fp_size + value_size <= 31 leaves room for the flag.
+template <typename EntT, bool FL = (sizeof(EntT) == 8)>
 __device__ __forceinline__ uint32_t ent_e(EntT x) {
-  if constexpr (sizeof(EntT) == 8) return (uint32_t)(x >> 1);
+  if constexpr (FL) return (uint32_t)(x >> 1);
   else return x;
 }
 // dedupe rule (src/routing_filter.c:471-482 for new entries; old entries are never
 // deduplicated, :559-597): drop x if it equals its predecessor and is a new entry.
-template <typename EntT>
+template <typename EntT, bool FL = (sizeof(EntT) == 8)>
 __device__ __forceinline__ bool ent_drop(EntT x, EntT prev) {
-  if constexpr (sizeof(EntT) == 8) return x == prev && (x & 1ull);
+  if constexpr (FL) return x == prev && (x & EntT(1));
   else return x == prev;
 }
 
@@ -581,12 +583,18 @@ __device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_
   *uniq_out = uniq;
 }
 
-template <typename EntT>
+// DUAL (32-bit incremental builds): a coarse bucket's entries come from two places -- its
+// new entries, scattered into part, and its run of the old filter's decoded entries
+// (already in order: old32 + P.old_first + ob_lo[cb], ob_n[cb] of them), loaded as (e << 1).
+template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ cb_filter,
                                                      const uint32_t* __restrict__ cb_count,
                                                      const uint32_t* __restrict__ cb_start,
                                                      const EntT* __restrict__ part,
+                                                     const uint32_t* __restrict__ old32,
+                                                     const uint32_t* __restrict__ ob_lo,
+                                                     const uint32_t* __restrict__ ob_n,
                                                      uint32_t* __restrict__ sorted32,
                                                      uint32_t* __restrict__ idx_cnt,
                                                      uint32_t* __restrict__ idx_start,
@@ -600,8 +608,8 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   __shared__ EntT s_b[SORT_CAP];
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[MAX_BINS + 1];
   __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
-  __shared__ uint32_t s_fo[sizeof(EntT) == 8 ? MAX_IPC : 1];
-  __shared__ uint32_t s_ho[sizeof(EntT) == 8 ? MAX_IPC : 1];
+  __shared__ uint32_t s_fo[FL ? MAX_IPC : 1];
+  __shared__ uint32_t s_ho[FL ? MAX_IPC : 1];
   constexpr uint32_t BIG_LIST = 64;
   __shared__ uint32_t s_big[BIG_LIST];  // bins over 8 entries (s_nbig may exceed the list)
   __shared__ uint32_t s_nbig;
@@ -628,10 +636,20 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   uint32_t r[PER];
   const EntT* src = part + P.e_first + c.cb_rel;
   const uint32_t nm1 = n ? n - 1 : 0u;
+  if constexpr (DUAL) {
+    const uint32_t nn = n - ob_n[cb];  // new entries first, then the old run
+    const uint32_t* osrc = old32 + P.old_first + ob_lo[cb];
 #pragma unroll
-  for (int k = 0; k < PER; k++) v[k] = src[min(threadIdx.x + k * SORT_NT, nm1)];
+    for (int k = 0; k < PER; k++) {
+      const uint32_t j = min(threadIdx.x + k * SORT_NT, nm1);
+      v[k] = j < nn ? src[j] : (EntT)(osrc[j - nn] << 1);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < PER; k++) v[k] = src[min(threadIdx.x + k * SORT_NT, nm1)];
+  }
   for (uint32_t i = threadIdx.x; i <= nbins; i += SORT_NT) s_bin[i] = 0;
-  if constexpr (sizeof(EntT) == 8) {
+  if constexpr (FL) {
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
   if (threadIdx.x == 0) s_nbig = 0;
@@ -643,7 +661,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     if (threadIdx.x + k * SORT_NT < n) {
-      const uint32_t e = ent_e(v[k]);
+      const uint32_t e = ent_e<EntT, FL>(v[k]);
       const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
       r[k] = atomicAdd(&s_bin[b], 1u);
     }
@@ -687,7 +705,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   for (int k = 0; k < PER; k++) {
     const uint32_t i = threadIdx.x + k * SORT_NT;
     if (i < n) {
-      const uint32_t e = ent_e(v[k]);
+      const uint32_t e = ent_e<EntT, FL>(v[k]);
       const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
       s_b[s_bin[b] + r[k]] = v[k];
     }
@@ -801,7 +819,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       const uint32_t i = i0 + k;
       if ((uint32_t)k < drun && i < n) {
         w[k] = s_b[i];
-        const bool drop = (i > 0) && ent_drop(w[k], prev);
+        const bool drop = (i > 0) && ent_drop<EntT, FL>(w[k], prev);
         if (!drop) { keep_mask |= 1u << k; cnt++; }
         prev = w[k];
       }
@@ -817,22 +835,22 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   // previous entry's; an index's first entry compares against UINT32_MAX >> value_size.
   const uint32_t NONE = 0xffffffffu;
   auto index_of = [&](uint32_t e) -> uint32_t { return ish >= 32 ? 0u : ((e >> ish) & (ipc - 1)); };
-  uint32_t lprev = (i0 > 0 && i0 <= n) ? index_of(ent_e(prev0)) : NONE;
-  uint32_t fprev = (i0 > 0 && i0 <= n) ? (ent_e(prev0) >> P.vs) : 0u;
+  uint32_t lprev = (i0 > 0 && i0 <= n) ? index_of(ent_e<EntT, FL>(prev0)) : NONE;
+  uint32_t fprev = (i0 > 0 && i0 <= n) ? (ent_e<EntT, FL>(prev0) >> P.vs) : 0u;
   uint32_t uniq = 0;
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t i = i0 + k;
     if ((uint32_t)k < drun && i < n) {
-      const uint32_t e = ent_e(w[k]);
+      const uint32_t e = ent_e<EntT, FL>(w[k]);
       const uint32_t li = index_of(e), fp = e >> P.vs;
       if (keep_mask & (1u << k)) {
         s_sorted[pos] = e;
         for (uint32_t l = lprev + 1; l <= li; l++) s_first[l] = pos;  // lprev NONE: from 0
         uniq += (fp != (li != lprev ? (0xffffffffu >> P.vs) : fprev)) ? 1u : 0u;
         pos++;
-        if constexpr (sizeof(EntT) == 8) {
-          if (!(w[k] & 1ull)) {  // old entry: remember each index's smallest (num_unique quirk)
+        if constexpr (FL) {
+          if (!(w[k] & EntT(1))) {  // old entry: remember each index's smallest (num_unique quirk)
             atomicMin(&s_fo[li], e);
             s_ho[li] = 1;
           }
@@ -850,7 +868,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       if (llast == NONE || l > llast) s_first[l] = kept;
     if (threadIdx.x == 0) s_first[ipc] = kept;
   }
-  if constexpr (sizeof(EntT) == 8) {
+  if constexpr (FL) {
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) {
       first_old[c.idx0 + i] = s_fo[i];
       has_old[c.idx0 + i] = s_ho[i];
@@ -873,12 +891,15 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
 
 // K4b: coarse buckets larger than LDS (duplicate-heavy inputs). One workgroup per listed
 // bucket, working in global memory: `scratch` is the K1 entry array (free after K3).
-template <typename EntT>
+template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ cb_filter,
                                                         const uint32_t* __restrict__ cb_count,
                                                         const uint32_t* __restrict__ cb_start,
                                                         const EntT* __restrict__ part,
+                                                        const uint32_t* __restrict__ old32,
+                                                        const uint32_t* __restrict__ ob_lo,
+                                                        const uint32_t* __restrict__ ob_n,
                                                         EntT* __restrict__ scratch,
                                                         uint32_t* __restrict__ sorted32,
                                                         uint32_t* __restrict__ idx_cnt,
@@ -902,7 +923,10 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     const uint32_t cbl = cb - P.cb_base;
     CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_start[cb], P.e_first};
     const uint32_t nbins = 1u << P.bbits, bmask = nbins - 1;
-    const EntT* src = part + P.e_first + c.cb_rel;
+    const EntT* srcp = part + P.e_first + c.cb_rel;
+    const uint32_t nn = DUAL ? n - ob_n[cb] : n;
+    const uint32_t* osrc = DUAL ? old32 + P.old_first + ob_lo[cb] : nullptr;
+    auto src = [&](uint32_t i) -> EntT { return (!DUAL || i < nn) ? srcp[i] : (EntT)(osrc[i - nn] << 1); };
     EntT* tmp = scratch + P.e_first + c.cb_rel;
     uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
     const uint32_t ipc = 1u << (P.bbits - lis), ish = lis + P.rvs;
@@ -910,7 +934,7 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     for (uint32_t i = threadIdx.x; i < ipc; i += BIG_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += BIG_NT) {
-      const uint32_t e = ent_e(src[i]);
+      const uint32_t e = ent_e<EntT, FL>(src(i));
       atomicAdd(&s_bin[P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask)], 1u);
     }
     __syncthreads();
@@ -926,8 +950,8 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += BIG_NT) {
-      const EntT x = src[i];
-      const uint32_t e = ent_e(x);
+      const EntT x = src(i);
+      const uint32_t e = ent_e<EntT, FL>(x);
       tmp[atomicAdd(&s_cur[P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask)], 1u)] = x;
     }
     __syncthreads();
@@ -952,16 +976,16 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
       EntT x = 0;
       if (i < n) {
         x = tmp[i];
-        keep = (i == 0 || !ent_drop(x, tmp[i - 1])) ? 1u : 0u;
+        keep = (i == 0 || !ent_drop<EntT, FL>(x, tmp[i - 1])) ? 1u : 0u;
       }
       uint32_t tot;
       const uint32_t p = block_excl_scan<BIG_NT>(keep, s_tmp, &tot);
       const uint32_t run = s_run;
       if (keep) {
-        dst[run + p] = ent_e(x);
-        if constexpr (sizeof(EntT) == 8) {
-          if (!(x & 1ull)) {
-            const uint32_t e = ent_e(x);
+        dst[run + p] = ent_e<EntT, FL>(x);
+        if constexpr (FL) {
+          if (!(x & EntT(1))) {
+            const uint32_t e = ent_e<EntT, FL>(x);
             const uint32_t li = ish >= 32 ? 0u : ((e >> ish) & (ipc - 1));
             atomicMin(&s_fo[li], e);
             s_ho[li] = 1;
@@ -973,7 +997,7 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
       __syncthreads();
     }
     const uint32_t kept = s_run;
-    if constexpr (sizeof(EntT) == 8) {
+    if constexpr (FL) {
       for (uint32_t i = threadIdx.x; i < ipc; i += BIG_NT) {
         first_old[c.idx0 + i] = s_fo[i];
         has_old[c.idx0 + i] = s_ho[i];
@@ -1692,9 +1716,11 @@ __global__ void k_old_counts(const FilterPlan* __restrict__ plans, const uint32_
 // one workgroup per filter: exclusive scan of its old indices' counts -> pos (filter-relative),
 // and the sentinel (~0) on the entry slots past the decoded entries (old_region counts the old
 // filter's num_fingerprints, duplicates included; k_old_count / k_scatter skip sentinels)
+// (32-bit incremental builds: ent is null -- no sentinels -- and old_tot[f] gets the total)
 __global__ __launch_bounds__(LAYOUT_NT) void k_old_scan(const FilterPlan* __restrict__ plans,
                                                         const uint32_t* __restrict__ cnt,
-                                                        uint32_t* __restrict__ pos, uint64_t* __restrict__ ent) {
+                                                        uint32_t* __restrict__ pos, uint64_t* __restrict__ ent,
+                                                        uint32_t* __restrict__ old_tot) {
   __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
   const FilterPlan& P = plans[blockIdx.x];
   const uint32_t n = P.old_num_indices;
@@ -1715,18 +1741,22 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_old_scan(const FilterPlan* __rest
     if (i < n) pos[P.old_idx_base + i] = run;
     run += v[k];
   }
+  if (old_tot && threadIdx.x == 0) old_tot[blockIdx.x] = total;
+  if (!ent) return;
   uint64_t* tail = ent + P.e_first + P.num_new;
   for (uint32_t j = total + threadIdx.x; j < P.old_region; j += LAYOUT_NT) tail[j] = ~0ull;
 }
 
 // k_old_decode: one wave per old index. Entry k of the block: bucket offset = number of
 // 1-bits before its 0-bit in the encoding (routing_get_bucket_counts, :281-306); value
-// bits re-widened to the new value_size (:536-543). Written as (e << 1) | 0 (old flag).
+// bits re-widened to the new value_size (:536-543). Written as (e << 1) | 0 (old flag) into
+// the 64-bit entry array, or (32-bit incremental builds, old32 set) as e into the filter's
+// run of old32 -- in order, since the old image holds its entries sorted.
 __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict__ plans,
                                                     const uint32_t* __restrict__ old_idx_filter,
                                                     uint32_t num_old_idx, const uint32_t* __restrict__ pos,
-                                                    uint64_t* __restrict__ ent, uint32_t lis,
-                                                    uint32_t fp_size) {
+                                                    uint64_t* __restrict__ ent, uint32_t* __restrict__ old32,
+                                                    uint32_t lis, uint32_t fp_size) {
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   if (g >= num_old_idx) return;  // uniform per wave
@@ -1740,7 +1770,8 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
   const uint64_t ebit = (hdr + 2) * 8;
   const uint64_t rbit = (hdr + 2 + enc) * 8;
   const uint32_t total_bits = c + index_size;
-  uint64_t* out = ent + P.e_first + P.num_new + pos[g];
+  uint64_t* out = old32 ? nullptr : ent + P.e_first + P.num_new + pos[g];
+  uint32_t* out32 = old32 ? old32 + P.old_first + pos[g] : nullptr;
   const uint32_t old_vmask = (uint32_t)((1ull << P.old_vs) - 1);
   // walk the encoding 64 bits per lane-step: each lane takes one 64-bit chunk per round
   uint32_t zeros_before = 0, ones_before = 0;
@@ -1774,12 +1805,45 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
       const uint32_t old_value = e_old & old_vmask;
       const uint32_t fpv = e_old >> P.old_vs;
       const uint32_t e = (fpv << P.vs) | old_value;
-      out[k] = (uint64_t)e << 1;
+      if (out32) out32[k] = e;
+      else out[k] = (uint64_t)e << 1;
       k++;
     }
     ones_before = __shfl(ones_ex + ones, WAVE - 1, WAVE);
     zeros_before = __shfl(zer_ex + zer, WAVE - 1, WAVE);
   }
+}
+
+// 32-bit incremental builds: each coarse bucket's run of the filter's old entries. The old
+// entries are sorted, so the run of coarse bucket c starts at the first entry >= c << esh;
+// one thread per coarse bucket, then cb_count (the new entries' histogram) += run length.
+__global__ __launch_bounds__(256) void k_old_cb_bounds(const FilterPlan* __restrict__ plans,
+                                                       const uint32_t* __restrict__ cb_filter, uint32_t num_cb,
+                                                       const uint32_t* __restrict__ old32,
+                                                       const uint32_t* __restrict__ old_tot, uint32_t fp_size,
+                                                       uint32_t* __restrict__ ob_lo, uint32_t* __restrict__ ob_n,
+                                                       uint32_t* __restrict__ cb_count) {
+  const uint32_t cb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cb >= num_cb) return;
+  const uint32_t f = cb_filter[cb];
+  const FilterPlan& P = plans[f];
+  const uint32_t cl = cb - P.cb_base, ncb = 1u << P.cbits;
+  const uint32_t tot = P.old_num_indices ? old_tot[f] : 0u;
+  const uint32_t* o = old32 + P.old_first;
+  const uint32_t esh = fp_size + P.vs - P.cbits;
+  auto lb = [&](uint32_t c) -> uint32_t {  // first entry whose coarse bucket >= c
+    uint32_t lo = 0, hi = tot;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((o[mid] >> esh) < c) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  const uint32_t lo = (P.cbits == 0 || cl == 0) ? 0u : lb(cl);
+  const uint32_t hi = cl + 1 == ncb ? tot : lb(cl + 1);
+  ob_lo[cb] = lo;
+  ob_n[cb] = hi - lo;
+  cb_count[cb] += hi - lo;
 }
 
 // ======================================================================================
@@ -2695,10 +2759,10 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
   }
 
 // counts: per coarse bucket counter array (atomically accumulated); gate: see k_hash_count
-template <typename EntT>
+template <typename EntT, bool FL = (sizeof(EntT) == 8)>
 static int launch_hash_count_t(const LaunchArgs& a, EntT* ent, uint32_t* counts, const uint32_t* gate) {
   dim3 g(a.num_tiles), b(TILE_NT);
-#define L(K) hipLaunchKernelGGL((k_hash_count<K, EntT>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, \
+#define L(K) hipLaunchKernelGGL((k_hash_count<K, EntT, FL>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, \
                                 a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, counts, gate)
   KIND_SWITCH(a.kind, L);
 #undef L
@@ -2706,30 +2770,30 @@ static int launch_hash_count_t(const LaunchArgs& a, EntT* ent, uint32_t* counts,
   return 0;
 }
 
-template <typename EntT>
+template <typename EntT, bool FL = (sizeof(EntT) == 8)>
 static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* gate) {
   if (a.num_tiles) {
-    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
+    hipLaunchKernelGGL((k_scatter<EntT, FL>), dim3(a.num_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
                        a.tile_filter, a.tile_start, 0u, a.fp_size, ent, part, a.cb_cursor, gate);
     CHECK_LAUNCH();
   }
-  if (a.num_old_tiles) {
-    hipLaunchKernelGGL((k_scatter<EntT>), dim3(a.num_old_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
+  if (a.num_old_tiles && !a.flag32) {  // 32-bit incremental builds read the old runs in K4
+    hipLaunchKernelGGL((k_scatter<EntT, FL>), dim3(a.num_old_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
                        a.old_tile_filter, a.old_tile_start, 1u, a.fp_size, ent, part, a.cb_cursor, gate);
     CHECK_LAUNCH();
   }
   return 0;
 }
 
-template <typename EntT>
+template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* spill) {
-  hipLaunchKernelGGL((k_cb_sort<EntT>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
-                     a.cb_count, a.cb_start, part, a.sorted32, a.idx_cnt, a.idx_start, a.outs, a.overflow,
+  hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
+                     a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start, a.outs, a.overflow,
                      a.lis, a.first_old, a.has_old, spill);
   CHECK_LAUNCH();
   REC(EV_B_SORT);
-  hipLaunchKernelGGL((k_cb_sort_big<EntT>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
-                     a.cb_count, a.cb_start, part, ent, a.sorted32, a.idx_cnt, a.idx_start, a.outs,
+  hipLaunchKernelGGL((k_cb_sort_big<EntT, FL, DUAL>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans,
+                     a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, ent, a.sorted32, a.idx_cnt, a.idx_start, a.outs,
                      a.overflow, a.lis, a.first_old, a.has_old);
   CHECK_LAUNCH();
   REC(EV_B_SORT_BIG);
@@ -2740,7 +2804,28 @@ extern "C" int rf_launch_plines(const LaunchArgs* pa);
 
 extern "C" int rf_launch_build(const LaunchArgs* pa) {
   const LaunchArgs& a = *pa;
-  if (a.wide) {
+  if (a.wide && a.flag32) {
+    // incremental add, 32-bit flagged entries (fp_size + value_size <= 31): the new entries
+    // are hashed, counted and scattered; each coarse bucket's run of the (sorted) old
+    // entries decoded by rf_launch_old_decode is located by k_old_cb_bounds and read by K4
+    // straight from old32 -- the old entries are neither counted nor scattered
+    uint32_t* ent = (uint32_t*)a.ent;
+    uint32_t* part = (uint32_t*)a.part;
+    if (a.num_tiles) { int rc = launch_hash_count_t<uint32_t, true>(a, ent, a.cb_count, nullptr); if (rc) return rc; }
+    if (a.num_cb) {
+      hipLaunchKernelGGL(k_old_cb_bounds, dim3((a.num_cb + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a.plans,
+                         a.cb_filter, a.num_cb, a.old32, a.old_tot, a.fp_size, a.ob_lo, a.ob_n, a.cb_count);
+      CHECK_LAUNCH();
+    }
+    REC(EV_B_HASH);
+    hipLaunchKernelGGL(k_cb_scan, dim3(a.num_filters), dim3(256), 0, (hipStream_t)a.stream, a.plans, a.cb_count,
+                       a.cb_count, a.cb_start, a.cb_cursor, nullptr);
+    CHECK_LAUNCH();
+    REC(EV_B_SCAN);
+    if (int rc = launch_scatter_t<uint32_t, true>(a, ent, part, nullptr)) return rc;
+    REC(EV_B_SCATTER);
+    if (int rc = launch_sort_t<uint32_t, true, true>(a, ent, part, nullptr)) return rc;
+  } else if (a.wide) {
     // incremental add: 64-bit entries; old entries first (decoded by rf_launch_old_decode)
     uint64_t* ent = (uint64_t*)a.ent;
     uint64_t* part = (uint64_t*)a.part;
@@ -2814,12 +2899,12 @@ extern "C" int rf_launch_old_decode(const LaunchArgs* pa) {
                      a.old_idx_filter, a.num_old_idx, a.old_cnt);
   CHECK_LAUNCH();
   hipLaunchKernelGGL(k_old_scan, dim3(a.num_filters), dim3(LAYOUT_NT), 0, (hipStream_t)a.stream, a.plans, a.old_cnt,
-                     a.old_pos, (uint64_t*)a.ent);
+                     a.old_pos, a.flag32 ? nullptr : (uint64_t*)a.ent, a.old_tot);
   CHECK_LAUNCH();
   const uint32_t waves_per_block = 256 / WAVE;
   hipLaunchKernelGGL(k_old_decode, dim3((a.num_old_idx + waves_per_block - 1) / waves_per_block), dim3(256), 0,
-                     (hipStream_t)a.stream, a.plans, a.old_idx_filter, a.num_old_idx, a.old_pos, (uint64_t*)a.ent,
-                     a.lis, a.fp_size);
+                     (hipStream_t)a.stream, a.plans, a.old_idx_filter, a.num_old_idx, a.old_pos,
+                     a.flag32 ? nullptr : (uint64_t*)a.ent, a.flag32 ? a.old32 : nullptr, a.lis, a.fp_size);
   CHECK_LAUNCH();
   return 0;
 }

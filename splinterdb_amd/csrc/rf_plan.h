@@ -35,6 +35,7 @@ constexpr uint32_t ERR_INDEX_OVERFLOW = 1u, ERR_BLOCK_TOO_BIG = 2u, ERR_PAGE_CAP
 struct FilterPlan {
   uint64_t e_first;    // first entry slot of this filter in the entry arrays
   uint64_t key_first;  // first input (key / hash) of this filter's new fingerprints
+  uint64_t old_first;  // 32-bit incremental builds: first of its decoded old entries in old32
   uint32_t num_new;    // new fingerprints
   uint32_t old_region; // entry slots reserved for decoded old entries (old num_fingerprints)
   uint32_t num_fp;     // routing_filter.num_fingerprints (new + old)
@@ -89,6 +90,11 @@ struct LaunchArgs {
   uint32_t num_old_idx;
   uint32_t* old_cnt;  // per old index: entries (num_remainders), then their start
   uint32_t* old_pos;
+  uint32_t flag32;     // incremental build with 32-bit flagged entries (fp_size + value_size <= 31)
+  uint32_t* old32;     // flag32: every filter's decoded old entries, in order (P.old_first ..)
+  uint32_t* old_tot;   // flag32: decoded old entries per filter
+  uint32_t* ob_lo;     // flag32: per coarse bucket, its run of old entries (start, length)
+  uint32_t* ob_n;
   const void* in0;
   const uint64_t* offs;
   uint32_t key_len, fp_size, seed, lis, page_size;

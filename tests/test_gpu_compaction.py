@@ -30,7 +30,12 @@ def chain_ids(g, v, n):
 
 
 @pytest.mark.skipif(not R.available(), reason="reference library not built")
-def test_chain_rounds_match_reference():
+@pytest.mark.parametrize("entries", ["flag32", "wide64"])
+def test_chain_rounds_match_reference(entries, monkeypatch):
+    """both incremental pipelines: 32-bit flagged entries with the old runs read in place
+    (fp_size + value_size <= 31, the default) and 64-bit entries (forced here)"""
+    if entries == "wide64":
+        monkeypatch.setenv("RF_AMD_WIDE64", "1")
     F, V, n = 3, 4, 20000
     cfg = E.routing_config_init(fingerprint_size=26, log_index_size=8, seed=42)
     eng = E.Engine(0)
