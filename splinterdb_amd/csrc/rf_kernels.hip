@@ -1757,60 +1757,80 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
                                                     uint32_t num_old_idx, const uint32_t* __restrict__ pos,
                                                     uint64_t* __restrict__ ent, uint32_t* __restrict__ old32,
                                                     uint32_t lis, uint32_t fp_size) {
+  // the index's block (header, encoding, remainders: at most one page) is first copied into
+  // a per-wave LDS slice with coalesced 16-byte loads; every bit read below is from LDS
+  constexpr uint32_t SLICE = MAX_PAGE + 64;
+  __shared__ __attribute__((aligned(16))) uint8_t s_blk[256 / WAVE][SLICE];
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   if (g >= num_old_idx) return;  // uniform per wave
   const FilterPlan& P = plans[old_idx_filter[g]];
   const uint32_t wid = g - P.old_idx_base;  // old index within its filter
   const uint32_t index_size = 1u << lis;
-  const uint64_t hdr = P.old_slots[wid];
-  const uint8_t* pg = P.old_pages;
-  const uint32_t c = (uint32_t)pg[hdr] | ((uint32_t)pg[hdr + 1] << 8);
+  const uint64_t hdr_g = P.old_slots[wid];
+  const uint8_t* gp = P.old_pages;
+  const uint32_t c = (uint32_t)gp[hdr_g] | ((uint32_t)gp[hdr_g + 1] << 8);
   const uint32_t enc = (c + index_size - 1) / 8 + 4;
+  const uint64_t a0 = hdr_g & ~15ull;
+  // bytes used: header + encoding + remainders, plus the 12 an unaligned 8-byte read may touch
+  const uint32_t used = (uint32_t)(hdr_g - a0) + 2 + enc + (uint32_t)(((uint64_t)c * P.old_rvs + 7) / 8) + 12;
+  const uint32_t nq = min((used + 15) / 16, SLICE / 16);
+  uint8_t* sb = s_blk[threadIdx.x / WAVE];
+  for (uint32_t q = lane; q < nq; q += WAVE)
+    reinterpret_cast<v4u*>(sb)[q] = *reinterpret_cast<const v4u*>(gp + a0 + 16ull * q);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint8_t* pg = sb;
+  const uint64_t hdr = hdr_g - a0;
   const uint64_t ebit = (hdr + 2) * 8;
   const uint64_t rbit = (hdr + 2 + enc) * 8;
   const uint32_t total_bits = c + index_size;
   uint64_t* out = old32 ? nullptr : ent + P.e_first + P.num_new + pos[g];
   uint32_t* out32 = old32 ? old32 + P.old_first + pos[g] : nullptr;
   const uint32_t old_vmask = (uint32_t)((1ull << P.old_vs) - 1);
-  // walk the encoding 64 bits per lane-step: each lane takes one 64-bit chunk per round
-  uint32_t zeros_before = 0, ones_before = 0;
-  for (uint32_t base = 0; base < total_bits; base += 64 * WAVE) {
-    const uint32_t bit0 = base + lane * 64;
-    uint64_t x = 0;
-    uint32_t nb = 0;
-    if (bit0 < total_bits) {
-      nb = min(64u, total_bits - bit0);
-      const uint64_t bp = ebit + bit0;
-      const uint32_t sh = (uint32_t)(bp & 7);
-      x = ld_u64_unaligned(pg, bp >> 3) >> sh;
-      if (sh) x |= (uint64_t)pg[(bp >> 3) + 8] << (64 - sh);  // the chunk's top bits
-      if (nb < 64) x &= (1ull << nb) - 1;
+  // zeros (entries) before each 64-bit word of the encoding -> LDS, then one lane per entry:
+  // entry k sits at the k-th zero bit; its bucket offset = 1-bits before it = position - k
+  // (routing_get_bucket_counts, :281-306)
+  __shared__ uint32_t s_zp[256 / WAVE][MAX_PAGE * 8 / 64 + 2];  // the encoding lies in one page
+  uint32_t* zp = s_zp[threadIdx.x / WAVE];
+  const uint32_t nw = (total_bits + 63) / 64;
+  auto word = [&](uint32_t w) -> uint64_t {  // encoding bits [64w, 64w + 64), zero padded
+    const uint64_t bp = ebit + 64ull * w;
+    const uint32_t sh = (uint32_t)(bp & 7);
+    uint64_t x = ld_u64_unaligned(pg, bp >> 3) >> sh;
+    if (sh) x |= (uint64_t)pg[(bp >> 3) + 8] << (64 - sh);
+    const uint32_t nb = min(64u, total_bits - 64 * w);
+    return nb < 64 ? x | ~((1ull << nb) - 1) : x;  // bits past the end read as ones
+  };
+  uint32_t zeros_before = 0;
+  for (uint32_t w0 = 0; w0 < nw; w0 += WAVE) {
+    const uint32_t w = w0 + lane;
+    const uint32_t z = w < nw ? 64u - __popcll(word(w)) : 0u;
+    const uint32_t inc = wave_incl_scan(z);
+    if (w < nw) zp[w] = zeros_before + inc - z;
+    zeros_before += __shfl(inc, WAVE - 1, WAVE);
+  }
+  if (lane == 0) zp[nw] = zeros_before;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (uint32_t k = lane; k < c; k += WAVE) {
+    uint32_t lo = 0, hi = nw;  // last word with zp[w] <= k
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (zp[mid] <= k) lo = mid; else hi = mid;
     }
-    const uint32_t ones = __popcll(x);
-    const uint32_t zer = nb - ones;
-    const uint32_t ones_ex = wave_incl_scan(ones) - ones + ones_before;
-    const uint32_t zer_ex = wave_incl_scan(zer) - zer + zeros_before;
-    // every zero bit of this chunk is an entry
-    uint64_t z = ~x & (nb == 64 ? ~0ull : ((1ull << nb) - 1));
-    uint32_t k = zer_ex;
-    while (z) {
-      const uint32_t b = __builtin_ctzll(z);
-      z &= z - 1;
-      // bucket offset = 1-bits before this 0-bit = chunk-prefix ones + (b - zeros before b in chunk)
-      const uint32_t bo = ones_ex + (b - (k - zer_ex));
-      const uint32_t rv = ld_bits(pg, rbit + (uint64_t)k * P.old_rvs, P.old_rvs);
-      const uint32_t bucket = wid * index_size + bo;
-      const uint32_t e_old = (P.old_rvs >= 32 ? 0u : (bucket << P.old_rvs)) | rv;
-      const uint32_t old_value = e_old & old_vmask;
-      const uint32_t fpv = e_old >> P.old_vs;
-      const uint32_t e = (fpv << P.vs) | old_value;
-      if (out32) out32[k] = e;
-      else out[k] = (uint64_t)e << 1;
-      k++;
-    }
-    ones_before = __shfl(ones_ex + ones, WAVE - 1, WAVE);
-    zeros_before = __shfl(zer_ex + zer, WAVE - 1, WAVE);
+    const uint32_t b = 64 * lo + select64_fast(~word(lo), k - zp[lo]);
+    const uint32_t bo = b - k;
+    const uint32_t rv = ld_bits(pg, rbit + (uint64_t)k * P.old_rvs, P.old_rvs);
+    const uint32_t bucket = wid * index_size + bo;
+    const uint32_t e_old = (P.old_rvs >= 32 ? 0u : (bucket << P.old_rvs)) | rv;
+    const uint32_t old_value = e_old & old_vmask;
+    const uint32_t fpv = e_old >> P.old_vs;
+    const uint32_t e = (fpv << P.vs) | old_value;
+    if (out32) out32[k] = e;
+    else out[k] = (uint64_t)e << 1;
   }
 }
 
