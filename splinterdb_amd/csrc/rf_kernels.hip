@@ -608,12 +608,16 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   __shared__ EntT s_b[SORT_CAP];
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[MAX_BINS + 1];
   __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
-  __shared__ uint32_t s_fo[FL ? MAX_IPC : 1];
-  __shared__ uint32_t s_ho[FL ? MAX_IPC : 1];
+  // incremental builds: per index, its smallest old entry and whether it has one; they live
+  // in s_bin past s_first's ipc + 1 words, initialised once the bins are no longer read (no
+  // LDS beyond the fresh build's, so the same 3 workgroups per CU)
+  static_assert(MAX_BINS + 1 >= 2048 + 2 * MAX_IPC && MAX_IPC + 1 <= 2048, "s_fo / s_ho inside s_bin");
   constexpr uint32_t BIG_LIST = 64;
   __shared__ uint32_t s_big[BIG_LIST];  // bins over 8 entries (s_nbig may exceed the list)
   __shared__ uint32_t s_nbig;
   uint32_t* s_first = s_bin;  // compacted start of each index: reuses s_bin once bins are sorted
+  uint32_t* s_fo = s_bin + 2048;
+  uint32_t* s_ho = s_bin + 2048 + MAX_IPC;
   const uint32_t cb = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's buckets share an XCD (its partition's L2)
   const uint32_t f = cb_filter[cb];
   const FilterPlan& P = plans[f];
@@ -649,9 +653,6 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     for (int k = 0; k < PER; k++) v[k] = src[min(threadIdx.x + k * SORT_NT, nm1)];
   }
   for (uint32_t i = threadIdx.x; i <= nbins; i += SORT_NT) s_bin[i] = 0;
-  if constexpr (FL) {
-    for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
-  }
   if (threadIdx.x == 0) s_nbig = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
@@ -803,6 +804,9 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     }
     __syncthreads();
   }
+  if constexpr (FL) {  // s_bin is no longer read; the scan below orders these before use
+    for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
+  }
   DBG_PHASE(4);
   // dedupe + compaction: thread t owns the contiguous run [t*drun, t*drun + drun), drun =
   // ceil(n / SORT_NT) made odd (lanes drun words apart fall on distinct LDS banks) and
@@ -838,6 +842,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   uint32_t lprev = (i0 > 0 && i0 <= n) ? index_of(ent_e<EntT, FL>(prev0)) : NONE;
   uint32_t fprev = (i0 > 0 && i0 <= n) ? (ent_e<EntT, FL>(prev0) >> P.vs) : 0u;
   uint32_t uniq = 0;
+  uint32_t fo_li = NONE;  // index of this run's last recorded old entry
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t i = i0 + k;
@@ -850,9 +855,14 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
         uniq += (fp != (li != lprev ? (0xffffffffu >> P.vs) : fprev)) ? 1u : 0u;
         pos++;
         if constexpr (FL) {
-          if (!(w[k] & EntT(1))) {  // old entry: remember each index's smallest (num_unique quirk)
+          // old entry: remember each index's smallest (num_unique quirk). The run is in
+          // order, so its first old entry of an index is its smallest there: one LDS atomic
+          // per (run, index) instead of one per old entry (all of an index's entries would
+          // otherwise contend for one address)
+          if (!(w[k] & EntT(1)) && li != fo_li) {
             atomicMin(&s_fo[li], e);
             s_ho[li] = 1;
+            fo_li = li;
           }
         }
       }
@@ -2286,6 +2296,10 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
                                                 uint4* __restrict__ lines, uint32_t num_idx,
                                                 uint32_t lmax, uint32_t lis, uint32_t page_size,
                                                 uint32_t force) {
+  // the index's block (at most one page) is first copied into a per-wave LDS slice with
+  // coalesced 16-byte loads; both phases then read their bits from LDS
+  constexpr uint32_t SLICE = MAX_PAGE + 64;
+  __shared__ __attribute__((aligned(16))) uint8_t s_blk[256 / WAVE][SLICE];
   extern __shared__ uint32_t s_dyn[];
   const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
   const uint32_t g = blockIdx.x * (blockDim.x / WAVE) + wv;
@@ -2296,12 +2310,23 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
                       g - P.idx_base < P.num_indices;
   const uint32_t IS = 1u << lis;
   const uint32_t lgG = active ? P.lg_line - 1 : 0u, G = 1u << lgG, L = IS >> lgG;
-  const uint8_t* pg = pages + (uint64_t)P.page_base * page_size;
+  const uint8_t* pg = s_blk[wv];
   uint64_t rel = 0;
   uint32_t c = 0;
   if (active) {
-    rel = slots[g];
-    c = (uint32_t)pg[rel] | ((uint32_t)pg[rel + 1] << 8);
+    const uint8_t* gp = pages + (uint64_t)P.page_base * page_size;
+    const uint64_t rel_g = slots[g];
+    c = (uint32_t)gp[rel_g] | ((uint32_t)gp[rel_g + 1] << 8);
+    const uint64_t a0 = rel_g & ~15ull;
+    const uint32_t used = (uint32_t)(rel_g - a0) + 2 + (c + IS - 1) / 8 + 4 +
+                          (uint32_t)(((uint64_t)c * P.rvs + 7) / 8) + 12;
+    const uint32_t nq = min((used + 15) / 16, SLICE / 16);
+    for (uint32_t q = lane; q < nq; q += WAVE)
+      reinterpret_cast<v4u*>(s_blk[wv])[q] = *reinterpret_cast<const v4u*>(gp + a0 + 16ull * q);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    rel = rel_g - a0;
     const uint64_t ebit = (rel + 2) * 8;
     const uint32_t nbits = c + IS;
     if (lane == 0) { s_a[0] = 0; s_a[L] = nbits; }

@@ -6,7 +6,7 @@
 #   3. the bench lines (c2 with the CPU baseline, c3, c4) with roofline traffic from (1).
 # usage: bash tools/profile_round.sh <tag>      (outputs under gpurun_out/prof_<tag>/)
 set -o pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/prof_$TAG
@@ -24,8 +24,10 @@ timeout -k 10 300 python3 bench.py --workload c3 --no-cpu-baseline --pmc none > 
 timeout -k 10 300 python3 bench.py --workload c4 --no-cpu-baseline --pmc none > $O/bench_c4.json 2> $O/bench_c4.err || { echo "bench c4 failed"; exit 1; }
 timeout -k 10 300 python3 bench.py --workload c5 --pmc none > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 failed"; exit 1; }
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-e2e --routed-probe --pmc none > $O/bench_c2_routed.json 2> $O/bench_c2_routed.err || { echo "bench routed failed"; exit 1; }
-for k in 1 2 3 4; do
-  timeout -k 10 100 python3 tools/phase_times.py $k > $O/phases_k$k.txt 2>&1 || { echo "phase times $k failed"; exit 1; }
-done
-timeout -k 10 100 ./tools/gather_bench > $O/gather_$TAG.txt 2>&1 || { echo "gather bench failed"; exit 1; }
+# L2 behaviour of the probe (and every kernel) at C2 and C3: hits, misses, HBM read requests
+TCC="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"
+timeout -s KILL 120 rocprofv3 --pmc $TCC --output-format csv -d $O/tcc2 -o c2 -- python3 $BENCH > $O/tcc2.log 2>&1 || { echo "pmc tcc c2 failed"; exit 1; }
+timeout -s KILL 180 rocprofv3 --pmc $TCC --output-format csv -d $O/tcc3 -o c3 -- python3 $BENCH --workload c3 > $O/tcc3.log 2>&1 || { echo "pmc tcc c3 failed"; exit 1; }
+python3 tools/tcc_summary.py $O/tcc2/c2_counter_collection.csv $O/tcc3/c3_counter_collection.csv > $O/tcc_$TAG.txt || exit 1
+timeout -k 10 300 python3 bench.py --workload compaction --steps 5 --warmup 1 > $O/bench_compaction.json 2> $O/bench_compaction.err || { echo "bench compaction failed"; exit 1; }
 cat $O/bench_c2.json
