@@ -194,7 +194,7 @@ struct rf_amd_batch {
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
       d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill,
-      d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n;
+      d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n, d_pg_noline;
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
@@ -206,7 +206,7 @@ struct rf_amd_batch {
             &d_cb_filter, &d_overflow, &d_idx_cnt, &d_idx_start, &d_slots, &d_page_first, &d_pg_filter,
             &d_pages, &d_tile_filter, &d_tile_start, &d_old_tile_filter, &d_old_tile_start, &d_old_cnt,
             &d_old_pos, &d_first_old, &d_has_old, &d_pplans, &d_lines, &d_idx_filter, &d_spill,
-            &d_old_idx_filter, &d_old32, &d_old_tot, &d_ob_lo, &d_ob_n};
+            &d_old_idx_filter, &d_old32, &d_old_tot, &d_ob_lo, &d_ob_n, &d_pg_noline};
   }
 };
 
@@ -264,12 +264,15 @@ static uint32_t vsize_of(uint32_t value) { return value == 0 ? 0 : 32 - __builti
 // bound; table size measured not to matter for the probe, overflow rate does).
 // Returns g + 1, or 0 = no lines (rvs > 32: probes walk the image).
 // K6 cuts a filter's probe lines from its LDS page images when the per-page group table
-// fits (blocks per page <= page_size / smallest block, each with IS/G + 1 entries).
-static bool lines_in_assembly(uint32_t lis, uint32_t lg_line, uint32_t page_size) {
+// fits: each block needs IS/G + 1 entries. Returns 0: never (k_plines cuts every line),
+// 1: always (even a page of the smallest blocks fits), 2: page by page -- K6 flags a page
+// whose blocks do not fit and k_plines cuts those pages' lines.
+static int lines_in_assembly(uint32_t lis, uint32_t lg_line, uint32_t page_size) {
   const uint32_t IS = 1u << lis, L = IS >> (lg_line - 1);
   const uint32_t min_block = 2 + (IS - 1) / 8 + 4 + 3;
   const uint32_t maxb = page_size / min_block + 1;
-  return maxb <= ASM_MAXB_HOST && (uint64_t)maxb * (L + 1) <= ASM_GT_HOST;
+  if (maxb > ASM_MAXB_HOST || L + 1 > ASM_GT_HOST) return 0;
+  return (uint64_t)maxb * (L + 1) <= ASM_GT_HOST ? 1 : 2;
 }
 
 static double line_sigma() {
@@ -364,8 +367,10 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     p.pf_base = pf_base;
     p.lg_line = line_log_group(lis, p.rvs, (double)nfp / (double)(1ull << lnb));
     p.line_base = (uint32_t)line_base;
-    p.lines_asm = p.lg_line && lines_in_assembly(lis, p.lg_line, P);
-    if (p.lg_line && !p.lines_asm) b->plines_needed = true;
+    const int la = p.lg_line ? lines_in_assembly(lis, p.lg_line, P) : 0;
+    p.lines_asm = la != 0;
+    p.lines_flag = la == 2;
+    if (p.lg_line && la != 1) b->plines_needed = true;
     if (p.lg_line) {
       line_base += (uint64_t)p.num_indices << (lis - (p.lg_line - 1));
       b->line_lmax = std::max(b->line_lmax, IS >> (p.lg_line - 1));
@@ -447,6 +452,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   rc |= b->d_idx_filter.alloc(4ull * b->I, pool);
   rc |= b->d_page_first.alloc(4 * b->PF, pool);
   rc |= b->d_pg_filter.alloc(4 * b->PS, pool);
+  rc |= b->d_pg_noline.alloc(4 * b->PS + 4, pool);
   rc |= b->d_pages.alloc((size_t)b->PS * P + 256, pool);
   rc |= b->d_tile_filter.alloc(4 * b->tile_filter.size(), pool);
   rc |= b->d_tile_start.alloc(4 * b->tile_start.size(), pool);
@@ -598,6 +604,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.lines = b->d_lines.as<uint4>();
   a.line_lmax = b->line_lmax;
   a.plines_needed = b->plines_needed ? 1u : 0u;
+  a.pg_noline = b->d_pg_noline.as<uint32_t>();
   a.idx_filter = b->d_idx_filter.as<uint32_t>();
   a.num_idx = b->I;
   a.page_first = b->d_page_first.as<uint32_t>();

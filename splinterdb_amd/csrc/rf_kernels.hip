@@ -1372,6 +1372,7 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                      const uint32_t* __restrict__ page_first,
                                                      const FilterOut* __restrict__ outs,
                                                      uint8_t* __restrict__ pages, uint4* __restrict__ lines,
+                                                     uint32_t* __restrict__ pg_noline,
                                                      uint32_t lis, uint32_t page_size) {
   __shared__ __attribute__((aligned(16))) uint32_t s_pg[MAX_PAGE / 4 + 4];
   __shared__ uint32_t s_wpre[ASM_MAXB];
@@ -1602,6 +1603,11 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   // (E) probe lines of the page's blocks, cut from the LDS image (format: "probe lines").
   // E1: popcount scan over the blocks' encoding words -> group boundaries in s_gs.
   const uint32_t lgG = P.lg_line - 1, G = 1u << lgG, L = IS >> lgG;
+  if (P.lines_flag) {  // this page's group table may not fit s_gs: then k_plines cuts its lines
+    const bool over = nb * (L + 1) > ASM_GT;
+    if (threadIdx.x == 0) pg_noline[slot] = over ? 1u : 0u;
+    if (over) return;
+  }
   uint32_t wc[2], wsum = 0;  // encoding words per block (2 blocks per thread)
 #pragma unroll
   for (int q = 0; q < 2; q++) {
@@ -1767,80 +1773,69 @@ __global__ __launch_bounds__(256) void k_old_decode(const FilterPlan* __restrict
                                                     uint32_t num_old_idx, const uint32_t* __restrict__ pos,
                                                     uint64_t* __restrict__ ent, uint32_t* __restrict__ old32,
                                                     uint32_t lis, uint32_t fp_size) {
-  // the index's block (header, encoding, remainders: at most one page) is first copied into
-  // a per-wave LDS slice with coalesced 16-byte loads; every bit read below is from LDS
-  constexpr uint32_t SLICE = MAX_PAGE + 64;
-  __shared__ __attribute__((aligned(16))) uint8_t s_blk[256 / WAVE][SLICE];
+  // Entry k sits at the k-th zero bit of the encoding; its bucket offset = 1-bits before it
+  // = position - k (routing_get_bucket_counts, :281-306). One lane per encoding byte lists
+  // its zero positions (at most 8) at the byte's zero prefix in a small LDS list, then one
+  // lane per entry reads its position and its remainder. Consecutive lanes read consecutive
+  // bytes and bit ranges (coalesced), and no lane walks a chain of entries. An index with
+  // more entries than the list holds is decoded in CAP-entry chunks.
+  constexpr uint32_t CAP = 1024;
+  __shared__ uint16_t s_pos[256 / WAVE][CAP];
   const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   if (g >= num_old_idx) return;  // uniform per wave
   const FilterPlan& P = plans[old_idx_filter[g]];
   const uint32_t wid = g - P.old_idx_base;  // old index within its filter
   const uint32_t index_size = 1u << lis;
-  const uint64_t hdr_g = P.old_slots[wid];
-  const uint8_t* gp = P.old_pages;
-  const uint32_t c = (uint32_t)gp[hdr_g] | ((uint32_t)gp[hdr_g + 1] << 8);
+  const uint64_t hdr = P.old_slots[wid];
+  const uint8_t* pg = P.old_pages;
+  const uint32_t c = (uint32_t)pg[hdr] | ((uint32_t)pg[hdr + 1] << 8);
   const uint32_t enc = (c + index_size - 1) / 8 + 4;
-  const uint64_t a0 = hdr_g & ~15ull;
-  // bytes used: header + encoding + remainders, plus the 12 an unaligned 8-byte read may touch
-  const uint32_t used = (uint32_t)(hdr_g - a0) + 2 + enc + (uint32_t)(((uint64_t)c * P.old_rvs + 7) / 8) + 12;
-  const uint32_t nq = min((used + 15) / 16, SLICE / 16);
-  uint8_t* sb = s_blk[threadIdx.x / WAVE];
-  for (uint32_t q = lane; q < nq; q += WAVE)
-    reinterpret_cast<v4u*>(sb)[q] = *reinterpret_cast<const v4u*>(gp + a0 + 16ull * q);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint8_t* pg = sb;
-  const uint64_t hdr = hdr_g - a0;
-  const uint64_t ebit = (hdr + 2) * 8;
   const uint64_t rbit = (hdr + 2 + enc) * 8;
   const uint32_t total_bits = c + index_size;
   uint64_t* out = old32 ? nullptr : ent + P.e_first + P.num_new + pos[g];
   uint32_t* out32 = old32 ? old32 + P.old_first + pos[g] : nullptr;
   const uint32_t old_vmask = (uint32_t)((1ull << P.old_vs) - 1);
-  // zeros (entries) before each 64-bit word of the encoding -> LDS, then one lane per entry:
-  // entry k sits at the k-th zero bit; its bucket offset = 1-bits before it = position - k
-  // (routing_get_bucket_counts, :281-306)
-  __shared__ uint32_t s_zp[256 / WAVE][MAX_PAGE * 8 / 64 + 2];  // the encoding lies in one page
-  uint32_t* zp = s_zp[threadIdx.x / WAVE];
-  const uint32_t nw = (total_bits + 63) / 64;
-  auto word = [&](uint32_t w) -> uint64_t {  // encoding bits [64w, 64w + 64), zero padded
-    const uint64_t bp = ebit + 64ull * w;
-    const uint32_t sh = (uint32_t)(bp & 7);
-    uint64_t x = ld_u64_unaligned(pg, bp >> 3) >> sh;
-    if (sh) x |= (uint64_t)pg[(bp >> 3) + 8] << (64 - sh);
-    const uint32_t nb = min(64u, total_bits - 64 * w);
-    return nb < 64 ? x | ~((1ull << nb) - 1) : x;  // bits past the end read as ones
-  };
-  uint32_t zeros_before = 0;
-  for (uint32_t w0 = 0; w0 < nw; w0 += WAVE) {
-    const uint32_t w = w0 + lane;
-    const uint32_t z = w < nw ? 64u - __popcll(word(w)) : 0u;
-    const uint32_t inc = wave_incl_scan(z);
-    if (w < nw) zp[w] = zeros_before + inc - z;
-    zeros_before += __shfl(inc, WAVE - 1, WAVE);
-  }
-  if (lane == 0) zp[nw] = zeros_before;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (uint32_t k = lane; k < c; k += WAVE) {
-    uint32_t lo = 0, hi = nw;  // last word with zp[w] <= k
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (zp[mid] <= k) lo = mid; else hi = mid;
+  uint16_t* zpos = s_pos[threadIdx.x / WAVE];
+  const uint32_t nbytes = (total_bits + 7) / 8;
+  const uint8_t* encb = pg + hdr + 2;  // the encoding is byte aligned
+  for (uint32_t k0 = 0; k0 < c; k0 += CAP) {
+    uint32_t zeros_before = 0;
+    for (uint32_t b0 = 0; b0 < nbytes && zeros_before < k0 + CAP; b0 += WAVE) {
+      const uint32_t bb = b0 + lane;
+      uint32_t z = 0;
+      if (bb < nbytes) {
+        const uint32_t nb = min(8u, total_bits - 8 * bb);
+        z = ~(uint32_t)encb[bb] & ((1u << nb) - 1);  // bits past the end are not entries
+      }
+      const uint32_t cnt = __popc(z);
+      const uint32_t inc = wave_incl_scan(cnt);
+      uint32_t at = zeros_before + inc - cnt;
+      while (z) {
+        if (at >= k0 && at < k0 + CAP) zpos[at - k0] = (uint16_t)(8 * bb + __builtin_ctz(z));
+        at++;
+        z &= z - 1;
+      }
+      zeros_before += __shfl(inc, WAVE - 1, WAVE);
     }
-    const uint32_t b = 64 * lo + select64_fast(~word(lo), k - zp[lo]);
-    const uint32_t bo = b - k;
-    const uint32_t rv = ld_bits(pg, rbit + (uint64_t)k * P.old_rvs, P.old_rvs);
-    const uint32_t bucket = wid * index_size + bo;
-    const uint32_t e_old = (P.old_rvs >= 32 ? 0u : (bucket << P.old_rvs)) | rv;
-    const uint32_t old_value = e_old & old_vmask;
-    const uint32_t fpv = e_old >> P.old_vs;
-    const uint32_t e = (fpv << P.vs) | old_value;
-    if (out32) out32[k] = e;
-    else out[k] = (uint64_t)e << 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t k1 = min(c, k0 + CAP);
+    for (uint32_t k = k0 + lane; k < k1; k += WAVE) {
+      const uint32_t bo = (uint32_t)zpos[k - k0] - k;
+      const uint32_t rv = ld_bits(pg, rbit + (uint64_t)k * P.old_rvs, P.old_rvs);
+      const uint32_t bucket = wid * index_size + bo;
+      const uint32_t e_old = (P.old_rvs >= 32 ? 0u : (bucket << P.old_rvs)) | rv;
+      const uint32_t old_value = e_old & old_vmask;
+      const uint32_t fpv = e_old >> P.old_vs;
+      const uint32_t e = (fpv << P.vs) | old_value;
+      if (out32) out32[k] = e;
+      else out[k] = (uint64_t)e << 1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is rewritten next chunk
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -2293,6 +2288,7 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
                                                 const uint64_t* __restrict__ slots,
                                                 const uint8_t* __restrict__ pages,
                                                 const FilterOut* __restrict__ outs,
+                                                const uint32_t* __restrict__ pg_noline,
                                                 uint4* __restrict__ lines, uint32_t num_idx,
                                                 uint32_t lmax, uint32_t lis, uint32_t page_size,
                                                 uint32_t force) {
@@ -2306,8 +2302,10 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
   uint32_t* s_a = s_dyn + wv * (lmax + 1);
   const uint32_t f = g < num_idx ? idx_filter[g] : 0u;
   const FilterPlan& P = plans[f];
-  const bool active = g < num_idx && P.lg_line != 0 && (force || !P.lines_asm) && !(outs && outs[f].error) &&
-                      g - P.idx_base < P.num_indices;
+  bool active = g < num_idx && P.lg_line != 0 && !(outs && outs[f].error) && g - P.idx_base < P.num_indices;
+  // lines K6 did not cut: filters it never cuts, and the pages it flagged (lines_flag)
+  if (active && !force && P.lines_asm)
+    active = P.lines_flag && pg_noline && pg_noline[P.page_base + (uint32_t)(slots[g] / page_size)] != 0;
   const uint32_t IS = 1u << lis;
   const uint32_t lgG = active ? P.lg_line - 1 : 0u, G = 1u << lgG, L = IS >> lgG;
   const uint8_t* pg = s_blk[wv];
@@ -2918,7 +2916,7 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
   REC(EV_B_LAYOUT);
   hipLaunchKernelGGL(k_assemble, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans, a.pg_filter,
                      a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages, a.lines,
-                     a.lis, a.page_size);
+                     a.pg_noline, a.lis, a.page_size);
   CHECK_LAUNCH();
   if (a.plines_needed)
     if (int rc = rf_launch_plines(&a)) return rc;
@@ -2931,7 +2929,7 @@ extern "C" int rf_launch_plines(const LaunchArgs* pa) {
   if (!a.line_lmax) return 0;  // no filter of the batch has lines
   const size_t lds = 4ull * (256 / WAVE) * (a.line_lmax + 1);
   hipLaunchKernelGGL(k_plines, dim3((a.num_idx + 3) / 4), dim3(256), lds, (hipStream_t)a.stream, a.plans,
-                     a.idx_filter, a.slots, a.pages, a.outs, a.lines, a.num_idx, a.line_lmax, a.lis,
+                     a.idx_filter, a.slots, a.pages, a.outs, a.pg_noline, a.lines, a.num_idx, a.line_lmax, a.lis,
                      a.page_size, a.plines_force);
   CHECK_LAUNCH();
   return 0;

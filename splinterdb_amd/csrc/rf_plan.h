@@ -50,7 +50,8 @@ struct FilterPlan {
   // old filter (incremental add)
   uint32_t old_num_indices, old_vs, old_rvs, npo;  // npo = new indices per old index
   uint32_t old_idx_base;  // first of this filter's old indices in the batch's old-index list
-  uint32_t pad0;
+  uint32_t lines_flag;    // lines_asm, but a page's group table may not fit K6's LDS: such pages
+                          // are flagged in pg_noline and k_plines cuts their indices' lines
   const uint8_t* old_pages;
   const uint64_t* old_slots;
 };
@@ -120,6 +121,7 @@ struct LaunchArgs {
   const uint32_t* idx_filter;
   uint32_t num_idx;
   uint32_t* page_first;
+  uint32_t* pg_noline;      // per page slot: K6 left this page's probe lines to k_plines
   const uint32_t* pg_filter;
   uint32_t num_page_slots;
   uint8_t* pages;
