@@ -556,6 +556,32 @@ def run_compaction(args, rank, world, dist, dev, coll_dev, backend):
     tr = S.max_over_ranks((time.perf_counter() - tr) / rb_reps, dist, coll_dev)
     rb_walls /= rb_reps
 
+    # drop-in latency (beside value): one routing_filter_add of 2^20-1 host hashes through
+    # rf_amd_filter_add -- what the shim pays per call -- fresh, then onto that filter
+    dropin = None
+    if rank == 0:
+        hh = torch.empty(n, dtype=torch.int32, device=dev)
+        E.hash_keys(cfg, keys[0][:n], 24, n, hh, engine=eng)
+        h0 = hh.cpu().numpy().view(np.uint32).copy()
+        E.hash_keys(cfg, keys[1][:n], 24, n, hh, engine=eng)
+        h1 = hh.cpu().numpy().view(np.uint32).copy()
+        E.routing_filter_add(cfg, None, h0, 0, engine=eng)  # warm
+        t_f, t_i = [], []
+        for _ in range(5):
+            ta = time.perf_counter()
+            f0 = E.routing_filter_add(cfg, None, h0, 0, engine=eng)
+            tb = time.perf_counter()
+            E.routing_filter_add(cfg, f0, h1, 1, engine=eng)
+            tc = time.perf_counter()
+            t_f.append(tb - ta)
+            t_i.append(tc - tb)
+        dropin = {"fresh_add_ms": round(float(np.median(t_f)) * 1e3, 3),
+                  "incremental_add_ms": round(float(np.median(t_i)) * 1e3, 3),
+                  "keys": n,
+                  "note": "rf_amd_filter_add (host hashes in, host image out, old image uploaded), "
+                          "median of 5"}
+        del hh
+
     # ---- verification (outside the timed region) -------------------------------------
     # every round's keys find their value in the final filters (filter_test.c:100-116)
     ok = True
@@ -619,6 +645,7 @@ def run_compaction(args, rank, world, dist, dev, coll_dev, backend):
                      "traffic": None, "alg_bytes": int(alg)},
         "verified": verified, "sha_checked_filters": sha_checked,
         "num_unique_filter0": int(final[0].num_unique),
+        "dropin_latency": dropin,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_baseline as CB
