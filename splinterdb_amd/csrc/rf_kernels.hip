@@ -336,7 +336,10 @@ extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid) {
 // -> scatter pipeline (K1, K2, K3 gated on *spill) then rebuilds the partition.
 // ======================================================================================
 template <int KIND>
-__global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_hash_scatter(const FilterPlan* __restrict__ plans,
+#ifndef RF_SCAT_WPE
+#define RF_SCAT_WPE 4
+#endif
+__global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(RF_SCAT_WPE))) void k_hash_scatter(const FilterPlan* __restrict__ plans,
                                                           const uint32_t* __restrict__ tile_filter,
                                                           const uint32_t* __restrict__ tile_start,
                                                           const void* __restrict__ in0,
@@ -1695,28 +1698,6 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
 // ======================================================================================
 // K0: incremental add -- decode an old filter into entries (src/routing_filter.c:496-544)
 // ======================================================================================
-// exclusive scan of n <= MAX_INDICES counts in one workgroup
-__global__ __launch_bounds__(LAYOUT_NT) void k_scan_small(const uint32_t* __restrict__ in,
-                                                          uint32_t* __restrict__ out, uint32_t n) {
-  __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
-  constexpr int PER = MAX_INDICES / LAYOUT_NT;
-  uint32_t v[PER], sum = 0;
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const uint32_t i = threadIdx.x * PER + k;
-    v[k] = i < n ? in[i] : 0u;
-    sum += v[k];
-  }
-  uint32_t total;
-  uint32_t run = block_excl_scan<LAYOUT_NT>(sum, s_tmp, &total);
-#pragma unroll
-  for (int k = 0; k < PER; k++) {
-    const uint32_t i = threadIdx.x * PER + k;
-    if (i < n) out[i] = run;
-    run += v[k];
-  }
-}
-
 // Every old index of the batch in one list (filter f's at P.old_idx_base ..): the decode of
 // all old filters is three launches, whatever the number of filters.
 // k_old_counts: per old index, num_remainders from its header -> cnt

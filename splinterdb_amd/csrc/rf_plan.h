@@ -16,7 +16,10 @@ constexpr uint32_t MAX_IPC = 512;     // indices per coarse bucket (2^(12-3))
 
 // kernel shapes
 constexpr int TILE_NT = 256;
-constexpr int TILE_KEYS = 16384;  // keys per K1/K3 tile
+#ifndef RF_TILE_KEYS
+#define RF_TILE_KEYS 16384
+#endif
+constexpr int TILE_KEYS = RF_TILE_KEYS;  // keys per K1/K3 tile
 constexpr int SCAT_NT = 512;
 constexpr int SORT_NT = 512;
 constexpr int SORT_CAP = 9216;   // entries per coarse bucket held in LDS (means 4096..8192, sd < 91)

@@ -72,6 +72,15 @@ def test_chain_rounds_match_reference(entries, monkeypatch):
                 assert got.size == want.pages.size and (got == want.pages).all(), (v, f)
                 assert (hs[f][: inf[f].num_indices].numpy().view(np.uint64) == want.slots).all(), (v, f)
             prev = b
+        # lookups of every round's keys in the final filters (probe lines cut page by page
+        # by K6 or by k_plines for the pages it flags) == the reference's routing_filter_lookup
+        found = torch.empty(F * n, dtype=torch.int64, device="cuda:0")
+        for v in range(V):
+            prev.probe_keys_runs(dkeys[v], 24, [n] * F, found)
+            got = found.cpu().numpy().view(np.uint64)
+            for f in range(F):
+                want = ref.lookup_keys(rprev[f], keys[v][f * n:(f + 1) * n])
+                assert (got[f * n:(f + 1) * n] == want).all(), (v, f)
         prev.close()
         # the pool got the parked blocks back: a new batch of the same shape reuses them
         h0 = eng.pool_stats()["hits"]
