@@ -115,6 +115,14 @@ int rf_amd_batch_probe_hashes_runs(rf_amd_batch *b, const uint32_t *d_hashes, co
 int rf_amd_batch_build_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes);
 int rf_amd_batch_probe_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes, const uint32_t *h_filter_id,
                                    uint64_t n, uint64_t *h_found);
+/* lookups against many resident filters in ONE round trip (one H2D, a probe per group, one
+ * D2H, one synchronisation): group g probes counts[g] consecutive hashes of h_hashes against
+ * filter filter_index[g] (NULL: 0) of batches[g]. The batch form of trunk_merge_lookup's
+ * per-bundle routing_filter_lookup calls (src/trunk.c:6008-6075; routing_filter.h:87-92) and
+ * of routing_filter_lookup_async states (:130-155) flushed together. */
+int rf_amd_probe_many_hashes_host(rf_amd_engine *e, rf_amd_batch *const *batches,
+                                  const uint32_t *filter_index, const uint64_t *counts,
+                                  uint32_t num_groups, const uint32_t *h_hashes, uint64_t *h_found);
 /* device-allocation pool of the engine (batch work buffers are recycled across batches) */
 int rf_amd_engine_pool_stats(rf_amd_engine *e, uint64_t *pooled_bytes, uint64_t *hits, uint64_t *misses);
 

@@ -551,6 +551,46 @@ rfr_async_stats(uint64 *batches, uint64 *probes)
    return 1;
 }
 
+/* the shim's batched lookups (weak: absent from the reference's own library) */
+__attribute__((weak)) platform_status
+routing_filter_amd_lookup_batch(cache                *cc,
+                                const routing_config *cfg,
+                                routing_filter       *filters,
+                                const key            *keys,
+                                uint64                n,
+                                uint64               *found);
+
+/* n lookups (descs[filter_id[i]], key i): through routing_filter_amd_lookup_batch when the
+ * linked implementation has it (returns 1), else one routing_filter_lookup per key (0) */
+int
+rfr_lookup_batch(rfr_stack      *s,
+                 routing_filter *descs,
+                 const uint32   *filter_id,
+                 const uint8    *keys,
+                 uint32          key_len,
+                 uint64          n,
+                 uint64         *found)
+{
+   if (!routing_filter_amd_lookup_batch) {
+      for (uint64 i = 0; i < n; i++) {
+         key k = key_create(FALSE, key_len, keys + i * key_len);
+         routing_filter_lookup((cache *)&s->cc, &s->rcfg, &descs[filter_id[i]], k, &found[i]);
+      }
+      return 0;
+   }
+   routing_filter *fl = malloc(sizeof(*fl) * (n ? n : 1));
+   key            *kl = malloc(sizeof(*kl) * (n ? n : 1));
+   for (uint64 i = 0; i < n; i++) {
+      fl[i] = descs[filter_id[i]];
+      kl[i] = key_create(FALSE, key_len, keys + i * key_len);
+   }
+   platform_status rc =
+      routing_filter_amd_lookup_batch((cache *)&s->cc, &s->rcfg, fl, kl, n, found);
+   free(fl);
+   free(kl);
+   return SUCCESS(rc) ? 1 : -1;
+}
+
 /* routing_filter_print of the linked implementation, with platform_default_log pointed at
  * stdout for the call (the library's default is /dev/null, platform_log.c:15-24) */
 void

@@ -87,6 +87,8 @@ def lib(path=LIB_PATH):
         L.rfr_lookup_keys_async_many.restype = u64
         L.rfr_lookup_keys_async_many.argtypes = [vp, vp, vp, vp, u32, u64, vp, ctypes.POINTER(u64)]
         L.rfr_async_stats.restype = i32
+        L.rfr_lookup_batch.restype = i32
+        L.rfr_lookup_batch.argtypes = [vp, vp, vp, vp, u32, u64, vp]
         L.rfr_async_stats.argtypes = [ctypes.POINTER(u64), ctypes.POINTER(u64)]
         L.rfr_print.argtypes = [vp, RF]
         L.rfr_print.restype = None
@@ -232,6 +234,20 @@ class Stack:
         cb = self.L.rfr_lookup_keys_async_many(self.h, ctypes.addressof(arr), None if fid is None else _p(fid),
                                                _p(k), key_len, n, _p(out), ctypes.byref(running))
         return out, int(cb), int(running.value)
+
+    def lookup_batch(self, descs, keys, filter_id, key_len=24):
+        """len(keys) lookups (descs[filter_id[i]], key i): one routing_filter_amd_lookup_batch
+        call in the shim's stack, one routing_filter_lookup per key in the reference's.
+        Returns (found, batched)."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = k.size // key_len
+        arr = (RoutingFilter * max(1, len(descs)))(*descs)
+        fid = np.ascontiguousarray(filter_id, dtype=np.uint32)
+        out = np.zeros(n, dtype=np.uint64)
+        r = self.L.rfr_lookup_batch(self.h, ctypes.addressof(arr), _p(fid), _p(k), key_len, n, _p(out))
+        if r < 0:
+            raise RuntimeError("routing_filter_amd_lookup_batch failed")
+        return out, bool(r)
 
     def async_stats(self):
         b, p = ctypes.c_uint64(0), ctypes.c_uint64(0)

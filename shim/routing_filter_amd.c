@@ -488,38 +488,154 @@ routing_filter_amd_flush(void)
       return;
    }
    qsort(q, n, sizeof(*q), cmp_state_filter); /* stable grouping is enough: order unused */
-   uint32 *h     = malloc(sizeof(uint32) * n);
-   uint64 *found = malloc(sizeof(uint64) * n);
-   platform_assert(h && found);
+   uint32          *h      = malloc(sizeof(uint32) * n);
+   uint64          *found  = malloc(sizeof(uint64) * n);
+   rf_amd_batch   **groups = malloc(sizeof(*groups) * n);
+   uint64          *counts = malloc(sizeof(uint64) * n);
+   platform_status *grc    = malloc(sizeof(*grc) * n);
+   platform_assert(h && found && groups && counts && grc);
+   /* every distinct filter's states form one group; all groups go to the GPU in one round
+      trip (rf_amd_probe_many_hashes_host) */
+   uint32 ng = 0, nok = 0;
    for (uint64 s = 0; s < n;) {
       uint64 t = s;
       while (t < n && q[t]->filter.addr == q[s]->filter.addr) {
-         h[t] = q[t]->fp; /* the full 32-bit hash, stored when the state was queued */
          t++;
       }
       rf_amd_batch   *b;
       platform_status rc = resident(q[s]->cc, q[s]->cfg, &q[s]->filter, &b);
-      if (SUCCESS(rc)) {
-         rc = status_of(rf_amd_batch_probe_hashes_host(b, h + s, NULL, t - s, found + s));
+      grc[s]             = rc;
+      if (SUCCESS(rc)) { /* probed groups first, in queue order */
+         for (uint64 i = s; i < t; i++) {
+            h[nok + (i - s)] = q[i]->fp; /* the full 32-bit hash, stored when queued */
+         }
+         groups[ng] = b;
+         counts[ng] = t - s;
+         ng++;
+         nok += t - s;
       }
+      s = t;
+   }
+   platform_status prc =
+      status_of(rf_amd_probe_many_hashes_host(engine(), groups, NULL, counts, ng, h, found));
+   uint64 at = 0;
+   for (uint64 s = 0; s < n;) {
+      uint64 t = s;
+      while (t < n && q[t]->filter.addr == q[s]->filter.addr) {
+         t++;
+      }
+      platform_status rc = SUCCESS(grc[s]) ? prc : grc[s];
       for (uint64 i = s; i < t; i++) {
          routing_filter_lookup_async_state *st = q[i];
-         *st->found_values                     = SUCCESS(rc) ? found[i] : 0;
-         st->__async_result                    = rc;
-         async_callback_fn cb                  = st->callback;
-         void             *arg                 = st->callback_arg;
+         *st->found_values = SUCCESS(rc) ? found[at + (i - s)] : 0;
+         st->__async_result = rc;
+         async_callback_fn cb  = st->callback;
+         void             *arg = st->callback_arg;
          __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
          if (cb) {
             cb(arg);
          }
       }
-      __atomic_fetch_add(&g_async_batches, 1, __ATOMIC_RELAXED);
+      if (SUCCESS(grc[s])) {
+         at += t - s;
+      }
       s = t;
    }
+   __atomic_fetch_add(&g_async_batches, 1, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_probes, n, __ATOMIC_RELAXED);
    free(h);
    free(found);
+   free(groups);
+   free(counts);
+   free(grc);
    free(q);
+}
+
+typedef struct lookup_ref {
+   uint64 addr; /* the filter's index extent */
+   uint64 i;    /* position in the caller's arrays */
+} lookup_ref;
+
+static int
+cmp_lookup_ref(const void *a, const void *b)
+{
+   const lookup_ref *x = a, *y = b;
+   if (x->addr != y->addr) {
+      return x->addr < y->addr ? -1 : 1;
+   }
+   return x->i < y->i ? -1 : (x->i > y->i ? 1 : 0);
+}
+
+/* n lookups (filters[i], keys[i]) in one GPU round trip: the batch form of the per-bundle
+ * routing_filter_lookup calls of trunk_merge_lookup (src/trunk.c:6008-6075). found[i] equals
+ * what routing_filter_lookup(cc, cfg, &filters[i], keys[i], &found[i]) would return. */
+platform_status
+routing_filter_amd_lookup_batch(cache                *cc,
+                                const routing_config *cfg,
+                                routing_filter       *filters,
+                                const key            *keys,
+                                uint64                n,
+                                uint64               *found)
+{
+   if (n == 0) {
+      return STATUS_OK;
+   }
+   lookup_ref      *order  = malloc(sizeof(*order) * n);
+   uint32          *h      = malloc(sizeof(uint32) * n);
+   uint64          *fo     = malloc(sizeof(uint64) * n);
+   rf_amd_batch   **groups = malloc(sizeof(*groups) * n);
+   uint64          *counts = malloc(sizeof(uint64) * n);
+   platform_assert(order && h && fo && groups && counts);
+   /* group the lookups by filter */
+   for (uint64 i = 0; i < n; i++) {
+      order[i].addr = filters[i].addr;
+      order[i].i    = i;
+   }
+   qsort(order, n, sizeof(*order), cmp_lookup_ref);
+   platform_status rc = STATUS_OK;
+   uint32          ng = 0;
+   uint64          m  = 0;
+   for (uint64 s = 0; s < n && SUCCESS(rc);) {
+      uint64 t = s;
+      while (t < n && order[t].addr == order[s].addr) {
+         t++;
+      }
+      if (order[s].addr == 0) { /* NULL filter finds nothing (:1003-1006) */
+         for (uint64 i = s; i < t; i++) {
+            found[order[i].i] = 0;
+         }
+      } else {
+         rf_amd_batch *b;
+         rc = resident(cc, cfg, &filters[order[s].i], &b);
+         if (SUCCESS(rc)) {
+            for (uint64 i = s; i < t; i++) {
+               h[m + (i - s)] = data_key_hash(cfg->data_cfg, keys[order[i].i], cfg->seed);
+            }
+            groups[ng] = b;
+            counts[ng] = t - s;
+            ng++;
+            m += t - s;
+         }
+      }
+      s = t;
+   }
+   if (SUCCESS(rc)) {
+      rc = status_of(rf_amd_probe_many_hashes_host(engine(), groups, NULL, counts, ng, h, fo));
+   }
+   if (SUCCESS(rc)) {
+      uint64 at = 0;
+      for (uint64 i = 0; i < n; i++) {
+         if (order[i].addr != 0) {
+            found[order[i].i] = fo[at++];
+         }
+      }
+   }
+   free(order);
+   free(h);
+   free(fo);
+   free(groups);
+   free(counts);
+   return rc;
 }
 
 void

@@ -742,6 +742,51 @@ extern "C" int rf_amd_batch_probe_hashes_host(rf_amd_batch* b, const uint32_t* h
   return 0;
 }
 
+// Lookups against many resident filters in one round trip: group g probes counts[g] hashes
+// (consecutive in h_hashes) against filter filter_index[g] of batches[g]. One H2D of every
+// hash and filter id, one probe launch per group on the engine stream, one D2H, one
+// synchronisation -- the batch form of trunk_merge_lookup's per-bundle routing_filter_lookup
+// calls (src/trunk.c:6008-6075) and of a flush of queued routing_filter_lookup_async states.
+extern "C" int rf_amd_probe_many_hashes_host(rf_amd_engine* e, rf_amd_batch* const* batches,
+                                             const uint32_t* filter_index, const uint64_t* counts,
+                                             uint32_t num_groups, const uint32_t* h_hashes, uint64_t* h_found) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (num_groups && (!batches || !counts)) return fail(RF_AMD_EINVAL, "null group arrays");
+  uint64_t n = 0;
+  for (uint32_t g = 0; g < num_groups; g++) {
+    rf_amd_batch* b = batches[g];
+    if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "group on an unbuilt or foreign batch");
+    if (filter_index && filter_index[g] >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
+    n += counts[g];
+  }
+  if (n == 0) return 0;
+  if (!h_hashes || !h_found) return fail(RF_AMD_EINVAL, "null probe buffer");
+  HIPCHK(hipSetDevice(e->device));
+  std::lock_guard<std::mutex> lk(e->stage.mu);
+  if (int rc = stage_reserve(e, 16ull * n + 16)) return rc;
+  uint8_t* hh = static_cast<uint8_t*>(e->stage.h);
+  uint8_t* dd = static_cast<uint8_t*>(e->stage.d);
+  const size_t o_fid = 4 * n, o_found = (8 * n + 7) & ~7ull;
+  memcpy(hh, h_hashes, 4 * n);
+  uint32_t* hf = reinterpret_cast<uint32_t*>(hh + o_fid);
+  for (uint32_t g = 0, at = 0; g < num_groups; at += (uint32_t)counts[g], g++)
+    std::fill(hf + at, hf + at + counts[g], filter_index ? filter_index[g] : 0u);
+  HIPCHK(hipMemcpyAsync(dd, hh, 8 * n, hipMemcpyHostToDevice, e->stream));
+  uint64_t at = 0;
+  for (uint32_t g = 0; g < num_groups; g++) {
+    if (counts[g] == 0) continue;
+    if (int rc = do_probe(batches[g], IN_HASH, dd + 4 * at, nullptr, 4,
+                          reinterpret_cast<const uint32_t*>(dd + o_fid) + at, counts[g],
+                          reinterpret_cast<uint64_t*>(dd + o_found) + at, e->stream))
+      return rc;
+    at += counts[g];
+  }
+  HIPCHK(hipMemcpyAsync(hh + o_found, dd + o_found, 8 * n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  memcpy(h_found, hh + o_found, 8 * n);
+  return 0;
+}
+
 static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
                     const uint32_t* fid, uint64_t n, uint64_t* found, void* stream,
                     const uint64_t* d_runs) {

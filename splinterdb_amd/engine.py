@@ -46,7 +46,7 @@ EXPORTED = [
     "rf_amd_hash_keys", "rf_amd_hash_var_keys",
     "rf_amd_batch_export", "rf_amd_batch_import", "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
     "rf_amd_batch_build_hashes_host", "rf_amd_batch_probe_hashes_host", "rf_amd_engine_pool_stats",
-    "rf_amd_filter_print_abs", "rf_amd_batch_infos", "rf_amd_batch_destroy_on",
+    "rf_amd_filter_print_abs", "rf_amd_batch_infos", "rf_amd_batch_destroy_on", "rf_amd_probe_many_hashes_host",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -166,6 +166,7 @@ def load_library(build_if_missing=True):
     L.rf_amd_filter_print_abs.argtypes = [ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage), u64, vp, vp]
     L.rf_amd_batch_infos.argtypes = [vp, ctypes.POINTER(RfFilterInfo), vp]
     L.rf_amd_batch_destroy_on.argtypes = [vp, vp]
+    L.rf_amd_probe_many_hashes_host.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     _lib = L
     return L
 

@@ -117,12 +117,41 @@ def test_lookup_async_coalesced_equals_reference(pair):
     # every state was queued and completed by a flush with its callback fired; the states
     # whose arrival filled the queue (every 1024th) were flushed inside their own first call
     assert cb_s == P and run_s == P - P // 1024
-    assert p1 - p0 == P and 0 < b1 - b0 <= 3 * (P // 1024 + 1)
+    assert p1 - p0 == P and 0 < b1 - b0 <= P // 1024 + 1  # one GPU round trip per flush
     assert run_r == 0  # the reference's coroutine finds every page in the cache
     # and the synchronous form agrees with both
     for f in range(3):
         m = fid == f
         assert (shim.lookup_keys(descs_s[f], probe[m]) == want[m]).all()
+
+
+def test_lookup_batch_equals_reference_lookups(pair):
+    """routing_filter_amd_lookup_batch (the trunk_merge_lookup batch form): 30,000 lookups
+    spread over five filters and a NULL filter, in one GPU round trip, equal the reference's
+    routing_filter_lookup of each (filter, key)"""
+    ref, shim = pair
+    descs_r, descs_s, allkeys = [], [], []
+    for f, n in enumerate((1000, 80_000, 300_000, 5, 40_000)):
+        keys = K.random_keys(n, seed=200 + f)
+        h = ref.hash_keys(keys)
+        descs_r.append(ref.add(h, value=f))
+        descs_s.append(shim.add(h, value=f))
+        allkeys.append(keys)
+    descs_r.append(R.RoutingFilter())  # NULL filter: finds nothing
+    descs_s.append(R.RoutingFilter())
+    rng = np.random.default_rng(5)
+    P = 30_000
+    fid = rng.integers(0, 6, size=P).astype(np.uint32)
+    probe = K.random_keys(P, seed=0xBEE)
+    for i in np.nonzero(rng.random(P) < 0.6)[0]:
+        if fid[i] < 5:
+            src = allkeys[fid[i]]
+            probe[i] = src[rng.integers(0, src.shape[0])]
+    want, batched_r = ref.lookup_batch(descs_r, probe, fid)
+    got, batched_s = shim.lookup_batch(descs_s, probe, fid)
+    assert batched_s and not batched_r
+    assert (got == want).all()
+    assert (got[fid == 5] == 0).all() and (got[fid < 5] != 0).sum() > 0.4 * P
 
 
 def test_print_identical_to_reference(pair, capfd):
