@@ -105,14 +105,16 @@ __global__ __launch_bounds__(TILE_NT) void k_hash_count(const FilterPlan* __rest
                                                         uint32_t key_len, uint32_t fp_size,
                                                         uint32_t seed, EntT* __restrict__ ent,
                                                         uint32_t* __restrict__ cb_count,
-                                                        const uint32_t* __restrict__ gate) {
+                                                        const uint32_t* __restrict__ gate, uint32_t num_tiles) {
   __shared__ uint32_t s_hist[MAX_CB];
   if (gate && *gate == 0) return;  // fallback pass of the fused build: not needed
-  const uint32_t t = blockIdx.x;
+  // tiles grid-strided: the gated fallback launches a small grid (it is rarely needed)
+  for (uint32_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
   const FilterPlan& P = plans[tile_filter[t]];
   const uint32_t start = tile_start[t];
   const uint32_t count = min((uint32_t)TILE_KEYS, P.num_new - start);
   const uint32_t num_cb = 1u << P.cbits;
+  __syncthreads();  // the previous tile's histogram has been flushed
   for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) s_hist[i] = 0;
   __syncthreads();
   const uint32_t esh = fp_size + P.vs - P.cbits;  // entry >> esh = coarse bucket
@@ -131,6 +133,7 @@ __global__ __launch_bounds__(TILE_NT) void k_hash_count(const FilterPlan* __rest
   for (uint32_t i = threadIdx.x; i < num_cb; i += TILE_NT) {
     const uint32_t c = s_hist[i];
     if (c) atomicAdd(&cb_count[P.cb_base + i], c);
+  }
   }
 }
 
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
                                                      const EntT* __restrict__ ent,
                                                      EntT* __restrict__ part,
                                                      uint32_t* __restrict__ cb_cursor,
-                                                     const uint32_t* __restrict__ gate) {
+                                                     const uint32_t* __restrict__ gate, uint32_t num_tiles) {
   // The tile is sorted by coarse bucket in LDS, then each bucket's run is written by
   // consecutive lanes: whole 64-byte granules instead of scattered 4-byte stores.
   __shared__ EntT s_stage[TILE_KEYS];
@@ -218,7 +221,9 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
   if (gate && *gate == 0) return;
   constexpr int PER = TILE_KEYS / SCAT_NT;
   constexpr int BPT = MAX_CB / SCAT_NT;
-  const uint32_t t = blockIdx.x;
+  // tiles grid-strided: the gated fallback launches a small grid (it is rarely needed)
+  for (uint32_t t = blockIdx.x; t < num_tiles; t += gridDim.x) {
+  __syncthreads();  // the previous tile's staging has been written out
   const FilterPlan& P = plans[tile_filter[t]];
   const uint32_t start = tile_start[t];
   const uint32_t region = region_is_old ? P.old_region : P.num_new;
@@ -289,6 +294,7 @@ __global__ __launch_bounds__(SCAT_NT) void k_scatter(const FilterPlan* __restric
   for (uint32_t j = threadIdx.x; j < valid_total; j += SCAT_NT) {
     const EntT x = s_stage[j];
     dst[s_off[cb_of(x)] + j] = x;
+  }
   }
 }
 
@@ -2783,11 +2789,15 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
   }
 
 // counts: per coarse bucket counter array (atomically accumulated); gate: see k_hash_count
+// gated launches (the fused build's spill fallback, almost never needed) use a small grid
+// that strides over the tiles: most of their cost was dispatching one workgroup per tile
+constexpr uint32_t GATED_GRID = 256;
+
 template <typename EntT, bool FL = (sizeof(EntT) == 8)>
 static int launch_hash_count_t(const LaunchArgs& a, EntT* ent, uint32_t* counts, const uint32_t* gate) {
-  dim3 g(a.num_tiles), b(TILE_NT);
+  dim3 g(gate ? min(a.num_tiles, GATED_GRID) : a.num_tiles), b(TILE_NT);
 #define L(K) hipLaunchKernelGGL((k_hash_count<K, EntT, FL>), g, b, 0, (hipStream_t)a.stream, a.plans, a.tile_filter, \
-                                a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, counts, gate)
+                                a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, ent, counts, gate, a.num_tiles)
   KIND_SWITCH(a.kind, L);
 #undef L
   CHECK_LAUNCH();
@@ -2797,13 +2807,15 @@ static int launch_hash_count_t(const LaunchArgs& a, EntT* ent, uint32_t* counts,
 template <typename EntT, bool FL = (sizeof(EntT) == 8)>
 static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* gate) {
   if (a.num_tiles) {
-    hipLaunchKernelGGL((k_scatter<EntT, FL>), dim3(a.num_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.tile_filter, a.tile_start, 0u, a.fp_size, ent, part, a.cb_cursor, gate);
+    hipLaunchKernelGGL((k_scatter<EntT, FL>), dim3(gate ? min(a.num_tiles, GATED_GRID) : a.num_tiles), dim3(SCAT_NT), 0,
+                       (hipStream_t)a.stream, a.plans, a.tile_filter, a.tile_start, 0u, a.fp_size, ent, part,
+                       a.cb_cursor, gate, a.num_tiles);
     CHECK_LAUNCH();
   }
   if (a.num_old_tiles && !a.flag32) {  // 32-bit incremental builds read the old runs in K4
-    hipLaunchKernelGGL((k_scatter<EntT, FL>), dim3(a.num_old_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.old_tile_filter, a.old_tile_start, 1u, a.fp_size, ent, part, a.cb_cursor, gate);
+    hipLaunchKernelGGL((k_scatter<EntT, FL>), dim3(gate ? min(a.num_old_tiles, GATED_GRID) : a.num_old_tiles),
+                       dim3(SCAT_NT), 0, (hipStream_t)a.stream, a.plans, a.old_tile_filter, a.old_tile_start, 1u,
+                       a.fp_size, ent, part, a.cb_cursor, gate, a.num_old_tiles);
     CHECK_LAUNCH();
   }
   return 0;
