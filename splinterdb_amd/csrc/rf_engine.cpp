@@ -411,7 +411,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     e_first = 0;
     for (auto& p : b->plans) {
       p.e_first = e_first;
-      e_first += (uint64_t)SORT_CAP << p.cbits;
+      e_first += (uint64_t)CB_REGION << p.cbits;
     }
   }
   if (b->wide) {

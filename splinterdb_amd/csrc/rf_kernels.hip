@@ -505,7 +505,7 @@ __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(RF_SCAT
     const uint32_t x = s_stage[j];
     const uint32_t cb = cb_of(x);
     const uint32_t slot = s_off[cb] + j;  // position inside the bucket's region
-    if (slot < (uint32_t)SORT_CAP) dst[(uint64_t)cb * SORT_CAP + slot] = x;
+    if (slot < (uint32_t)SORT_CAP) dst[(uint64_t)cb * CB_REGION + slot] = x;
   }
   DBG_PHASE_K(2, 8);
 }
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   const uint32_t n = cb_count[cb];
   const uint32_t cbl = cb - P.cb_base;
   // fused build without spill: fixed SORT_CAP regions; otherwise the scanned starts
-  const uint32_t cb_rel = (spill && *spill == 0) ? cbl * (uint32_t)SORT_CAP : cb_start[cb];
+  const uint32_t cb_rel = (spill && *spill == 0) ? cbl * CB_REGION : cb_start[cb];
   CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_rel, P.e_first};
   if (n > SORT_CAP) {  // handled by k_cb_sort_big
     if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;

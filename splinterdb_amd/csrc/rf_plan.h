@@ -23,6 +23,11 @@ constexpr int TILE_KEYS = RF_TILE_KEYS;  // keys per K1/K3 tile
 constexpr int SCAT_NT = 512;
 constexpr int SORT_NT = 512;
 constexpr int SORT_CAP = 9216;   // entries per coarse bucket held in LDS (means 4096..8192, sd < 91)
+#ifndef RF_REGION_PAD
+#define RF_REGION_PAD 0
+#endif
+// fused build: each coarse bucket's region in `part` (SORT_CAP slots, spaced CB_REGION apart)
+constexpr uint32_t CB_REGION = SORT_CAP + RF_REGION_PAD;
 constexpr int BIG_NT = 1024;
 constexpr int BIG_GRID = 64;
 constexpr int LAYOUT_NT = 1024;

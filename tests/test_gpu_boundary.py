@@ -200,3 +200,17 @@ def test_probe_runs_equal_per_probe_filter_ids(oracle):
     torch.cuda.synchronize()
     assert torch.equal(f_ids, f_h)
     assert torch.equal(f_r2, f_i2)
+    # and both shapes equal the oracle's routing_filter_lookup of each probe in its filter
+    # (runs crossing waves, empty runs, and waves spanning five filters: the wave table path)
+    ocfg = oracle.make_config()
+    starts = np.cumsum([0] + sizes)
+    ofs = [oracle.filter_add(ocfg, oracle.hash_fixed(K.seq_keys(int(starts[i]), sizes[i]).reshape(-1), 24),
+                             value=vals[i]) for i in range(len(sizes))]
+    for cs, got in ((counts, f_runs), (counts2, f_r2)):
+        want = np.zeros(P, dtype=np.uint64)
+        at = 0
+        for i, c in enumerate(cs):
+            if c:
+                want[at:at + c] = ofs[i].lookup_hashes(h[at:at + c])
+            at += c
+        assert (got.cpu().numpy().view(np.uint64) == want).all()
