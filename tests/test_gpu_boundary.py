@@ -114,7 +114,9 @@ def test_estimate_unique_keys(oracle):
         oracle.estimate_unique_keys_from_count(oracle.make_config(), f.num_unique)
 
 
-def test_lookup_async_matches_sync_probe():
+def test_lookup_async_matches_sync_probe(oracle):
+    """rf_amd_lookup_async (routing_filter_lookup_async, routing_filter.h:130-155) returns the
+    oracle's routing_filter_lookup of every probe in its filter, and fires its callback."""
     cfg = E.routing_config_init()
     sizes, vals = [200_000, 50_000, 123_457], [0, 7, 63 - 32]
     keys = K.random_keys(sum(sizes), seed=5)
@@ -129,6 +131,14 @@ def test_lookup_async_matches_sync_probe():
     b.probe_keys(dev(pk), 24, dev(fid), pk.shape[0], found)
     torch.cuda.synchronize()
     want = found.cpu().numpy().view(np.uint64)
+    ocfg = oracle.make_config()
+    starts = np.cumsum([0] + sizes)
+    ph = oracle.hash_fixed(pk.reshape(-1), 24)
+    for i in range(3):
+        of = oracle.filter_add(ocfg, oracle.hash_fixed(keys[starts[i]:starts[i + 1]].reshape(-1), 24),
+                               value=vals[i])
+        sel = fid == i
+        assert (of.lookup_hashes(ph[sel]) == want[sel]).all()
     fired = threading.Event()
     la = E.LookupAsync(b, pk, fid, callback=fired.set)
     got = la.wait()
