@@ -152,7 +152,9 @@ uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
 #define RF_AMD_NUM_TIMINGS 9
 /* enable = number of event sets kept (0 = off): each build starts the next set of a ring,
  * so the stages of the last `enable` build+probe rounds can be read without synchronising
- * between them (rf_amd_batch_timings_back: back = 0 is the latest round). */
+ * between them (rf_amd_batch_timings_back: back = 0 is the latest round). A negative
+ * enable keeps -enable sets but records only the probe's start and end (every build stage
+ * reads back as -1): 2 event records per round instead of 10. */
 int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
 int rf_amd_batch_timings_back(rf_amd_batch *b, uint32_t back, float *ms, uint32_t n);
 /* diagnostics library only (librf_amd_stamps.so; the product library returns EINVAL for a

@@ -198,6 +198,7 @@ struct rf_amd_batch {
   bool built = false;
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
+  uint32_t ev_mask = EV_MASK_ALL;     // EV_MASK_PROBE: the probe's two events only
   ~rf_amd_batch() {
     for (auto ev : events) (void)hipEventDestroy(ev);
   }
@@ -613,6 +614,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.pages = b->d_pages.as<uint8_t>();
   a.outs = b->d_outs.p ? b->d_outs.as<FilterOut>() : nullptr;
   a.events = b->events.empty() ? nullptr : reinterpret_cast<void**>(b->events.data() + (size_t)b->ev_set * NUM_EVENTS);
+  a.ev_mask = b->ev_mask;
   return a;
 }
 
@@ -633,7 +635,7 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   a.in0 = in0;
   a.offs = offs;
   a.key_len = key_len;
-  if (a.events) HIPCHK(hipEventRecord(((hipEvent_t*)a.events)[EV_B_START], st));
+  if (a.events && (a.ev_mask >> EV_B_START & 1u)) HIPCHK(hipEventRecord(((hipEvent_t*)a.events)[EV_B_START], st));
   if (rf_launch_build_init(st, b->d_cb_count.as<uint32_t>(), b->wide ? nullptr : b->d_cb_cursor.as<uint32_t>(),
                            b->CB, b->d_outs.as<uint32_t>(), (uint32_t)(sizeof(FilterOut) / 4 * b->F),
                            b->d_overflow.as<uint32_t>(), b->wide ? nullptr : b->d_spill.as<uint32_t>()))
@@ -905,6 +907,8 @@ extern "C" int rf_amd_batch_set_timing(rf_amd_batch* b, int enable) {
   for (auto ev : b->events) (void)hipEventDestroy(ev);
   b->events.clear();
   b->ev_sets = b->ev_set = 0;
+  b->ev_mask = enable < 0 ? EV_MASK_PROBE : EV_MASK_ALL;
+  if (enable < 0) enable = -enable;
   if (enable > 0) {
     b->events.resize((size_t)NUM_EVENTS * enable);
     for (auto& ev : b->events) HIPCHK(hipEventCreate(&ev));
@@ -923,6 +927,7 @@ extern "C" int rf_amd_batch_timings_back(rf_amd_batch* b, uint32_t back, float* 
       {EV_B_LAYOUT, EV_B_ASSEMBLE}, {EV_B_START, EV_B_ASSEMBLE}, {EV_P_START, EV_P_END}};
   for (uint32_t i = 0; i < RF_AMD_NUM_TIMINGS; i++) {
     ms[i] = -1.f;
+    if (!(b->ev_mask >> pairs[i][0] & 1u) || !(b->ev_mask >> pairs[i][1] & 1u)) continue;  // not recorded
     if (hipEventSynchronize(ev[pairs[i][1]]) != hipSuccess) continue;
     float t = 0;
     if (hipEventElapsedTime(&t, ev[pairs[i][0]], ev[pairs[i][1]]) == hipSuccess) ms[i] = t;

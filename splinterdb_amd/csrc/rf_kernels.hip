@@ -2776,7 +2776,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
 // launch wrappers (called from rf_engine.cpp)
 // ======================================================================================
 #define CHECK_LAUNCH() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
-#define REC(slot) do { if (a.events) (void)hipEventRecord((hipEvent_t)a.events[slot], (hipStream_t)a.stream); } while (0)
+#define REC(slot) do { if (a.events && (a.ev_mask >> (slot) & 1u)) (void)hipEventRecord((hipEvent_t)a.events[slot], (hipStream_t)a.stream); } while (0)
 
 // dispatch on the input kind (template parameter of the hashing kernels)
 #define KIND_SWITCH(kind, L)           \

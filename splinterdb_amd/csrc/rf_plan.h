@@ -140,10 +140,15 @@ struct LaunchArgs {
   const uint64_t* probe_runs;  // probes grouped by filter: runs[f] <= i < runs[f+1] (nullptr: per-probe ids)
   const uint32_t* wave_tab;    // with probe_runs: per 64-probe wave, filter << 7 | leading probes in it
   void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)
+  uint32_t ev_mask;  // slots recorded (bit per EventSlot): all, or only the probe's two
 };
 
 // per-stage timing events: build = [B_START .. B_ASSEMBLE], probe = [P_START, P_END]
 enum EventSlot { EV_B_START = 0, EV_B_HASH, EV_B_SCAN, EV_B_SCATTER, EV_B_SORT, EV_B_SORT_BIG,
                  EV_B_LAYOUT, EV_B_ASSEMBLE, EV_P_START, EV_P_END, NUM_EVENTS };
+// probe-only timing: just the probe's start/end events, so a timed loop pays for 2 event
+// records per step instead of one between every kernel (10 records cost a C2 step 42 us)
+constexpr uint32_t EV_MASK_ALL = (1u << NUM_EVENTS) - 1;
+constexpr uint32_t EV_MASK_PROBE = 1u << EV_P_START | 1u << EV_P_END;
 
 }  // namespace rf

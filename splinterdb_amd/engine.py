@@ -666,9 +666,11 @@ class FilterBatch:
     STAGES = ["partition", "count_scan", "scatter", "cb_sort", "cb_sort_big", "layout",
               "assemble", "build_total", "probe"]
 
-    def set_timing(self, enable=True, sets=1):
-        """Per-stage HIP-event timing; `sets` rounds (build + probe) kept in a ring."""
-        _check(load_library().rf_amd_batch_set_timing(self.h, sets if enable else 0))
+    def set_timing(self, enable=True, sets=1, probe_only=False):
+        """Per-stage HIP-event timing; `sets` rounds (build + probe) kept in a ring.
+        probe_only: record only the probe's two events (the build stages read -1)."""
+        n = sets if enable else 0
+        _check(load_library().rf_amd_batch_set_timing(self.h, -n if probe_only else n))
 
     def debug_lines(self) -> np.ndarray:
         """The batch's device-only probe lines (diagnostics), as an (N, 64) uint8 array."""
