@@ -290,6 +290,20 @@ static void bucket_bounds(const uint8_t *encoding, uint64_t len, uint64_t bucket
    }
 }
 
+/* exported for tests/test_ref_pinning.py, which fuzzes them against the reference's own
+ * static RadixSort / routing_get_bucket_bounds (oracle/ref_static.c) */
+uint32_t *rfo_radix_sort(uint32_t *pData, uint32_t *pTemp, uint32_t count, uint32_t fp_size)
+{
+   uint32_t mBuf[4 * 256];
+   return radix_sort(pData, mBuf, pTemp, count, fp_size);
+}
+
+void rfo_bucket_bounds(const uint8_t *encoding, uint64_t len, uint64_t bucket_offset, uint64_t *start,
+                       uint64_t *end)
+{
+   bucket_bounds(encoding, len, bucket_offset, start, end);
+}
+
 static int ensure_pages(const rfo_config *cfg, rfo_filter *f, uint32_t need)
 {
    if (need <= f->pages_cap) {

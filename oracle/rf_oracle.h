@@ -84,6 +84,11 @@ int      rfo_estimate_unique_fp(const rfo_config *cfg, const rfo_filter *filters
 uint32_t rfo_estimate_unique_keys_from_count(const rfo_config *cfg, uint64_t num_unique);
 uint64_t rfo_space_use_bytes(const rfo_config *cfg, const rfo_filter *f);
 void     rfo_bucket_counts(const rfo_config *cfg, const uint8_t *hdr, uint32_t *count);
+/* RadixSort (returns pData or pTemp: the buffer holding the result) and
+ * routing_get_bucket_bounds, exposed for the pinning tests */
+uint32_t *rfo_radix_sort(uint32_t *pData, uint32_t *pTemp, uint32_t count, uint32_t fp_size);
+void     rfo_bucket_bounds(const uint8_t *encoding, uint64_t len, uint64_t bucket_offset, uint64_t *start,
+                           uint64_t *end);
 
 /* handle-style helpers for ctypes */
 rfo_filter *rfo_filter_new(void);

@@ -276,3 +276,99 @@ def test_estimate_unique_keys_from_count_matches_reference(stacks, oracle):
             assert abs(int(got) - int(want)) <= 1, (fps, u, got, want)
             if u >= 1000:
                 assert got == want, (fps, u)
+
+
+# ---- the reference's static helpers, called one by one -----------------------------------
+# oracle/_ref/libref_static.so compiles the unmodified src/routing_filter.c inside
+# oracle/ref_static.c so RadixSort (:54-131) and routing_get_bucket_bounds (:230-279) can be
+# called directly; routing_get_bucket_counts (:281-306) too. The restatement's equivalents
+# (oracle/rf_oracle.c) must agree on every fuzzed input, including which buffer RadixSort
+# leaves the result in and what it leaves in the caller's array.
+REF_STATIC = os.path.join(os.path.dirname(R.LIB_PATH), "libref_static.so")
+
+
+@pytest.fixture(scope="module")
+def static_libs():
+    import ctypes
+    from oracle import oracle as O
+    if not os.path.exists(REF_STATIC):
+        pytest.skip("oracle/_ref/libref_static.so not built")
+    ref, orc = ctypes.CDLL(REF_STATIC), O.lib()
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    ref.refs_radix_sort.argtypes = [vp, vp, u32, u32]
+    ref.refs_radix_sort.restype = vp
+    orc.rfo_radix_sort.argtypes = [vp, vp, u32, u32]
+    orc.rfo_radix_sort.restype = vp
+    ref.refs_bucket_bounds.argtypes = [vp, u64, u64, vp, vp]
+    orc.rfo_bucket_bounds.argtypes = [vp, u64, u64, vp, vp]
+    ref.refs_bucket_counts.argtypes = [u32, vp, vp]
+    return ref, orc
+
+
+def test_reference_radix_sort_fuzz(static_libs):
+    ref, orc = static_libs
+    rng = np.random.default_rng(0x5A17)
+    for t in range(300):
+        fp = int(rng.integers(0, 33))
+        count = int(rng.choice([0, 1, 2, 7, int(rng.integers(3, 300)), int(rng.integers(300, 20000))]))
+        hi = 1 << fp
+        if t % 4 == 0:  # duplicate-heavy
+            vals = rng.integers(0, min(hi, 50) or 1, count, dtype=np.uint64)
+        else:
+            vals = rng.integers(0, hi, count, dtype=np.uint64)
+        data = vals.astype(np.uint32)
+        outs = []
+        for L, fn in ((ref, ref.refs_radix_sort), (orc, orc.rfo_radix_sort)):
+            a, tmp = data.copy(), np.zeros_like(data)
+            p = fn(a.ctypes.data, tmp.ctypes.data, count, fp)
+            which = "data" if count == 0 or p == a.ctypes.data else ("temp" if p == tmp.ctypes.data else "?")
+            outs.append((which, a, tmp))
+        (w1, a1, t1), (w2, a2, t2) = outs
+        assert w1 == w2 and w1 != "?", (t, fp, count, w1, w2)
+        assert (a1 == a2).all() and (t1 == t2).all(), (t, fp, count)
+        res = a1 if w1 == "data" else t1
+        assert (res == np.sort(data)).all(), (t, fp, count)
+
+
+def _encoding(rng, lis, c):
+    """a unary bucket encoding as routing_filter_add writes it (src/routing_filter.c:546-633):
+    per bucket n_b zeros then a one, then 0xFF padding to (c + index_size - 1) / 8 + 4 bytes;
+    followed by random bytes (the remainders that follow it on a page)"""
+    IS = 1 << lis
+    nb = np.bincount(rng.integers(0, IS, c), minlength=IS) if c else np.zeros(IS, dtype=np.int64)
+    enc_len = (c + IS - 1) // 8 + 4
+    bits = np.ones(enc_len * 8 + 64, dtype=np.uint8)
+    pos = 0
+    for b in range(IS):
+        bits[pos:pos + nb[b]] = 0
+        pos += nb[b] + 1
+    enc = np.packbits(bits[:enc_len * 8], bitorder="little")
+    tail = rng.integers(0, 256, 64, dtype=np.uint8)
+    return nb, enc_len, np.concatenate([enc, tail])
+
+
+def test_reference_bucket_bounds_and_counts_fuzz(static_libs):
+    import ctypes
+    ref, orc = static_libs
+    from oracle import oracle as O
+    rng = np.random.default_rng(0xB0B)
+    for t in range(120):
+        lis = int(rng.integers(1, 13))
+        c = int(rng.choice([0, 1, int(rng.integers(2, 64)), int(rng.integers(64, 4097))]))
+        nb, enc_len, buf = _encoding(rng, lis, c)
+        starts = np.concatenate([[0], np.cumsum(nb)[:-1]])
+        s1, e1, s2, e2 = (ctypes.c_uint64() for _ in range(4))
+        offs = range(1 << lis) if lis <= 9 else rng.integers(0, 1 << lis, 200)
+        for off in offs:
+            off = int(off)
+            ref.refs_bucket_bounds(buf.ctypes.data, enc_len, off, ctypes.byref(s1), ctypes.byref(e1))
+            orc.rfo_bucket_bounds(buf.ctypes.data, enc_len, off, ctypes.byref(s2), ctypes.byref(e2))
+            assert (s1.value, e1.value) == (s2.value, e2.value), (t, lis, c, off)
+            assert (s1.value, e1.value) == (starts[off], starts[off] + nb[off]), (t, lis, c, off)
+        hdr = np.concatenate([np.array([c & 0xff, c >> 8], dtype=np.uint8), buf])
+        cr = np.zeros(1 << lis, dtype=np.uint32)
+        co = np.zeros(1 << lis, dtype=np.uint32)
+        ref.refs_bucket_counts(lis, hdr.ctypes.data, cr.ctypes.data)
+        ocfg = O.make_config(log_index_size=lis)
+        O.lib().rfo_bucket_counts(ctypes.byref(ocfg), hdr.ctypes.data_as(ctypes.c_void_p), co.ctypes.data_as(ctypes.c_void_p))
+        assert (cr == co).all() and (cr == nb).all(), (t, lis, c)

@@ -1,16 +1,16 @@
 #!/bin/bash
 # Build librf_amd from a git revision into tools/ab/librf_amd_<tag>.so (A/B experiments).
-# usage: tools/ab_build.sh <rev> <tag>
+# usage: tools/ab_build.sh <rev> <tag> ["-DMACRO=V ..."]   (rev WT = the working tree)
 set -e
-REV=$1; TAG=$2; D=$(mktemp -d)
+REV=$1; TAG=$2; DEFS=$3; D=$(mktemp -d)
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p $D/splinterdb_amd/csrc $D/include
 for f in splinterdb_amd/csrc/rf_kernels.hip splinterdb_amd/csrc/rf_engine.cpp splinterdb_amd/csrc/rf_device.h splinterdb_amd/csrc/rf_plan.h include/rf_amd.h; do
-  git -C $ROOT show $REV:$f > $D/$f
+  if [ "$REV" = WT ]; then cp $ROOT/$f $D/$f; else git -C $ROOT show $REV:$f > $D/$f; fi
 done
 H=/opt/rocm/bin/hipcc
-$H --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c $D/splinterdb_amd/csrc/rf_kernels.hip -o $D/k.o
-$H -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c $D/splinterdb_amd/csrc/rf_engine.cpp -o $D/e.o
+$H --offload-arch=gfx950 -O3 -std=c++17 -fPIC $DEFS -c $D/splinterdb_amd/csrc/rf_kernels.hip -o $D/k.o
+$H -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $DEFS -c $D/splinterdb_amd/csrc/rf_engine.cpp -o $D/e.o
 $H --offload-arch=gfx950 -shared -fPIC -o $ROOT/tools/ab/librf_amd_$TAG.so $D/k.o $D/e.o
 rm -rf $D
 echo built tools/ab/librf_amd_$TAG.so
