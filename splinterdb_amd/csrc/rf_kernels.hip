@@ -595,6 +595,10 @@ __device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_
 // DUAL (32-bit incremental builds): a coarse bucket's entries come from two places -- its
 // new entries, scattered into part, and its run of the old filter's decoded entries
 // (already in order: old32 + P.old_first + ob_lo[cb], ob_n[cb] of them), loaded as (e << 1).
+// Only the new entries are ranked and sorted (s_b[0, nn)); the old run is stored as it comes
+// (s_b[nn, n)), and the dedupe pass reads the two sorted runs through a merge path. Old
+// flagged values are even and new ones odd, so no old value equals a new one and the merge
+// yields exactly the order a sort of all n would (old first on equal e).
 template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ cb_filter,
@@ -650,12 +654,15 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   const EntT* src = part + P.e_first + c.cb_rel;
   const uint32_t nm1 = n ? n - 1 : 0u;
   if constexpr (DUAL) {
-    const uint32_t nn = n - ob_n[cb];  // new entries first, then the old run
+    // new entries first, then the old run, loaded raw (one load per element from a selected
+    // address: nothing computed on the data before the barrier below, so it does not wait
+    // for the loads); old values get their flag (<< 1) when stored into s_b
+    const uint32_t nn = n - ob_n[cb];
     const uint32_t* osrc = old32 + P.old_first + ob_lo[cb];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const uint32_t j = min(threadIdx.x + k * SORT_NT, nm1);
-      v[k] = j < nn ? src[j] : (EntT)(osrc[j - nn] << 1);
+      v[k] = *(j < nn ? reinterpret_cast<const uint32_t*>(src) + j : osrc + (j - nn));
     }
   } else {
 #pragma unroll
@@ -667,10 +674,13 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   DBG_PHASE(0);
+  // the entries ranked and sorted here: all of them, or (DUAL) the new ones
+  uint32_t nsort = n;
+  if constexpr (DUAL) nsort = n - ob_n[cb];
   // per-bin rank (bin = filter bucket within the coarse bucket)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
-    if (threadIdx.x + k * SORT_NT < n) {
+    if (threadIdx.x + k * SORT_NT < nsort) {
       const uint32_t e = ent_e<EntT, FL>(v[k]);
       const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
       r[k] = atomicAdd(&s_bin[b], 1u);
@@ -707,17 +717,19 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       const uint32_t e8[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
       for (uint32_t k = 0; k < nbins; k++) s_bin[k] = e8[k];
     }
-    if (threadIdx.x == 0) s_bin[nbins] = n;
+    if (threadIdx.x == 0) s_bin[nbins] = nsort;
   }
   __syncthreads();
   DBG_PHASE(2);
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t i = threadIdx.x + k * SORT_NT;
-    if (i < n) {
+    if (i < nsort) {
       const uint32_t e = ent_e<EntT, FL>(v[k]);
       const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
       s_b[s_bin[b] + r[k]] = v[k];
+    } else if (i < n) {
+      s_b[i] = v[k] << 1;  // DUAL: the old run, already in order, flagged old
     }
   }
   __syncthreads();
@@ -731,8 +743,8 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   // entries that sort before it: smaller, or equal and earlier).
   {
     constexpr EntT EMAX = ~EntT(0);
-    uint32_t S = 8;  // largest power of two <= 8 with S * n / nbins <= 8
-    while (S > 1 && (uint64_t)S * n > 8ull * nbins) S >>= 1;
+    uint32_t S = 8;  // largest power of two <= 8 with S * nsort / nbins <= 8
+    while (S > 1 && (uint64_t)S * nsort > 8ull * nbins) S >>= 1;
     if (S > nbins) S = nbins;
     const uint32_t nseg = nbins / S;
     for (uint32_t sg = threadIdx.x; sg < nseg; sg += SORT_NT) {
@@ -824,14 +836,40 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   uint32_t keep_mask = 0, cnt = 0;
   EntT w[PER];
   const uint32_t i0 = threadIdx.x * drun;
-  const EntT prev0 = (i0 > 0 && i0 <= n) ? s_b[i0 - 1] : EntT(0);
+  EntT prev0 = (!DUAL && i0 > 0 && i0 <= n) ? s_b[i0 - 1] : EntT(0);
+  // DUAL: element i of the merged order of A = s_b[0, nsort) and B = s_b[nsort, n). The
+  // split of the first i0 - 1 elements (ia of them from A) by binary search; this thread's
+  // prev0 and run are the next drun + 1 elements of the merge.
+  uint32_t ia = 0, ib = 0;
+  if constexpr (DUAL) {
+    const uint32_t na = nsort, nbo = n - nsort;
+    const EntT* A = s_b;
+    const EntT* B = s_b + nsort;
+    const uint32_t d = i0 > 0 ? min(i0 - 1, n) : 0u;
+    uint32_t lo = d > nbo ? d - nbo : 0u, hi = min(d, na);
+    while (lo < hi) {  // ia = number of A elements among the first d merged ones
+      const uint32_t mid = (lo + hi) >> 1;
+      if (A[mid] < B[d - mid - 1]) lo = mid + 1; else hi = mid;
+    }
+    ia = lo;
+    ib = d - lo;
+    if (i0 > 0 && i0 <= n) {  // merged element i0 - 1
+      const bool ta = ib >= nbo || (ia < na && A[ia] < B[ib]);
+      prev0 = ta ? A[ia++] : B[ib++];
+    }
+  }
   {
     EntT prev = prev0;
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const uint32_t i = i0 + k;
       if ((uint32_t)k < drun && i < n) {
-        w[k] = s_b[i];
+        if constexpr (DUAL) {
+          const bool ta = ib >= n - nsort || (ia < nsort && s_b[ia] < s_b[nsort + ib]);
+          w[k] = ta ? s_b[ia++] : s_b[nsort + ib++];
+        } else {
+          w[k] = s_b[i];
+        }
         const bool drop = (i > 0) && ent_drop<EntT, FL>(w[k], prev);
         if (!drop) { keep_mask |= 1u << k; cnt++; }
         prev = w[k];

@@ -1,5 +1,6 @@
 """Per-phase shader-clock timing of the instrumented build kernels (diagnostics).
-Run on the GPU box: python tools/phase_times.py [filters] [keys_per_filter]"""
+Run on the GPU box: python tools/phase_times.py [kid] [filters] [keys_per_filter]
+(PT_CHAIN=R: stamp round R of compaction chains instead of a fresh build)"""
 import os
 import sys
 
@@ -9,7 +10,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from splinterdb_amd import build as B  # noqa: E402
 
-os.environ["RF_AMD_LIB"] = B.LIB_STAMPS  # stamps are compiled only into this build
+os.environ["RF_AMD_LIB"] = os.environ.get("PT_LIB") or B.LIB_STAMPS  # stamps: diagnostics build only
 from splinterdb_amd import engine as E  # noqa: E402
 from splinterdb_amd import keys as K  # noqa: E402
 
@@ -17,16 +18,32 @@ KID = int(sys.argv[1]) if len(sys.argv) > 1 else 1  # 1 = bucket sort, 2 = fused
 F = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 8_000_000
 cfg = E.routing_config_init()
-keys = K.seq_keys_torch(0, F * n, 24, "cuda:0")
-b = E.FilterBatch(cfg, [n] * F)
-for _ in range(2):
-    b.build_keys(keys, 24)
-torch.cuda.synchronize()
-buf = torch.zeros(1 << 22, dtype=torch.int64, device="cuda:0")
+CHAIN = int(os.environ.get("PT_CHAIN", "0"))  # > 0: stamp round CHAIN of compaction chains
+buf = torch.zeros(1 << 24, dtype=torch.int64, device="cuda:0")
 L = E.load_library()
-E._check(L.rf_amd_debug_phase_buffer(buf.data_ptr(), KID))
-b.build_keys(keys, 24)
-torch.cuda.synchronize()
+if CHAIN:
+    # bench.py --workload compaction's chains: round v of filter g adds (g << 32) + (v + 1) j
+    gid = torch.arange(F, device="cuda:0", dtype=torch.int64)[:, None] << 32
+    j = torch.arange(n, device="cuda:0", dtype=torch.int64)[None, :]
+    prev = None
+    for v in range(CHAIN):
+        keys = K.ids_keys_torch((gid + (v + 1) * j).reshape(-1), 24)
+        b = E.FilterBatch(cfg, [n] * F, [v] * F, old=[(prev, f) for f in range(F)] if prev else None)
+        if v == CHAIN - 1:
+            torch.cuda.synchronize()
+            E._check(L.rf_amd_debug_phase_buffer(buf.data_ptr(), KID))
+        b.build_keys(keys, 24)
+        torch.cuda.synchronize()
+        prev = b
+else:
+    keys = K.seq_keys_torch(0, F * n, 24, "cuda:0")
+    b = E.FilterBatch(cfg, [n] * F)
+    for _ in range(2):
+        b.build_keys(keys, 24)
+    torch.cuda.synchronize()
+    E._check(L.rf_amd_debug_phase_buffer(buf.data_ptr(), KID))
+    b.build_keys(keys, 24)
+    torch.cuda.synchronize()
 E._check(L.rf_amd_debug_phase_buffer(None, 0))
 ts = buf.cpu().numpy().reshape(-1, 16)
 used = ts[:, 8] != 0
