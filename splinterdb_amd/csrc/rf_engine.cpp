@@ -353,6 +353,16 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     int cb = (int)lnb - (int)CB_LOG_MEAN;
     if (cb < 0) cb = 0;
     if (cb > (int)(lnb - lis)) cb = (int)(lnb - lis);
+    // load factor ~1 (nfp just over a power of two: C3/C4's 2^20 keys) leaves coarse buckets
+    // of 2^12 buckets half full (~4K of SORT_CAP entries), and K4's cost is mostly per
+    // workgroup: use coarse buckets of 2^13 buckets (~8K entries, still >= 9 sd under
+    // SORT_CAP) with K4 bins of two buckets each (at most MAX_BINS bins, MAX_IPC indices)
+    p.binsh = 0;
+    if (cb >= 1 && lnb - cb == CB_LOG_MEAN && lis + 9 >= CB_LOG_MEAN + 1 /* ipc <= MAX_IPC */ &&
+        nfp * 1000 <= (1026ull << lnb)) {
+      cb -= 1;
+      p.binsh = 1;
+    }
     p.cbits = (uint32_t)cb;
     p.bbits = lnb - p.cbits;
     p.e_first = e_first;

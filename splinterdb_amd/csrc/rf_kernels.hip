@@ -643,8 +643,8 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
     return;
   }
-  const uint32_t nbins = 1u << P.bbits;
-  const uint32_t bmask = nbins - 1;
+  const uint32_t nbins = 1u << (P.bbits - P.binsh);  // a bin = 2^binsh filter buckets
+  const uint32_t bmask = nbins - 1, bsh = P.rvs + P.binsh;
   const uint32_t ipc = 1u << (P.bbits - lis), ish = lis + P.rvs;
   // the bucket's entry loads go out first (clamped, branch-free) and land while the bin
   // counters are cleared; the barrier after the clearing orders only LDS (a full
@@ -682,7 +682,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   for (int k = 0; k < PER; k++) {
     if (threadIdx.x + k * SORT_NT < nsort) {
       const uint32_t e = ent_e<EntT, FL>(v[k]);
-      const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
+      const uint32_t b = bsh >= 32 ? 0u : ((e >> bsh) & bmask);
       r[k] = atomicAdd(&s_bin[b], 1u);
     }
   }
@@ -726,7 +726,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     const uint32_t i = threadIdx.x + k * SORT_NT;
     if (i < nsort) {
       const uint32_t e = ent_e<EntT, FL>(v[k]);
-      const uint32_t b = P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask);
+      const uint32_t b = bsh >= 32 ? 0u : ((e >> bsh) & bmask);
       s_b[s_bin[b] + r[k]] = v[k];
     } else if (i < n) {
       s_b[i] = v[k] << 1;  // DUAL: the old run, already in order, flagged old
@@ -979,7 +979,7 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     const uint32_t n = cb_count[cb];
     const uint32_t cbl = cb - P.cb_base;
     CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_start[cb], P.e_first};
-    const uint32_t nbins = 1u << P.bbits, bmask = nbins - 1;
+    const uint32_t nbins = 1u << (P.bbits - P.binsh), bmask = nbins - 1, bsh = P.rvs + P.binsh;
     const EntT* srcp = part + P.e_first + c.cb_rel;
     const uint32_t nn = DUAL ? n - ob_n[cb] : n;
     const uint32_t* osrc = DUAL ? old32 + P.old_first + ob_lo[cb] : nullptr;
@@ -992,7 +992,7 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n; i += BIG_NT) {
       const uint32_t e = ent_e<EntT, FL>(src(i));
-      atomicAdd(&s_bin[P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask)], 1u);
+      atomicAdd(&s_bin[bsh >= 32 ? 0u : ((e >> bsh) & bmask)], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     for (uint32_t i = threadIdx.x; i < n; i += BIG_NT) {
       const EntT x = src(i);
       const uint32_t e = ent_e<EntT, FL>(x);
-      tmp[atomicAdd(&s_cur[P.rvs >= 32 ? 0u : ((e >> P.rvs) & bmask)], 1u)] = x;
+      tmp[atomicAdd(&s_cur[bsh >= 32 ? 0u : ((e >> bsh) & bmask)], 1u)] = x;
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nbins; b += BIG_NT) {

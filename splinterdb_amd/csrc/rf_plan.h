@@ -51,6 +51,8 @@ struct FilterPlan {
   uint32_t vs, rem, rvs, lnb;
   uint32_t num_indices;
   uint32_t cbits, bbits;  // coarse-bucket bits, bucket-in-coarse-bucket bits (sum = lnb)
+  uint32_t binsh;         // K4 bins = buckets >> binsh (1: coarse buckets of 2^13 buckets at
+                          // load factor ~1, so a workgroup sorts ~8K entries, not ~4K)
   uint32_t cb_base, idx_base, page_base, page_cap, pf_base;
   // probe lines (device-only, 64 B per group of 2^(lg_line-1) buckets; lg_line 0 = none)
   uint32_t lg_line, line_base;

@@ -102,3 +102,45 @@ def test_random_geometry_parity(oracle, seed):
         assert (img2.num_unique, img2.num_pages) == (of2.num_unique, of2.num_pages), seed
         assert (img2.pages == of2.pages()).all(), seed
         assert (img2.slots == of2.slots()[: of2.num_indices]).all(), seed
+
+
+# Load factor ~1 (num_fingerprints within 2.6 % above a power of two, >= 2^13): the engine
+# plans coarse buckets of 2^13 filter buckets with K4 bins of two buckets (FilterPlan.binsh).
+# These geometries, fresh and incremental (32- and 64-bit pipelines), against the oracle.
+@pytest.mark.parametrize("lis,fp,k", [(4, 22, 13), (6, 26, 16), (8, 26, 18), (8, 26, 20), (9, 30, 17),
+                                      (11, 32, 19), (8, 32, 16)])
+def test_load_factor_one_geometries(oracle, lis, fp, k):
+    rng = np.random.default_rng(lis * 1000 + fp * 10 + k)
+    cfg = E.routing_config_init(fingerprint_size=fp, log_index_size=lis)
+    ocfg = oracle.make_config(fingerprint_size=fp, log_index_size=lis)
+    vmax = min(63, (1 << (32 - fp)) - 1)
+    sizes = [1 << k, (1 << k) + 5, int((1 << k) * 1.02)]
+    vals = [int(rng.integers(0, vmax + 1)) for _ in sizes]
+    hs = [_hashes(rng, n, dup=(i == 2)) for i, n in enumerate(sizes)]
+    ofs = [oracle.filter_add(ocfg, h, value=v) for h, v in zip(hs, vals)]
+    b = E.FilterBatch(cfg, sizes, vals)
+    b.build_hashes(dev(np.concatenate(hs)))
+    for f, of in enumerate(ofs):
+        img = b.image(f)
+        assert (img.num_unique, img.num_pages) == (of.num_unique, of.num_pages), f
+        assert (img.pages == of.pages()).all(), f
+        assert (img.slots == of.slots()[: of.num_indices]).all(), f
+    # an incremental add whose total lands at load factor ~1 again: 2^(k+1) fingerprints
+    n2 = (1 << (k + 1)) - sizes[0]
+    v2 = vmax
+    h2 = _hashes(rng, n2, dup=False)
+    of2 = oracle.filter_add(ocfg, h2, value=v2, old=ofs[0])
+    b2 = E.FilterBatch(cfg, [n2], [v2], old=[(b, 0)])
+    b2.build_hashes(dev(h2))
+    img2 = b2.image(0)
+    assert (img2.num_unique, img2.num_pages) == (of2.num_unique, of2.num_pages)
+    assert (img2.pages == of2.pages()).all()
+    assert (img2.slots == of2.slots()[: of2.num_indices]).all()
+    P = 20000
+    allh = np.concatenate([h2, hs[0]])
+    ph = np.concatenate([allh[rng.integers(0, allh.size, P // 2)],
+                         rng.integers(0, 1 << 32, size=P - P // 2, dtype=np.uint64).astype(np.uint32)])
+    found = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b2.probe_hashes(dev(ph), dev(np.zeros(P, dtype=np.uint32)), P, found)
+    torch.cuda.synchronize()
+    assert (found.cpu().numpy().view(np.uint64) == of2.lookup_hashes(ph)).all()

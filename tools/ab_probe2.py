@@ -44,7 +44,7 @@ for shape, (F, n) in shapes.items():
         found = torch.empty(N, dtype=torch.int64, device=dev)
         libs.append((os.path.basename(os.path.dirname(path)) + "/" + os.path.basename(path), L, b, found, nn, vals))
     torch.cuda.synchronize()
-    res = {name: {"probe": [], "build": [], "assemble": [], "sort": [], "partition": []} for name, *_ in libs}
+    res = {name: {"probe": [], "build": [], "assemble": [], "sort": [], "partition": [], "layout": []} for name, *_ in libs}
     arr = (ctypes.c_float * 9)()
     for rnd in range(7):
         for name, L, b, found, *_ in libs:
@@ -54,7 +54,7 @@ for shape, (F, n) in shapes.items():
             L.rf_amd_batch_timings(b, arr, 9)
             r = res[name]
             r["probe"].append(arr[8]); r["build"].append(arr[7]); r["assemble"].append(arr[6])
-            r["sort"].append(arr[3]); r["partition"].append(arr[0])
+            r["sort"].append(arr[3]); r["partition"].append(arr[0]); r["layout"].append(arr[5])
     ref = libs[0][3]
     same = all(torch.equal(ref, x[3]) for x in libs[1:])
     allfound = bool(((ref & 1) == 1).all())
