@@ -196,6 +196,7 @@ struct rf_amd_batch {
       d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill,
       d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n, d_pg_noline;
   bool built = false;
+  bool has_entries = false;  // built here: its sorted entries (d_part / d_sorted) are current
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
   uint32_t ev_mask = EV_MASK_ALL;     // EV_MASK_PROBE: the probe's two events only
@@ -310,6 +311,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   uint64_t e_first = 0, key_first = 0;
   uint32_t cb_base = 0, idx_base = 0, page_base = 0, pf_base = 0;
   uint64_t line_base = 0;
+  std::vector<std::pair<const rf_amd_batch*, const FilterPlan*>> olds(num_filters, {nullptr, nullptr});
   for (uint32_t f = 0; f < num_filters; f++) {
     FilterPlan& p = b->plans[f];
     memset(&p, 0, sizeof(p));
@@ -393,10 +395,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       p.npo = p.num_indices / op->num_indices;
       p.old_pages = ob->d_pages.as<uint8_t>() + (uint64_t)op->page_base * P;
       p.old_slots = ob->d_slots.as<uint64_t>() + op->idx_base;
-      p.old_idx_base = (uint32_t)b->old_idx_filter.size();
-      p.old_first = b->old_total;
-      b->old_total += p.old_region;
-      b->old_idx_filter.insert(b->old_idx_filter.end(), op->num_indices, f);
+      olds[f] = {ob, op};
     }
     for (uint32_t s = 0; s < p.num_new; s += TILE_KEYS) {
       b->tile_filter.push_back(f);
@@ -429,6 +428,29 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     // 32-bit entries when (e << 1) | flag fits: fp_size + value_size <= 31 in every filter
     b->flag32 = getenv("RF_AMD_WIDE64") == nullptr;
     for (const auto& p : b->plans) b->flag32 = b->flag32 && fps + p.vs <= 31;
+    // old filters: read in place from their batch's sorted entries when the geometry is the
+    // same (32-bit pipeline; the old batch built here, not imported), else decoded from the
+    // image -- only those join the batch's old-index list and old32
+    const bool direct_ok = b->flag32 && getenv("RF_AMD_OLD_DECODE") == nullptr;
+    for (uint32_t f = 0; f < num_filters; f++) {
+      const rf_amd_batch* ob = olds[f].first;
+      const FilterPlan* op = olds[f].second;
+      if (!op) continue;
+      FilterPlan& p = b->plans[f];
+      if (direct_ok && ob->has_entries && op->lnb == p.lnb && op->cbits == p.cbits &&
+          ob->cfg.fingerprint_size == fps && ob->cfg.log_index_size == lis) {
+        const uint32_t* es = ob->wide ? ob->d_sorted.as<uint32_t>() : ob->d_part.as<uint32_t>();
+        p.old_direct = 1;
+        p.old_entries = es + op->e_first;
+        p.old_idx_start = ob->d_idx_start.as<uint32_t>() + op->idx_base;
+        p.old_idx_cnt = ob->d_idx_cnt.as<uint32_t>() + op->idx_base;
+        continue;
+      }
+      p.old_idx_base = (uint32_t)b->old_idx_filter.size();
+      p.old_first = b->old_total;
+      b->old_total += p.old_region;
+      b->old_idx_filter.insert(b->old_idx_filter.end(), op->num_indices, f);
+    }
   }
   b->E = e_first;
   b->keys_total = key_first;
@@ -659,6 +681,7 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   int rc = rf_launch_build(&a);
   if (rc) return fail(RF_AMD_EINVAL, std::string("build launch: ") + hipGetErrorString((hipError_t)rc));
   b->built = true;
+  b->has_entries = true;
   return 0;
 }
 

@@ -658,7 +658,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     // address: nothing computed on the data before the barrier below, so it does not wait
     // for the loads); old values get their flag (<< 1) when stored into s_b
     const uint32_t nn = n - ob_n[cb];
-    const uint32_t* osrc = old32 + P.old_first + ob_lo[cb];
+    const uint32_t* osrc = (P.old_direct ? P.old_entries : old32 + P.old_first) + ob_lo[cb];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       const uint32_t j = min(threadIdx.x + k * SORT_NT, nm1);
@@ -729,7 +729,11 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       const uint32_t b = bsh >= 32 ? 0u : ((e >> bsh) & bmask);
       s_b[s_bin[b] + r[k]] = v[k];
     } else if (i < n) {
-      s_b[i] = v[k] << 1;  // DUAL: the old run, already in order, flagged old
+      // DUAL: the old run, already in order, flagged old (read in place: value bits re-widened
+      // to this filter's value_size, src/routing_filter.c:536-543; order is unchanged)
+      const uint32_t eo = (uint32_t)v[k];
+      const uint32_t e = P.old_direct ? ((eo >> P.old_vs) << P.vs) | (eo & ((1u << P.old_vs) - 1u)) : eo;
+      s_b[i] = (EntT)e << 1;
     }
   }
   __syncthreads();
@@ -982,8 +986,13 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     const uint32_t nbins = 1u << (P.bbits - P.binsh), bmask = nbins - 1, bsh = P.rvs + P.binsh;
     const EntT* srcp = part + P.e_first + c.cb_rel;
     const uint32_t nn = DUAL ? n - ob_n[cb] : n;
-    const uint32_t* osrc = DUAL ? old32 + P.old_first + ob_lo[cb] : nullptr;
-    auto src = [&](uint32_t i) -> EntT { return (!DUAL || i < nn) ? srcp[i] : (EntT)(osrc[i - nn] << 1); };
+    const uint32_t* osrc = DUAL ? (P.old_direct ? P.old_entries : old32 + P.old_first) + ob_lo[cb] : nullptr;
+    auto src = [&](uint32_t i) -> EntT {
+      if (!DUAL || i < nn) return srcp[i];
+      const uint32_t eo = osrc[i - nn];  // read in place: re-widen the value bits
+      const uint32_t e = P.old_direct ? ((eo >> P.old_vs) << P.vs) | (eo & ((1u << P.old_vs) - 1u)) : eo;
+      return (EntT)(e << 1);
+    };
     EntT* tmp = scratch + P.e_first + c.cb_rel;
     uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
     const uint32_t ipc = 1u << (P.bbits - lis), ish = lis + P.rvs;
@@ -1764,7 +1773,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_old_scan(const FilterPlan* __rest
                                                         uint32_t* __restrict__ old_tot) {
   __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
   const FilterPlan& P = plans[blockIdx.x];
-  const uint32_t n = P.old_num_indices;
+  const uint32_t n = P.old_direct ? 0u : P.old_num_indices;  // direct: read in place, no decode
   if (n == 0) return;
   constexpr int PER = MAX_INDICES / LAYOUT_NT;
   uint32_t v[PER], sum = 0;
@@ -1871,13 +1880,24 @@ __global__ __launch_bounds__(256) void k_old_cb_bounds(const FilterPlan* __restr
                                                        const uint32_t* __restrict__ cb_filter, uint32_t num_cb,
                                                        const uint32_t* __restrict__ old32,
                                                        const uint32_t* __restrict__ old_tot, uint32_t fp_size,
-                                                       uint32_t* __restrict__ ob_lo, uint32_t* __restrict__ ob_n,
-                                                       uint32_t* __restrict__ cb_count) {
+                                                       uint32_t lis, uint32_t* __restrict__ ob_lo,
+                                                       uint32_t* __restrict__ ob_n, uint32_t* __restrict__ cb_count) {
   const uint32_t cb = blockIdx.x * blockDim.x + threadIdx.x;
   if (cb >= num_cb) return;
   const uint32_t f = cb_filter[cb];
   const FilterPlan& P = plans[f];
   const uint32_t cl = cb - P.cb_base, ncb = 1u << P.cbits;
+  if (P.old_direct) {
+    // the old filter has this geometry: new coarse bucket cl is its coarse bucket cl, whose
+    // entries are those of its indices [cl * ipc, (cl + 1) * ipc), consecutive in its entry
+    // array (K4 compacts a coarse bucket's indices in order)
+    const uint32_t ipc = 1u << (P.bbits - lis), i0 = cl * ipc, i1 = i0 + ipc - 1;
+    const uint32_t lo = P.old_idx_start[i0], hi = P.old_idx_start[i1] + P.old_idx_cnt[i1];
+    ob_lo[cb] = lo;
+    ob_n[cb] = hi - lo;
+    cb_count[cb] += hi - lo;
+    return;
+  }
   const uint32_t tot = P.old_num_indices ? old_tot[f] : 0u;
   const uint32_t* o = old32 + P.old_first;
   const uint32_t esh = fp_size + P.vs - P.cbits;
@@ -2888,7 +2908,7 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
     if (a.num_tiles) { int rc = launch_hash_count_t<uint32_t, true>(a, ent, a.cb_count, nullptr); if (rc) return rc; }
     if (a.num_cb) {
       hipLaunchKernelGGL(k_old_cb_bounds, dim3((a.num_cb + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a.plans,
-                         a.cb_filter, a.num_cb, a.old32, a.old_tot, a.fp_size, a.ob_lo, a.ob_n, a.cb_count);
+                         a.cb_filter, a.num_cb, a.old32, a.old_tot, a.fp_size, a.lis, a.ob_lo, a.ob_n, a.cb_count);
       CHECK_LAUNCH();
     }
     REC(EV_B_HASH);

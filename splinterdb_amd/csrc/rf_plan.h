@@ -64,6 +64,14 @@ struct FilterPlan {
                           // are flagged in pg_noline and k_plines cuts their indices' lines
   const uint8_t* old_pages;
   const uint64_t* old_slots;
+  // 32-bit incremental builds whose old filter was built by this engine with the same
+  // geometry (lnb, coarse buckets): its entries are read in place from the old batch's
+  // sorted entry array (old_entries, old_idx_start / old_idx_cnt relative to it) -- no
+  // decode of its image. Value bits are re-widened (old_vs -> vs) as K4 loads them.
+  uint32_t old_direct;
+  const uint32_t* old_entries;
+  const uint32_t* old_idx_start;
+  const uint32_t* old_idx_cnt;
 };
 
 // one filter of routing_filter_estimate_unique_fp (src/routing_filter.c:702-848): the first

@@ -30,13 +30,18 @@ def chain_ids(g, v, n):
 
 
 @pytest.mark.skipif(not R.available(), reason="reference library not built")
-@pytest.mark.parametrize("entries", ["flag32", "wide64"])
+@pytest.mark.parametrize("entries", ["flag32", "flag32_decode", "wide64"])
 def test_chain_rounds_match_reference(entries, monkeypatch):
-    """both incremental pipelines: 32-bit flagged entries with the old runs read in place
-    (fp_size + value_size <= 31, the default) and 64-bit entries (forced here)"""
+    """both incremental pipelines: 32-bit flagged entries (fp_size + value_size <= 31, the
+    default) and 64-bit entries (forced here). With 32-bit entries a round whose geometry is
+    the previous round's (rounds 3 and 5: 40K -> 60K, 80K -> 100K fingerprints) reads the old
+    entries in place from the previous batch; the others decode the old image
+    (flag32_decode forces the decode for every round)"""
     if entries == "wide64":
         monkeypatch.setenv("RF_AMD_WIDE64", "1")
-    F, V, n = 3, 4, 20000
+    if entries == "flag32_decode":
+        monkeypatch.setenv("RF_AMD_OLD_DECODE", "1")
+    F, V, n = 3, 5, 20000
     cfg = E.routing_config_init(fingerprint_size=26, log_index_size=8, seed=42)
     eng = E.Engine(0)
     stream, copy = torch.cuda.Stream(), torch.cuda.Stream()
