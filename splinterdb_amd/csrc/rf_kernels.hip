@@ -650,7 +650,12 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   // counters are cleared; the barrier after the clearing orders only LDS (a full
   // __syncthreads would also wait for the loads)
   EntT v[PER];
-  uint32_t r[PER];
+  // ranks within a bin (< SORT_CAP): two 16-bit ranks per register -- the DUAL variant spilled
+  // with one register per rank
+  static_assert(SORT_CAP <= 65536 && PER % 2 == 0, "16-bit ranks, packed in pairs");
+  uint32_t rp[PER / 2];
+#pragma unroll
+  for (int k = 0; k < PER / 2; k++) rp[k] = 0;
   const EntT* src = part + P.e_first + c.cb_rel;
   const uint32_t nm1 = n ? n - 1 : 0u;
   if constexpr (DUAL) {
@@ -683,7 +688,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     if (threadIdx.x + k * SORT_NT < nsort) {
       const uint32_t e = ent_e<EntT, FL>(v[k]);
       const uint32_t b = bsh >= 32 ? 0u : ((e >> bsh) & bmask);
-      r[k] = atomicAdd(&s_bin[b], 1u);
+      rp[k / 2] |= atomicAdd(&s_bin[b], 1u) << (16 * (k & 1));
     }
   }
   __syncthreads();
@@ -727,7 +732,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     if (i < nsort) {
       const uint32_t e = ent_e<EntT, FL>(v[k]);
       const uint32_t b = bsh >= 32 ? 0u : ((e >> bsh) & bmask);
-      s_b[s_bin[b] + r[k]] = v[k];
+      s_b[s_bin[b] + ((rp[k / 2] >> (16 * (k & 1))) & 0xffffu)] = v[k];
     } else if (i < n) {
       // DUAL: the old run, already in order, flagged old (read in place: value bits re-widened
       // to this filter's value_size, src/routing_filter.c:536-543; order is unchanged)
