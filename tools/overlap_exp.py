@@ -19,15 +19,19 @@ keys = K.seq_keys_torch(0, N, 24, dev)
 fid = (torch.arange(N, device=dev, dtype=torch.int64) // n).to(torch.int32)
 found = [torch.empty(N, dtype=torch.int64, device=dev) for _ in range(2)]
 bs = [E.FilterBatch(cfg, [n] * F) for _ in range(2)]
-sA, sB = torch.cuda.Stream(), torch.cuda.Stream()
-steps = 10
+counts = [n] * F
+lo_p, hi_p = torch.cuda.Stream.priority_range()
+PRI = os.environ.get("OVL_PRI", "")  # "build" / "probe": that stream gets the high priority
+sA = torch.cuda.Stream(priority=hi_p if PRI == "build" else lo_p)
+sB = torch.cuda.Stream(priority=hi_p if PRI == "probe" else lo_p)
+steps = 20
 
 
 def serial():
     for k in range(steps):
         b = bs[k % 2]
         b.build_keys(keys, 24, stream=sA.cuda_stream)
-        b.probe_keys(keys, 24, fid, N, found[k % 2], stream=sA.cuda_stream)
+        b.probe_keys_runs(keys, 24, counts, found[k % 2], stream=sA.cuda_stream)
 
 
 def overlapped():
@@ -40,7 +44,7 @@ def overlapped():
         b.build_keys(keys, 24, stream=sA.cuda_stream)
         built[k].record(sA)
         sB.wait_event(built[k])
-        b.probe_keys(keys, 24, fid, N, found[k % 2], stream=sB.cuda_stream)
+        b.probe_keys_runs(keys, 24, counts, found[k % 2], stream=sB.cuda_stream)
         probed[k].record(sB)
 
 
@@ -52,4 +56,4 @@ for name, fn in (("serial", serial), ("overlapped", overlapped), ("serial", seri
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     ok = all(bool(((f & 1) == 1).all().item()) for f in found)
-    print(f"{name:10s} {dt * 1e3:.3f} ms/step  {N / dt / 1e6:,.0f} Mkeys/s  ok={ok}")
+    print(f"[{PRI or 'equal'}] {name:10s} {dt * 1e3:.3f} ms/step  {N / dt / 1e6:,.0f} Mkeys/s  ok={ok}")
