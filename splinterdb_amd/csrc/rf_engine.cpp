@@ -26,6 +26,8 @@ extern "C" int rf_launch_build(const LaunchArgs* a);
 extern "C" int rf_launch_old_decode(const LaunchArgs* a);
 extern "C" int rf_launch_wave_tab(void* stream, const uint64_t* runs, uint32_t nf, uint64_t n, uint32_t* tab);
 extern "C" int rf_launch_plines(const LaunchArgs* a);
+extern "C" int rf_launch_seg_fill(void* stream, const uint32_t* pre, uint32_t nf, uint32_t n, uint32_t* fof,
+                                  uint32_t* start, uint32_t mul);
 extern "C" int rf_launch_build_init(void* stream, uint32_t* cb_count, uint32_t* cb_cursor, uint32_t num_cb,
                                     uint32_t* outs_words, uint32_t num_out_words, uint32_t* overflow,
                                     uint32_t* spill);
@@ -182,8 +184,15 @@ struct rf_amd_batch {
   bool flag32 = false;      // wide build with 32-bit flagged entries (every fp_size + vs <= 31)
   uint64_t old_total = 0;   // flag32: decoded old entries reserved (sum of old num_fingerprints)
   std::vector<FilterPlan> plans;
-  std::vector<uint32_t> tile_filter, tile_start, old_tile_filter, old_tile_start, cb_filter, pg_filter, idx_filter,
-      old_idx_filter;
+  // per-filter prefix arrays (F + 1 each) of the batch's per-element maps: tiles, old tiles,
+  // coarse buckets, pages, indices, decoded old indices. The maps themselves (element ->
+  // filter, tile -> first key) are filled on the device (k_seg_fill), so creating a batch
+  // uploads O(filters) bytes, not O(indices + pages)
+  enum { PRE_TILE, PRE_OTILE, PRE_CB, PRE_PG, PRE_IDX, PRE_OIDX, NUM_PRE };
+  std::vector<uint32_t> pre;  // NUM_PRE x (F + 1)
+  uint32_t* pre_of(int k) { return pre.data() + (size_t)k * (F + 1); }
+  uint32_t num_tiles = 0, num_old_tiles = 0, num_old_idx = 0;
+  DevBuf d_pre;
   uint64_t E = 0, keys_total = 0;
   uint32_t CB = 0, I = 0, PS = 0, PF = 0;
   uint64_t NL = 0;         // probe lines (64 B each)
@@ -208,7 +217,7 @@ struct rf_amd_batch {
             &d_cb_filter, &d_overflow, &d_idx_cnt, &d_idx_start, &d_slots, &d_page_first, &d_pg_filter,
             &d_pages, &d_tile_filter, &d_tile_start, &d_old_tile_filter, &d_old_tile_start, &d_old_cnt,
             &d_old_pos, &d_first_old, &d_has_old, &d_pplans, &d_lines, &d_idx_filter, &d_spill,
-            &d_old_idx_filter, &d_old32, &d_old_tot, &d_ob_lo, &d_ob_n, &d_pg_noline};
+            &d_old_idx_filter, &d_old32, &d_old_tot, &d_ob_lo, &d_ob_n, &d_pg_noline, &d_pre};
   }
 };
 
@@ -306,6 +315,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   b->cfg = *cfg;
   b->F = num_filters;
   b->plans.resize(num_filters);
+  b->pre.assign((size_t)rf_amd_batch::NUM_PRE * (num_filters + 1), 0u);
   const uint32_t lis = cfg->log_index_size, fps = cfg->fingerprint_size, P = cfg->page_size;
   const uint32_t IS = 1u << lis;
   uint64_t e_first = 0, key_first = 0;
@@ -397,17 +407,14 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       p.old_slots = ob->d_slots.as<uint64_t>() + op->idx_base;
       olds[f] = {ob, op};
     }
-    for (uint32_t s = 0; s < p.num_new; s += TILE_KEYS) {
-      b->tile_filter.push_back(f);
-      b->tile_start.push_back(s);
+    {
+      auto pre = [&](int k, uint32_t count) { b->pre_of(k)[f + 1] = b->pre_of(k)[f] + count; };
+      pre(rf_amd_batch::PRE_TILE, (p.num_new + TILE_KEYS - 1) / TILE_KEYS);
+      pre(rf_amd_batch::PRE_OTILE, (p.old_region + TILE_KEYS - 1) / TILE_KEYS);
+      pre(rf_amd_batch::PRE_CB, 1u << p.cbits);
+      pre(rf_amd_batch::PRE_PG, p.page_cap);
+      pre(rf_amd_batch::PRE_IDX, p.num_indices);
     }
-    for (uint32_t s = 0; s < p.old_region; s += TILE_KEYS) {
-      b->old_tile_filter.push_back(f);
-      b->old_tile_start.push_back(s);
-    }
-    for (uint32_t i = 0; i < (1u << p.cbits); i++) b->cb_filter.push_back(f);
-    for (uint32_t i = 0; i < p.page_cap; i++) b->pg_filter.push_back(f);
-    b->idx_filter.insert(b->idx_filter.end(), p.num_indices, f);
     e_first += nfp;
     key_first += p.num_new;
     cb_base += 1u << p.cbits;
@@ -446,12 +453,20 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
         p.old_idx_cnt = ob->d_idx_cnt.as<uint32_t>() + op->idx_base;
         continue;
       }
-      p.old_idx_base = (uint32_t)b->old_idx_filter.size();
+      p.old_idx_base = b->num_old_idx;
       p.old_first = b->old_total;
       b->old_total += p.old_region;
-      b->old_idx_filter.insert(b->old_idx_filter.end(), op->num_indices, f);
+      b->num_old_idx += op->num_indices;
+    }
+    // decoded old indices per filter (0 for filters without an old filter or read in place)
+    uint32_t* po = b->pre_of(rf_amd_batch::PRE_OIDX);
+    for (uint32_t f = 0; f < num_filters; f++) {
+      const FilterPlan& p = b->plans[f];
+      po[f + 1] = po[f] + ((olds[f].second && !p.old_direct) ? p.old_num_indices : 0u);
     }
   }
+  b->num_tiles = b->pre_of(rf_amd_batch::PRE_TILE)[num_filters];
+  b->num_old_tiles = b->pre_of(rf_amd_batch::PRE_OTILE)[num_filters];
   b->E = e_first;
   b->keys_total = key_first;
   b->CB = cb_base;
@@ -487,14 +502,15 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   rc |= b->d_pg_filter.alloc(4 * b->PS, pool);
   rc |= b->d_pg_noline.alloc(4 * b->PS + 4, pool);
   rc |= b->d_pages.alloc((size_t)b->PS * P + 256, pool);
-  rc |= b->d_tile_filter.alloc(4 * b->tile_filter.size(), pool);
-  rc |= b->d_tile_start.alloc(4 * b->tile_start.size(), pool);
-  rc |= b->d_old_tile_filter.alloc(4 * b->old_tile_filter.size(), pool);
-  rc |= b->d_old_tile_start.alloc(4 * b->old_tile_start.size(), pool);
+  rc |= b->d_tile_filter.alloc(4ull * b->num_tiles, pool);
+  rc |= b->d_tile_start.alloc(4ull * b->num_tiles, pool);
+  rc |= b->d_old_tile_filter.alloc(4ull * b->num_old_tiles, pool);
+  rc |= b->d_old_tile_start.alloc(4ull * b->num_old_tiles, pool);
+  rc |= b->d_pre.alloc(4 * b->pre.size(), pool);
   if (b->wide) {
-    rc |= b->d_old_cnt.alloc(4 * b->old_idx_filter.size(), pool);
-    rc |= b->d_old_pos.alloc(4 * b->old_idx_filter.size(), pool);
-    rc |= b->d_old_idx_filter.alloc(4 * b->old_idx_filter.size(), pool);
+    rc |= b->d_old_cnt.alloc(4ull * b->num_old_idx, pool);
+    rc |= b->d_old_pos.alloc(4ull * b->num_old_idx, pool);
+    rc |= b->d_old_idx_filter.alloc(4ull * b->num_old_idx, pool);
     rc |= b->d_first_old.alloc(4 * b->I, pool);
     rc |= b->d_has_old.alloc(4 * b->I, pool);
     if (b->flag32) {
@@ -509,14 +525,16 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     return fail(RF_AMD_ENOMEM, "device allocation failed");
   }
   hipStream_t st = e->stream;
-  // Page bytes the reference never writes are zero on a fresh cache page (SURVEY finding 4);
-  // K6 writes every byte of every page it assembles (block bytes and the zero tail), so
-  // this fill only covers reserved pages a build does not use.
-  HIPCHK(hipMemsetAsync(b->d_pages.p, 0, b->d_pages.n, st));
+  // Page bytes the reference never writes are zero on a fresh cache page (SURVEY finding 4).
+  // K6 writes every byte of every page it assembles (block bytes and the zero tail), and no
+  // reader looks past a filter's num_pages, so the reserved pages a build does not use are
+  // not cleared (page_cap reserves ~2x the pages: clearing them cost a compaction round
+  // ~0.3 ms); only the tail pad that windowed reads of the last page may touch is zeroed.
+  HIPCHK(hipMemsetAsync(b->d_pages.as<uint8_t>() + (size_t)b->PS * P, 0, b->d_pages.n - (size_t)b->PS * P, st));
   if (const char* pz = getenv("RF_AMD_POISON")) {
-    // test hook: fill every work buffer -- the page images included, after the zero fill
-    // above -- with a pattern, so that a kernel reading memory it did not write in this
-    // build, or leaving page bytes unwritten, cannot pass the parity tests
+    // test hook: fill every work buffer -- the page images included -- with a pattern, so
+    // that a kernel reading memory it did not write in this build, or leaving page bytes
+    // unwritten, cannot pass the parity tests
     const int v = atoi(pz) & 0xff;
     for (DevBuf* d : {&b->d_ent, &b->d_part, &b->d_sorted, &b->d_cb_start, &b->d_idx_cnt, &b->d_idx_start,
                       &b->d_slots, &b->d_lines, &b->d_page_first, &b->d_pages, &b->d_first_old, &b->d_has_old,
@@ -532,15 +550,29 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     pp[f] = make_uint4(q.vs | (q.rem << 8) | (q.rvs << 16) | (q.lg_line << 24), q.line_base, q.idx_base, 0);
   }
   UP(b->d_pplans, pp);
-  UP(b->d_tile_filter, b->tile_filter);
-  UP(b->d_tile_start, b->tile_start);
-  UP(b->d_old_tile_filter, b->old_tile_filter);
-  UP(b->d_old_tile_start, b->old_tile_start);
-  UP(b->d_cb_filter, b->cb_filter);
-  UP(b->d_pg_filter, b->pg_filter);
-  UP(b->d_idx_filter, b->idx_filter);
-  UP(b->d_old_idx_filter, b->old_idx_filter);
+  UP(b->d_pre, b->pre);
 #undef UP
+  {
+    // element -> filter maps (and tile -> first key) from the prefix arrays, on the device
+    const uint32_t F1 = num_filters + 1;
+    const uint32_t* dp = b->d_pre.as<uint32_t>();
+    struct M { int k; DevBuf* fof; DevBuf* start; };
+    const M maps[] = {{rf_amd_batch::PRE_TILE, &b->d_tile_filter, &b->d_tile_start},
+                      {rf_amd_batch::PRE_OTILE, &b->d_old_tile_filter, &b->d_old_tile_start},
+                      {rf_amd_batch::PRE_CB, &b->d_cb_filter, nullptr},
+                      {rf_amd_batch::PRE_PG, &b->d_pg_filter, nullptr},
+                      {rf_amd_batch::PRE_IDX, &b->d_idx_filter, nullptr},
+                      {rf_amd_batch::PRE_OIDX, &b->d_old_idx_filter, nullptr}};
+    for (const M& m : maps) {
+      const uint32_t n = b->pre_of(m.k)[num_filters];
+      if (n == 0 || !m.fof->p) continue;
+      if (rf_launch_seg_fill(st, dp + (size_t)m.k * F1, num_filters, n, m.fof->as<uint32_t>(),
+                             m.start ? m.start->as<uint32_t>() : nullptr, TILE_KEYS)) {
+        delete b;
+        return fail(RF_AMD_EINVAL, "map fill launch failed");
+      }
+    }
+  }
   HIPCHK(hipStreamSynchronize(st));
   *out = b;
   return 0;
@@ -602,12 +634,12 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.num_filters = b->F;
   a.tile_filter = b->d_tile_filter.as<uint32_t>();
   a.tile_start = b->d_tile_start.as<uint32_t>();
-  a.num_tiles = (uint32_t)b->tile_filter.size();
+  a.num_tiles = b->num_tiles;
   a.old_tile_filter = b->d_old_tile_filter.as<uint32_t>();
   a.old_tile_start = b->d_old_tile_start.as<uint32_t>();
-  a.num_old_tiles = (uint32_t)b->old_tile_filter.size();
+  a.num_old_tiles = b->num_old_tiles;
   a.old_idx_filter = b->d_old_idx_filter.as<uint32_t>();
-  a.num_old_idx = (uint32_t)b->old_idx_filter.size();
+  a.num_old_idx = b->num_old_idx;
   a.old_cnt = b->d_old_cnt.as<uint32_t>();
   a.old_pos = b->d_old_pos.as<uint32_t>();
   a.flag32 = b->flag32 ? 1u : 0u;

@@ -3008,6 +3008,31 @@ extern "C" int rf_launch_old_decode(const LaunchArgs* pa) {
   return 0;
 }
 
+// Element -> filter map of a batch (tiles, coarse buckets, pages, indices): pre[f] = first
+// element of filter f (pre[0] = 0, pre[nf] = n); fof[i] = the f with pre[f] <= i < pre[f + 1]
+// (filters with no elements are skipped), start[i] = (i - pre[f]) * mul (a tile's first key).
+__global__ __launch_bounds__(256) void k_seg_fill(const uint32_t* __restrict__ pre, uint32_t nf, uint32_t n,
+                                                  uint32_t* __restrict__ fof, uint32_t* __restrict__ start,
+                                                  uint32_t mul) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t lo = 0, hi = nf;  // pre[lo] <= i < pre[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= i) lo = mid; else hi = mid;
+  }
+  fof[i] = lo;
+  if (start) start[i] = (i - pre[lo]) * mul;
+}
+
+extern "C" int rf_launch_seg_fill(void* stream, const uint32_t* pre, uint32_t nf, uint32_t n, uint32_t* fof,
+                                  uint32_t* start, uint32_t mul) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_seg_fill, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, pre, nf, n, fof, start, mul);
+  CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int rf_launch_wave_tab(void* stream, const uint64_t* runs, uint32_t nf, uint64_t n, uint32_t* tab) {
   const uint64_t nw = (n + WAVE - 1) / WAVE;
   if (nw == 0) return 0;
