@@ -30,7 +30,7 @@ extern "C" int rf_launch_seg_fill(void* stream, const uint32_t* pre, uint32_t nf
                                   uint32_t* start, uint32_t mul);
 extern "C" int rf_launch_build_init(void* stream, uint32_t* cb_count, uint32_t* cb_cursor, uint32_t num_cb,
                                     uint32_t* outs_words, uint32_t num_out_words, uint32_t* overflow,
-                                    uint32_t* spill);
+                                    uint32_t* spill, uint32_t* plist);
 extern "C" int rf_launch_probe(const LaunchArgs* a, int kind, const void* in0, const uint64_t* offs,
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found);
 
@@ -702,7 +702,8 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   if (a.events && (a.ev_mask >> EV_B_START & 1u)) HIPCHK(hipEventRecord(((hipEvent_t*)a.events)[EV_B_START], st));
   if (rf_launch_build_init(st, b->d_cb_count.as<uint32_t>(), b->wide ? nullptr : b->d_cb_cursor.as<uint32_t>(),
                            b->CB, b->d_outs.as<uint32_t>(), (uint32_t)(sizeof(FilterOut) / 4 * b->F),
-                           b->d_overflow.as<uint32_t>(), b->wide ? nullptr : b->d_spill.as<uint32_t>()))
+                           b->d_overflow.as<uint32_t>(), b->wide ? nullptr : b->d_spill.as<uint32_t>(),
+                           b->d_pg_noline.as<uint32_t>()))
     return fail(RF_AMD_EINVAL, "init kernel launch failed");
   if (b->wide) {
     // every old filter of the batch decoded by one launch sequence (which also marks the

@@ -1455,6 +1455,8 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   const FilterPlan& P = plans[f];
   const uint32_t p = slot - P.page_base;
   if (outs[f].error || p >= outs[f].num_pages) return;
+  // a filter whose lines K6 never cuts: its pages go to k_plines_list
+  if (!P.lines_asm && P.lg_line && threadIdx.x == 0) pg_noline[1 + atomicAdd(&pg_noline[0], 1u)] = slot;
   const uint32_t* pf = page_first + P.pf_base;
   const uint32_t b0 = pf[p], b1 = pf[p + 1], nb = b1 - b0;
   uint4* dst = reinterpret_cast<uint4*>(pages + (uint64_t)slot * page_size);
@@ -1666,8 +1668,10 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   const uint32_t lgG = P.lg_line - 1, G = 1u << lgG, L = IS >> lgG;
   if (P.lines_flag) {  // this page's group table may not fit s_gs: then k_plines cuts its lines
     const bool over = nb * (L + 1) > ASM_GT;
-    if (threadIdx.x == 0) pg_noline[slot] = over ? 1u : 0u;
-    if (over) return;
+    if (over) {
+      if (threadIdx.x == 0) pg_noline[1 + atomicAdd(&pg_noline[0], 1u)] = slot;  // k_plines_list
+      return;
+    }
   }
   uint32_t wc[2], wsum = 0;  // encoding words per block (2 blocks per thread)
 #pragma unroll
@@ -2019,7 +2023,7 @@ extern "C" int rf_launch_estimate(void* stream, const EstFilter* fl, uint32_t nu
 __global__ __launch_bounds__(256) void k_build_init(uint32_t* __restrict__ cb_count, uint32_t* __restrict__ cb_cursor,
                                                     uint32_t num_cb, uint32_t* __restrict__ outs_words,
                                                     uint32_t num_out_words, uint32_t* __restrict__ overflow,
-                                                    uint32_t* __restrict__ spill) {
+                                                    uint32_t* __restrict__ spill, uint32_t* __restrict__ plist) {
   const uint32_t stride = gridDim.x * 256;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < num_cb; i += stride) {
     cb_count[i] = 0;
@@ -2029,15 +2033,16 @@ __global__ __launch_bounds__(256) void k_build_init(uint32_t* __restrict__ cb_co
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     overflow[0] = 0;
     if (spill) spill[0] = 0;
+    if (plist) plist[0] = 0;  // k_plines_list's page count
   }
 }
 
 extern "C" int rf_launch_build_init(void* stream, uint32_t* cb_count, uint32_t* cb_cursor, uint32_t num_cb,
                                     uint32_t* outs_words, uint32_t num_out_words, uint32_t* overflow,
-                                    uint32_t* spill) {
+                                    uint32_t* spill, uint32_t* plist) {
   const uint32_t want = (num_cb > num_out_words ? num_cb : num_out_words) / 256 + 1;
   hipLaunchKernelGGL(k_build_init, dim3(want < 1024 ? want : 1024), dim3(256), 0, (hipStream_t)stream, cb_count,
-                     cb_cursor, num_cb, outs_words, num_out_words, overflow, spill);
+                     cb_cursor, num_cb, outs_words, num_out_words, overflow, spill, plist);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -2333,48 +2338,31 @@ __device__ __forceinline__ uint64_t bits64_at(const uint8_t* pg, uint64_t bitpos
 // One wave per index (4 per workgroup). Phase 1: popcount-prefix over the encoding, the
 // position after each group's last bucket terminator -> LDS. Phase 2: 4 lanes per line,
 // 16 bytes each, bit-copied from the image.
-__global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ plans,
-                                                const uint32_t* __restrict__ idx_filter,
-                                                const uint64_t* __restrict__ slots,
-                                                const uint8_t* __restrict__ pages,
-                                                const FilterOut* __restrict__ outs,
-                                                const uint32_t* __restrict__ pg_noline,
-                                                uint4* __restrict__ lines, uint32_t num_idx,
-                                                uint32_t lmax, uint32_t lis, uint32_t page_size,
-                                                uint32_t force) {
-  // the index's block (at most one page) is first copied into a per-wave LDS slice with
-  // coalesced 16-byte loads; both phases then read their bits from LDS
+// One index's probe lines, cut by one wave from its block in the image: the block (at most
+// one page) is first copied into the wave's LDS slice `blk` with coalesced 16-byte loads;
+// both phases then read their bits from LDS. s_a: the wave's group-start table (L + 1).
+__device__ __forceinline__ void plines_index(const FilterPlan& P, uint32_t g, const uint64_t* __restrict__ slots,
+                                             const uint8_t* __restrict__ pages, uint4* __restrict__ lines,
+                                             uint8_t* blk, uint32_t* s_a, uint32_t lane, uint32_t lis,
+                                             uint32_t page_size) {
   constexpr uint32_t SLICE = MAX_PAGE + 64;
-  __shared__ __attribute__((aligned(16))) uint8_t s_blk[256 / WAVE][SLICE];
-  extern __shared__ uint32_t s_dyn[];
-  const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
-  const uint32_t g = blockIdx.x * (blockDim.x / WAVE) + wv;
-  uint32_t* s_a = s_dyn + wv * (lmax + 1);
-  const uint32_t f = g < num_idx ? idx_filter[g] : 0u;
-  const FilterPlan& P = plans[f];
-  bool active = g < num_idx && P.lg_line != 0 && !(outs && outs[f].error) && g - P.idx_base < P.num_indices;
-  // lines K6 did not cut: filters it never cuts, and the pages it flagged (lines_flag)
-  if (active && !force && P.lines_asm)
-    active = P.lines_flag && pg_noline && pg_noline[P.page_base + (uint32_t)(slots[g] / page_size)] != 0;
   const uint32_t IS = 1u << lis;
-  const uint32_t lgG = active ? P.lg_line - 1 : 0u, G = 1u << lgG, L = IS >> lgG;
-  const uint8_t* pg = s_blk[wv];
-  uint64_t rel = 0;
-  uint32_t c = 0;
-  if (active) {
-    const uint8_t* gp = pages + (uint64_t)P.page_base * page_size;
-    const uint64_t rel_g = slots[g];
-    c = (uint32_t)gp[rel_g] | ((uint32_t)gp[rel_g + 1] << 8);
-    const uint64_t a0 = rel_g & ~15ull;
-    const uint32_t used = (uint32_t)(rel_g - a0) + 2 + (c + IS - 1) / 8 + 4 +
-                          (uint32_t)(((uint64_t)c * P.rvs + 7) / 8) + 12;
-    const uint32_t nq = min((used + 15) / 16, SLICE / 16);
-    for (uint32_t q = lane; q < nq; q += WAVE)
-      reinterpret_cast<v4u*>(s_blk[wv])[q] = *reinterpret_cast<const v4u*>(gp + a0 + 16ull * q);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    rel = rel_g - a0;
+  const uint32_t lgG = P.lg_line - 1, G = 1u << lgG, L = IS >> lgG;
+  const uint8_t* pg = blk;
+  const uint8_t* gp = pages + (uint64_t)P.page_base * page_size;
+  const uint64_t rel_g = slots[g];
+  const uint32_t c = (uint32_t)gp[rel_g] | ((uint32_t)gp[rel_g + 1] << 8);
+  const uint64_t a0 = rel_g & ~15ull;
+  const uint32_t used = (uint32_t)(rel_g - a0) + 2 + (c + IS - 1) / 8 + 4 +
+                        (uint32_t)(((uint64_t)c * P.rvs + 7) / 8) + 12;
+  const uint32_t nq = min((used + 15) / 16, SLICE / 16);
+  for (uint32_t q = lane; q < nq; q += WAVE)
+    reinterpret_cast<v4u*>(blk)[q] = *reinterpret_cast<const v4u*>(gp + a0 + 16ull * q);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t rel = rel_g - a0;
+  {
     const uint64_t ebit = (rel + 2) * 8;
     const uint32_t nbits = c + IS;
     if (lane == 0) { s_a[0] = 0; s_a[L] = nbits; }
@@ -2395,8 +2383,9 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
       ones_before = __shfl(ex + ones, WAVE - 1, WAVE);
     }
   }
-  __syncthreads();
-  if (!active) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint32_t rvs = P.rvs;
   const uint64_t ebit = (rel + 2) * 8;
   const uint32_t enc = (c + IS - 1) / 8 + 4;
@@ -2425,6 +2414,58 @@ __global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ p
     }
     lines[(line0 + gl) * 4 + qq] =
         make_uint4((uint32_t)w[0], (uint32_t)(w[0] >> 32), (uint32_t)w[1], (uint32_t)(w[1] >> 32));
+  }
+}
+
+
+// Probe lines K6 did not cut, per index (rf_amd_batch_import's images and the diagnostics
+// rebuild, force = 1: every filter): one wave per index.
+__global__ __launch_bounds__(256) void k_plines(const FilterPlan* __restrict__ plans,
+                                                const uint32_t* __restrict__ idx_filter,
+                                                const uint64_t* __restrict__ slots,
+                                                const uint8_t* __restrict__ pages,
+                                                const FilterOut* __restrict__ outs,
+                                                uint4* __restrict__ lines, uint32_t num_idx,
+                                                uint32_t lmax, uint32_t lis, uint32_t page_size,
+                                                uint32_t force) {
+  constexpr uint32_t SLICE = MAX_PAGE + 64;
+  __shared__ __attribute__((aligned(16))) uint8_t s_blk[256 / WAVE][SLICE];
+  extern __shared__ uint32_t s_dyn[];
+  const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const uint32_t g = blockIdx.x * (blockDim.x / WAVE) + wv;
+  if (g >= num_idx) return;  // uniform per wave
+  const uint32_t f = idx_filter[g];
+  const FilterPlan& P = plans[f];
+  if (P.lg_line == 0 || (outs && outs[f].error) || g - P.idx_base >= P.num_indices) return;
+  if (!force && P.lines_asm) return;  // K6 cuts (or lists) this filter's lines
+  plines_index(P, g, slots, pages, lines, s_blk[wv], s_dyn + wv * (lmax + 1), lane, lis, page_size);
+}
+
+// Builds: the pages whose lines K6 left (filters it never cuts, and pages whose group table
+// does not fit its LDS) are listed by K6 in plist (plist[0] = count, then page slots); a small
+// grid walks the list, one wave per index of a listed page. An empty list costs one load per
+// workgroup (a grid over every index of the batch cost a compaction round 0.18 ms).
+__global__ __launch_bounds__(256) void k_plines_list(const FilterPlan* __restrict__ plans,
+                                                     const uint32_t* __restrict__ pg_filter,
+                                                     const uint32_t* __restrict__ page_first,
+                                                     const uint64_t* __restrict__ slots,
+                                                     const uint8_t* __restrict__ pages,
+                                                     const uint32_t* __restrict__ plist,
+                                                     uint4* __restrict__ lines, uint32_t lmax, uint32_t lis,
+                                                     uint32_t page_size) {
+  constexpr uint32_t SLICE = MAX_PAGE + 64;
+  __shared__ __attribute__((aligned(16))) uint8_t s_blk[256 / WAVE][SLICE];
+  extern __shared__ uint32_t s_dyn[];
+  const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const uint32_t n = plist[0];
+  for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
+    const uint32_t slot = plist[1 + e];
+    const FilterPlan& P = plans[pg_filter[slot]];
+    const uint32_t* pf = page_first + P.pf_base;
+    const uint32_t p = slot - P.page_base, b1 = pf[p + 1];
+    for (uint32_t b = pf[p] + wv; b < b1; b += 256 / WAVE)
+      plines_index(P, P.idx_base + b, slots, pages, lines, s_blk[wv], s_dyn + wv * (lmax + 1), lane, lis,
+                   page_size);
   }
 }
 
@@ -2900,6 +2941,7 @@ static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint3
 }
 
 extern "C" int rf_launch_plines(const LaunchArgs* pa);
+static int launch_plines_list(const LaunchArgs& a);
 
 extern "C" int rf_launch_build(const LaunchArgs* pa) {
   const LaunchArgs& a = *pa;
@@ -2975,7 +3017,7 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
                      a.pg_noline, a.lis, a.page_size);
   CHECK_LAUNCH();
   if (a.plines_needed)
-    if (int rc = rf_launch_plines(&a)) return rc;
+    if (int rc = launch_plines_list(a)) return rc;
   REC(EV_B_ASSEMBLE);
   return 0;
 }
@@ -2985,8 +3027,19 @@ extern "C" int rf_launch_plines(const LaunchArgs* pa) {
   if (!a.line_lmax) return 0;  // no filter of the batch has lines
   const size_t lds = 4ull * (256 / WAVE) * (a.line_lmax + 1);
   hipLaunchKernelGGL(k_plines, dim3((a.num_idx + 3) / 4), dim3(256), lds, (hipStream_t)a.stream, a.plans,
-                     a.idx_filter, a.slots, a.pages, a.outs, a.pg_noline, a.lines, a.num_idx, a.line_lmax, a.lis,
+                     a.idx_filter, a.slots, a.pages, a.outs, a.lines, a.num_idx, a.line_lmax, a.lis,
                      a.page_size, a.plines_force);
+  CHECK_LAUNCH();
+  return 0;
+}
+
+// the pages K6 listed in a build (k_plines_list)
+static int launch_plines_list(const LaunchArgs& a) {
+  if (!a.line_lmax || !a.num_page_slots) return 0;
+  const size_t lds = 4ull * (256 / WAVE) * (a.line_lmax + 1);
+  const uint32_t grid = a.num_page_slots < 1024 ? a.num_page_slots : 1024;
+  hipLaunchKernelGGL(k_plines_list, dim3(grid), dim3(256), lds, (hipStream_t)a.stream, a.plans, a.pg_filter,
+                     a.page_first, a.slots, a.pages, a.pg_noline, a.lines, a.line_lmax, a.lis, a.page_size);
   CHECK_LAUNCH();
   return 0;
 }

@@ -139,7 +139,7 @@ struct LaunchArgs {
   const uint32_t* idx_filter;
   uint32_t num_idx;
   uint32_t* page_first;
-  uint32_t* pg_noline;      // per page slot: K6 left this page's probe lines to k_plines
+  uint32_t* pg_noline;      // [0] = count, then the page slots whose probe lines K6 left to k_plines_list
   const uint32_t* pg_filter;
   uint32_t num_page_slots;
   uint8_t* pages;
