@@ -203,7 +203,7 @@ struct rf_amd_batch {
   DevBuf d_plans, d_outs, d_ent, d_part, d_sorted, d_cb_count, d_cb_start, d_cb_cursor, d_cb_filter,
       d_overflow, d_idx_cnt, d_idx_start, d_slots, d_page_first, d_pg_filter, d_pages, d_tile_filter,
       d_tile_start, d_old_tile_filter, d_old_tile_start, d_old_cnt, d_old_pos, d_first_old, d_has_old, d_pplans, d_lines, d_idx_filter, d_spill,
-      d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n, d_pg_noline;
+      d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n, d_pg_noline, d_cb_out;
   bool built = false;
   bool has_entries = false;  // built here: its sorted entries (d_part / d_sorted) are current
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
@@ -217,7 +217,7 @@ struct rf_amd_batch {
             &d_cb_filter, &d_overflow, &d_idx_cnt, &d_idx_start, &d_slots, &d_page_first, &d_pg_filter,
             &d_pages, &d_tile_filter, &d_tile_start, &d_old_tile_filter, &d_old_tile_start, &d_old_cnt,
             &d_old_pos, &d_first_old, &d_has_old, &d_pplans, &d_lines, &d_idx_filter, &d_spill,
-            &d_old_idx_filter, &d_old32, &d_old_tot, &d_ob_lo, &d_ob_n, &d_pg_noline, &d_pre};
+            &d_old_idx_filter, &d_old32, &d_old_tot, &d_ob_lo, &d_ob_n, &d_pg_noline, &d_pre, &d_cb_out};
   }
 };
 
@@ -422,9 +422,16 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     page_base += p.page_cap;
     pf_base += p.page_cap + 1;
   }
-  if (!b->wide) {
-    // fresh build: the fused kernel partitions straight into SORT_CAP slots per coarse
-    // bucket (k_hash_scatter), so each filter's entry region is its buckets' regions
+  if (b->wide) {
+    // 32-bit entries when (e << 1) | flag fits: fp_size + value_size <= 31 in every filter
+    b->flag32 = getenv("RF_AMD_WIDE64") == nullptr;
+    for (const auto& p : b->plans) b->flag32 = b->flag32 && fps + p.vs <= 31;
+  }
+  if (!b->wide || b->flag32) {
+    // fresh and 32-bit incremental builds: the fused kernel partitions the new keys straight
+    // into SORT_CAP slots per coarse bucket (k_hash_scatter), so each filter's entry region is
+    // its buckets' regions (>= its num_fingerprints: incremental builds' sorted entries, laid
+    // out by the scan of new + old counts, fit in it too)
     e_first = 0;
     for (auto& p : b->plans) {
       p.e_first = e_first;
@@ -432,9 +439,6 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
     }
   }
   if (b->wide) {
-    // 32-bit entries when (e << 1) | flag fits: fp_size + value_size <= 31 in every filter
-    b->flag32 = getenv("RF_AMD_WIDE64") == nullptr;
-    for (const auto& p : b->plans) b->flag32 = b->flag32 && fps + p.vs <= 31;
     // old filters: read in place from their batch's sorted entries when the geometry is the
     // same (32-bit pipeline; the old batch built here, not imported), else decoded from the
     // image -- only those join the batch's old-index list and old32
@@ -487,6 +491,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   rc |= b->d_ent.alloc(esz * b->E + 64, pool);
   rc |= b->d_part.alloc(esz * b->E + 64, pool);
   if (b->wide) rc |= b->d_sorted.alloc(4 * b->E + 64, pool);
+  if (b->flag32) rc |= b->d_cb_out.alloc(4 * b->CB, pool);
   rc |= b->d_cb_count.alloc(4 * b->CB, pool);
   rc |= b->d_cb_start.alloc(4 * b->CB, pool);
   rc |= b->d_cb_cursor.alloc(4 * b->CB, pool);
@@ -661,6 +666,7 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.num_cb = b->CB;
   a.overflow = b->d_overflow.as<uint32_t>();
   a.spill = b->d_spill.p ? b->d_spill.as<uint32_t>() : nullptr;
+  a.cb_outs = b->d_cb_out.p ? b->d_cb_out.as<uint32_t>() : nullptr;
   a.idx_cnt = b->d_idx_cnt.as<uint32_t>();
   a.idx_start = b->d_idx_start.as<uint32_t>();
   a.first_old = b->d_first_old.as<uint32_t>();
@@ -700,9 +706,9 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   a.offs = offs;
   a.key_len = key_len;
   if (a.events && (a.ev_mask >> EV_B_START & 1u)) HIPCHK(hipEventRecord(((hipEvent_t*)a.events)[EV_B_START], st));
-  if (rf_launch_build_init(st, b->d_cb_count.as<uint32_t>(), b->wide ? nullptr : b->d_cb_cursor.as<uint32_t>(),
+  if (rf_launch_build_init(st, b->d_cb_count.as<uint32_t>(), (b->wide && !b->flag32) ? nullptr : b->d_cb_cursor.as<uint32_t>(),
                            b->CB, b->d_outs.as<uint32_t>(), (uint32_t)(sizeof(FilterOut) / 4 * b->F),
-                           b->d_overflow.as<uint32_t>(), b->wide ? nullptr : b->d_spill.as<uint32_t>(),
+                           b->d_overflow.as<uint32_t>(), (b->wide && !b->flag32) ? nullptr : b->d_spill.as<uint32_t>(),
                            b->d_pg_noline.as<uint32_t>()))
     return fail(RF_AMD_EINVAL, "init kernel launch failed");
   if (b->wide) {

@@ -341,10 +341,11 @@ extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid) {
 // SORT_CAP (duplicate-heavy or adversarial input) raises *spill; the exact count -> scan
 // -> scatter pipeline (K1, K2, K3 gated on *spill) then rebuilds the partition.
 // ======================================================================================
-template <int KIND>
 #ifndef RF_SCAT_WPE
 #define RF_SCAT_WPE 4
 #endif
+// FL (32-bit incremental builds): the entries are written flagged new, (e << 1) | 1.
+template <int KIND, bool FL = false>
 __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(RF_SCAT_WPE))) void k_hash_scatter(const FilterPlan* __restrict__ plans,
                                                           const uint32_t* __restrict__ tile_filter,
                                                           const uint32_t* __restrict__ tile_start,
@@ -368,8 +369,9 @@ __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(RF_SCAT
   for (uint32_t i = threadIdx.x; i < num_cb; i += SCAT_NT) s_off[i] = 0;
   __syncthreads();
   DBG_PHASE_K(2, 0);
-  const uint32_t esh = fp_size + P.vs - P.cbits;  // entry >> esh = coarse bucket
+  const uint32_t esh = fp_size + P.vs - P.cbits + (FL ? 1u : 0u);  // entry >> esh = coarse bucket
   auto cb_of = [&](uint32_t e) -> uint32_t { return P.cbits ? (e >> esh) : 0u; };
+  const uint32_t flag = FL ? 1u : 0u;
   uint32_t v[PER], rank[PER];
   // all key loads first (clamped index: no branch, every load in flight at once), then the
   // LDS ranking -- interleaving them serialises one HBM round trip per key
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(RF_SCAT
       for (int k = 0; k < HASH_CHUNK; k++) {
         uint32_t w[6] = {ka[k].x + z, ka[k].y, kb[k].x, kb[k].y, kc[k].x, kc[k].y};
         const uint32_t h = xxh32_24(w, seed);
-        v[k0 + k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+        v[k0 + k] = ((((h >> (32 - fp_size)) << P.vs) | P.value) << flag) | flag;
       }
     } else if constexpr (KIND == IN_VAR) {
       // variable-length keys: this wave's keys [wave * 64 * PER, +64 * PER) are one
@@ -435,14 +437,14 @@ __global__ __launch_bounds__(SCAT_NT) __attribute__((amdgpu_waves_per_eu(RF_SCAT
         }
         const uint32_t h = wave_hash_var<VWIN, false>(static_cast<const uint8_t*>(in0), o0, o1,
                                                       key_of(k0 + k) < count, s_vwin, seed, &vw0, &vw1);
-        v[k0 + k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+        v[k0 + k] = ((((h >> (32 - fp_size)) << P.vs) | P.value) << flag) | flag;
       }
     } else {
 #pragma unroll
       for (int k = k0; k < k0 + HASH_CHUNK; k++) {
         const uint32_t j = min(threadIdx.x + k * SCAT_NT, count - 1) + dep;
         const uint32_t h = hash_key<KIND>(in0, offs, key_len, seed, P.key_first + start + j);
-        v[k] = ((h >> (32 - fp_size)) << P.vs) | P.value;
+        v[k] = ((((h >> (32 - fp_size)) << P.vs) | P.value) << flag) | flag;
       }
     }
     static_assert(HASH_CHUNK == 8, "opaque dependency below takes 8 hashes");
@@ -615,7 +617,8 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
                                                      uint32_t* __restrict__ overflow,
                                                      uint32_t lis, uint32_t* __restrict__ first_old,
                                                      uint32_t* __restrict__ has_old,
-                                                     const uint32_t* __restrict__ spill) {
+                                                     const uint32_t* __restrict__ spill,
+                                                     const uint32_t* __restrict__ cb_outs) {
   constexpr int PER = SORT_CAP / SORT_NT;
   DBG_PHASE(15);
   __shared__ EntT s_b[SORT_CAP];
@@ -638,7 +641,10 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   const uint32_t cbl = cb - P.cb_base;
   // fused build without spill: fixed SORT_CAP regions; otherwise the scanned starts
   const uint32_t cb_rel = (spill && *spill == 0) ? cbl * CB_REGION : cb_start[cb];
-  CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_rel, P.e_first};
+  // where the sorted entries go: in place, or (32-bit incremental builds with the fused
+  // partition) at the scan of the coarse buckets' new + old counts (cb_outs)
+  const uint32_t cb_out = (DUAL && spill) ? cb_outs[cb] : cb_rel;
+  CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_out, P.e_first};
   if (n > SORT_CAP) {  // handled by k_cb_sort_big
     if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
     return;
@@ -656,7 +662,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   uint32_t rp[PER / 2];
 #pragma unroll
   for (int k = 0; k < PER / 2; k++) rp[k] = 0;
-  const EntT* src = part + P.e_first + c.cb_rel;
+  const EntT* src = part + P.e_first + cb_rel;
   const uint32_t nm1 = n ? n - 1 : 0u;
   if constexpr (DUAL) {
     // new entries first, then the old run, loaded raw (one load per element from a selected
@@ -973,7 +979,9 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
                                                         FilterOut* __restrict__ outs,
                                                         const uint32_t* __restrict__ overflow,
                                                         uint32_t lis, uint32_t* __restrict__ first_old,
-                                                        uint32_t* __restrict__ has_old) {
+                                                        uint32_t* __restrict__ has_old,
+                                                        const uint32_t* __restrict__ spill,
+                                                        const uint32_t* __restrict__ cb_outs) {
   __shared__ uint32_t s_bin[MAX_BINS + 1];
   __shared__ uint32_t s_fo[MAX_IPC];
   __shared__ uint32_t s_ho[MAX_IPC];
@@ -987,9 +995,13 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     const FilterPlan& P = plans[f];
     const uint32_t n = cb_count[cb];
     const uint32_t cbl = cb - P.cb_base;
-    CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_start[cb], P.e_first};
+    const uint32_t in_rel = (spill && *spill == 0) ? cbl * CB_REGION : cb_start[cb];
+    // fused 32-bit incremental builds: the sorted (and scratch) layout is the scan of the
+    // coarse buckets' new + old counts (cb_outs), the new entries' layout is the partition's
+    const uint32_t out_rel = (DUAL && spill) ? cb_outs[cb] : in_rel;
+    CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), out_rel, P.e_first};
     const uint32_t nbins = 1u << (P.bbits - P.binsh), bmask = nbins - 1, bsh = P.rvs + P.binsh;
-    const EntT* srcp = part + P.e_first + c.cb_rel;
+    const EntT* srcp = part + P.e_first + in_rel;
     const uint32_t nn = DUAL ? n - ob_n[cb] : n;
     const uint32_t* osrc = DUAL ? (P.old_direct ? P.old_entries : old32 + P.old_first) + ob_lo[cb] : nullptr;
     auto src = [&](uint32_t i) -> EntT {
@@ -2929,12 +2941,12 @@ template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* spill) {
   hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
                      a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start, a.outs, a.overflow,
-                     a.lis, a.first_old, a.has_old, spill);
+                     a.lis, a.first_old, a.has_old, spill, a.cb_outs);
   CHECK_LAUNCH();
   REC(EV_B_SORT);
   hipLaunchKernelGGL((k_cb_sort_big<EntT, FL, DUAL>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans,
                      a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, ent, a.sorted32, a.idx_cnt, a.idx_start, a.outs,
-                     a.overflow, a.lis, a.first_old, a.has_old);
+                     a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
   CHECK_LAUNCH();
   REC(EV_B_SORT_BIG);
   return 0;
@@ -2950,22 +2962,38 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
     // are hashed, counted and scattered; each coarse bucket's run of the (sorted) old
     // entries decoded by rf_launch_old_decode is located by k_old_cb_bounds and read by K4
     // straight from old32 -- the old entries are neither counted nor scattered
+    // The new keys take the fused partition (flagged entries into fixed regions of SORT_CAP
+    // slots per coarse bucket, spill fallback as for a fresh build); K4 / K4b write each
+    // coarse bucket's sorted new + old entries at the scan of the new + old counts
     uint32_t* ent = (uint32_t*)a.ent;
     uint32_t* part = (uint32_t*)a.part;
-    if (a.num_tiles) { int rc = launch_hash_count_t<uint32_t, true>(a, ent, a.cb_count, nullptr); if (rc) return rc; }
+    if (a.num_tiles) {
+#define L(K) hipLaunchKernelGGL((k_hash_scatter<K, true>), dim3(a.num_tiles), dim3(SCAT_NT), 0, (hipStream_t)a.stream, \
+                                a.plans, a.tile_filter, a.tile_start, a.in0, a.offs, a.key_len, a.fp_size, a.seed, \
+                                part, a.cb_count, a.spill)
+      KIND_SWITCH(a.kind, L);
+#undef L
+      CHECK_LAUNCH();
+    }
+    // spill fallback (returns at once unless *spill): exact new counts, packed starts, scatter
+    if (a.num_tiles) { int rc = launch_hash_count_t<uint32_t, true>(a, ent, a.cb_cursor, a.spill); if (rc) return rc; }
+    hipLaunchKernelGGL(k_cb_scan, dim3(a.num_filters), dim3(256), 0, (hipStream_t)a.stream, a.plans, a.cb_cursor,
+                       a.cb_count, a.cb_start, a.cb_cursor, a.spill);
+    CHECK_LAUNCH();
+    if (int rc = launch_scatter_t<uint32_t, true>(a, ent, part, a.spill)) return rc;
     if (a.num_cb) {
       hipLaunchKernelGGL(k_old_cb_bounds, dim3((a.num_cb + 255) / 256), dim3(256), 0, (hipStream_t)a.stream, a.plans,
                          a.cb_filter, a.num_cb, a.old32, a.old_tot, a.fp_size, a.lis, a.ob_lo, a.ob_n, a.cb_count);
       CHECK_LAUNCH();
     }
     REC(EV_B_HASH);
+    // the sorted layout: starts of the coarse buckets' new + old counts
     hipLaunchKernelGGL(k_cb_scan, dim3(a.num_filters), dim3(256), 0, (hipStream_t)a.stream, a.plans, a.cb_count,
-                       a.cb_count, a.cb_start, a.cb_cursor, nullptr);
+                       a.cb_count, a.cb_outs, a.cb_outs, nullptr);
     CHECK_LAUNCH();
     REC(EV_B_SCAN);
-    if (int rc = launch_scatter_t<uint32_t, true>(a, ent, part, nullptr)) return rc;
     REC(EV_B_SCATTER);
-    if (int rc = launch_sort_t<uint32_t, true, true>(a, ent, part, nullptr)) return rc;
+    if (int rc = launch_sort_t<uint32_t, true, true>(a, ent, part, a.spill)) return rc;
   } else if (a.wide) {
     // incremental add: 64-bit entries; old entries first (decoded by rf_launch_old_decode)
     uint64_t* ent = (uint64_t*)a.ent;

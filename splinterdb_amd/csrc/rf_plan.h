@@ -140,6 +140,7 @@ struct LaunchArgs {
   uint32_t num_idx;
   uint32_t* page_first;
   uint32_t* pg_noline;      // [0] = count, then the page slots whose probe lines K6 left to k_plines_list
+  uint32_t* cb_outs;        // 32-bit incremental builds: per coarse bucket, where K4 writes its sorted entries
   const uint32_t* pg_filter;
   uint32_t num_page_slots;
   uint8_t* pages;

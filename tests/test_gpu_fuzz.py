@@ -144,3 +144,38 @@ def test_load_factor_one_geometries(oracle, lis, fp, k):
     b2.probe_hashes(dev(ph), dev(np.zeros(P, dtype=np.uint32)), P, found)
     torch.cuda.synchronize()
     assert (found.cpu().numpy().view(np.uint64) == of2.lookup_hashes(ph)).all()
+
+
+# Incremental adds whose new fingerprints pile into a few coarse buckets: the fused partition
+# of the new keys spills (its fixed regions overflow), the fallback re-partitions them, and
+# coarse buckets of new + old entries beyond LDS go to K4b -- both entry pipelines.
+@pytest.mark.parametrize("entries", ["flag32", "wide64"])
+def test_incremental_spill_and_big_buckets(oracle, entries, monkeypatch):
+    if entries == "wide64":
+        monkeypatch.setenv("RF_AMD_WIDE64", "1")
+    rng = np.random.default_rng(77)
+    cfg = E.routing_config_init(fingerprint_size=26, log_index_size=8)
+    ocfg = oracle.make_config(fingerprint_size=26, log_index_size=8)
+    h1 = rng.integers(0, 1 << 32, size=300_000, dtype=np.uint64).astype(np.uint32)
+    of1 = oracle.filter_add(ocfg, h1, value=0)
+    b1 = E.FilterBatch(cfg, [h1.size], [0])
+    b1.build_hashes(dev(h1))
+    # 32K new hashes: 12K copies of 5 values near one another (one coarse bucket: over its
+    # SORT_CAP region and over LDS), the rest random
+    hot = (np.uint32(0x9E370000) + np.arange(5, dtype=np.uint32) * np.uint32(97))
+    h2 = np.concatenate([hot[rng.integers(0, 5, size=12_000)],
+                         rng.integers(0, 1 << 32, size=20_000, dtype=np.uint64).astype(np.uint32)])
+    rng.shuffle(h2)
+    of2 = oracle.filter_add(ocfg, h2, value=1, old=of1)
+    b2 = E.FilterBatch(cfg, [h2.size], [1], old=[(b1, 0)])
+    b2.build_hashes(dev(h2))
+    img = b2.image(0)
+    assert (img.num_unique, img.num_pages) == (of2.num_unique, of2.num_pages)
+    assert (img.pages == of2.pages()).all()
+    assert (img.slots == of2.slots()[: of2.num_indices]).all()
+    P = 20000
+    ph = np.concatenate([h2[:P // 2], h1[:P // 2]])
+    found = torch.zeros(P, dtype=torch.int64, device="cuda:0")
+    b2.probe_hashes(dev(ph), dev(np.zeros(P, dtype=np.uint32)), P, found)
+    torch.cuda.synchronize()
+    assert (found.cpu().numpy().view(np.uint64) == of2.lookup_hashes(ph)).all()
