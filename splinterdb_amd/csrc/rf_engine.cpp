@@ -54,7 +54,8 @@ static int fail(int rc, const std::string& msg) {
 // a new set of filters on every compaction, so in steady state rf_amd_batch_create finds
 // its ~25 work buffers here instead of calling hipMalloc. Sizes are rounded up to classes
 // of 1/8 of a power of two (at most 12.5 % slack); a block returns to the pool when its
-// batch is destroyed unless the pool already holds RF_AMD_POOL_MIB (default 32768) MiB.
+// batch is destroyed unless the pool already holds RF_AMD_POOL_MIB MiB (default: a quarter
+// of the device memory, at least 32 GiB).
 // rf_amd_batch_destroy synchronises the device first; rf_amd_batch_destroy_on instead
 // parks the blocks behind an event on the caller's stream (stream-ordered release, as
 // hipFreeAsync): they become reusable once that event has completed.
@@ -97,17 +98,21 @@ struct DevPool {
       parked.pop_back();
     }
   }
-  void* take(size_t cls) {
+  // best fit: the smallest pooled block of at least `*cls` bytes and at most twice that
+  // (compaction rounds grow from one round to the next, so exact classes rarely recur within
+  // a chain); *cls becomes the block's size
+  void* take(size_t* cls) {
     std::lock_guard<std::mutex> g(mu);
     if (!parked.empty()) reap_locked(false);
-    auto it = free_blocks.find(cls);
-    if (it == free_blocks.end()) {
+    auto it = free_blocks.lower_bound(*cls);
+    if (it == free_blocks.end() || it->first > 2 * *cls) {
       misses++;
       return nullptr;
     }
     void* p = it->second;
+    *cls = it->first;
     free_blocks.erase(it);
-    pooled -= cls;
+    pooled -= *cls;
     hits++;
     return p;
   }
@@ -160,7 +165,7 @@ struct DevBuf {
     release();
     pool = from;
     n = from ? DevPool::size_class(bytes ? bytes : 16) : (bytes ? bytes : 16);
-    if (from && (p = from->take(n)) != nullptr) return 0;
+    if (from && (p = from->take(&n)) != nullptr) return 0;
     hipError_t e = hipMalloc(&p, n);
     if (e != hipSuccess && from) {  // the pool may hold what this needs: give it back, retry
       from->drain();
@@ -232,8 +237,12 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
   auto* e = new rf_amd_engine();
   e->device = device;
   {
+    // default: a quarter of the device's memory (72 GB on MI355X), at least 32 GiB
     const char* lim = getenv("RF_AMD_POOL_MIB");
-    e->pool.limit = (size_t)(lim ? atoll(lim) : 32768) << 20;
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const size_t dflt = std::max<size_t>((size_t)32768 << 20, total_b / 4);
+    e->pool.limit = lim ? (size_t)atoll(lim) << 20 : dflt;
   }
   // a BLOCKING stream: ordered with the legacy null stream that torch and most callers use
   if (hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess) {
@@ -535,7 +544,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   // reader looks past a filter's num_pages, so the reserved pages a build does not use are
   // not cleared (page_cap reserves ~2x the pages: clearing them cost a compaction round
   // ~0.3 ms); only the tail pad that windowed reads of the last page may touch is zeroed.
-  HIPCHK(hipMemsetAsync(b->d_pages.as<uint8_t>() + (size_t)b->PS * P, 0, b->d_pages.n - (size_t)b->PS * P, st));
+  HIPCHK(hipMemsetAsync(b->d_pages.as<uint8_t>() + (size_t)b->PS * P, 0, 256, st));
   if (const char* pz = getenv("RF_AMD_POISON")) {
     // test hook: fill every work buffer -- the page images included -- with a pattern, so
     // that a kernel reading memory it did not write in this build, or leaving page bytes
