@@ -1138,13 +1138,17 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   if (threadIdx.x == 0) s_err = 0;
   __syncthreads();
   // sizes -> exclusive prefix (element j = k * LAYOUT_NT + thread: coalesced loads)
+  // every count load first, from a clamped index (no branch around a load: each branch
+  // ended in its own wait, 16 serialised round trips per thread), then the sizes
   uint32_t sz[PER], err = 0;
+#pragma unroll
+  for (int k = 0; k < PER; k++) sz[k] = idx_cnt[P.idx_base + min((uint32_t)(k * LAYOUT_NT) + threadIdx.x, n - 1)];
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const uint32_t j = k * LAYOUT_NT + threadIdx.x;
+    const uint32_t c = sz[k];
     sz[k] = 0;
     if (j < n) {
-      const uint32_t c = idx_cnt[P.idx_base + j];
       if (c > 4096) err |= ERR_INDEX_OVERFLOW;
       sz[k] = block_size(c, index_size, P.rvs);
       if (sz[k] > page_size) err |= ERR_BLOCK_TOO_BIG;
@@ -1480,20 +1484,29 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   const uint32_t IS = 1u << lis, rvs = P.rvs;
   // (A) metadata + entry offsets (2 blocks per thread)
-  uint32_t cj[2], oj[2], sum = 0;
+  uint32_t cj[2], oj[2], sj[2], sum = 0;
+  uint64_t sl[2];
+  // both blocks' metadata loads first (clamped index, no branch around a load: each branch
+  // waited for its own loads)
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint32_t g = P.idx_base + b0 + min(threadIdx.x * 2 + q, nb - 1);
+    cj[q] = idx_cnt[g];
+    sl[q] = slots[g];
+    sj[q] = idx_start[g];
+  }
   for (uint32_t i = threadIdx.x; i < MAX_PAGE / 16; i += ASM_NT) s_wm[i] = 0;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const uint32_t j = threadIdx.x * 2 + q;
-    cj[q] = 0;
     oj[q] = 0;
     if (j < nb) {
-      const uint32_t g = P.idx_base + b0 + j;
-      cj[q] = idx_cnt[g];
-      oj[q] = (uint32_t)(slots[g] - (uint64_t)p * page_size);
+      oj[q] = (uint32_t)(sl[q] - (uint64_t)p * page_size);
       s_off[j] = oj[q];
       s_c[j] = cj[q];
-      s_src[j] = idx_start[g];
+      s_src[j] = sj[q];
+    } else {
+      cj[q] = 0;
     }
     sum += cj[q];
   }
