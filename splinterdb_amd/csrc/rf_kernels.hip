@@ -2607,7 +2607,15 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
   return true;
 }
 
-constexpr int PROBE_NT = 256;
+// threads per probe workgroup: 1,024 for fixed-length keys and hashes (C3 probe 2.74 ->
+// 2.59 ms per 256M vs 256: a quarter of the workgroups, each longer), 256 for variable-length
+// keys (their per-wave 4 KiB LDS windows; C5 0.325 vs 0.337 ms)
+#ifndef RF_PROBE_NT
+#define RF_PROBE_NT 1024
+#endif
+constexpr int PROBE_NT = RF_PROBE_NT;
+constexpr int PROBE_NT_VAR = 256;
+__host__ __device__ constexpr int probe_nt(int kind) { return kind == IN_VAR ? PROBE_NT_VAR : PROBE_NT; }
 constexpr int PROBE_LDS_PAD = 0;
 constexpr int PROBE_PPL = 1;  // probes per lane (production)
 
@@ -2719,7 +2727,7 @@ __device__ __forceinline__ uint64_t probe_walk(const uint4 P, uint32_t h, uint32
 }
 
 template <int KIND, int OCC_LDS = 0, int PPL = 1>
-__global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pplans,
+__global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restrict__ pplans,
                                                     const FilterPlan* __restrict__ plans,
                                                     const uint8_t* __restrict__ pages,
                                                     const uint64_t* __restrict__ slots,
@@ -2740,7 +2748,8 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
 #else
   (void)ablate;
 #endif
-  const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (PROBE_NT * PPL) + threadIdx.x;
+  constexpr int NT = probe_nt(KIND);
+  const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (NT * PPL) + threadIdx.x;
   uint32_t h[PPL], fid[PPL];
   uint4 pp[PPL];
   constexpr bool WAVE_KEYS = KIND == IN_KEYS24 && PPL == 1 && OCC_LDS == 0;
@@ -2748,7 +2757,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     // 24-byte keys: the wave's 64 keys (1,536 contiguous bytes) are read with 16-byte
     // coalesced loads -- 12 cache lines per wave, where three strided 8-byte loads per lane
     // touch 36 -- and handed to their lanes through LDS
-    __shared__ v4u s_keys[PROBE_NT / WAVE][96];
+    __shared__ v4u s_keys[NT / WAVE][96];
     const uint32_t lane = threadIdx.x & (WAVE - 1);
     const uint64_t wf = i0 - lane;
     fid[0] = 0xffffffffu;
@@ -2799,7 +2808,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
     // variable-length keys: the wave's 64 keys are one contiguous byte range, read into a
     // 4 KiB LDS window with coalesced 16-byte loads and hashed from there (wave_hash_var)
     constexpr uint32_t VCAP = 4096;
-    __shared__ __attribute__((aligned(16))) uint32_t s_vk[PROBE_NT / WAVE][VCAP / 4 + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_vk[NT / WAVE][VCAP / 4 + 4];
     fid[0] = 0xffffffffu;
     h[0] = 0;
     uint64_t o0 = 0, o1 = 0;
@@ -2817,7 +2826,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
 #pragma unroll
   for (int q = 0; q < PPL; q++) {
     if constexpr (WAVE_KEYS || WAVE_VAR) break;
-    const uint64_t i = i0 + (uint64_t)q * PROBE_NT;
+    const uint64_t i = i0 + (uint64_t)q * NT;
     fid[q] = 0xffffffffu;
     h[q] = 0;
     if (i < n) {
@@ -2876,7 +2885,7 @@ __global__ __launch_bounds__(PROBE_NT) void k_probe(const uint4* __restrict__ pp
   }
 #pragma unroll
   for (int q = 0; q < PPL; q++) {
-    const uint64_t i = i0 + (uint64_t)q * PROBE_NT;
+    const uint64_t i = i0 + (uint64_t)q * NT;
     if (i >= n) continue;
     uint64_t r = 0;
     if (pp[q].w) {
@@ -3144,7 +3153,8 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
 #else
   const int ppl = PROBE_PPL;
 #endif
-  dim3 g((uint32_t)((n + PROBE_NT * ppl - 1) / (PROBE_NT * ppl))), b(PROBE_NT);
+  const int nt = probe_nt(kind);
+  dim3 g((uint32_t)((n + (uint64_t)nt * ppl - 1) / ((uint64_t)nt * ppl))), b(nt);
   REC(EV_P_START);
 #define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, a.wave_tab, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
 #if RF_DIAG
