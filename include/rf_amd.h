@@ -108,23 +108,50 @@ int rf_amd_batch_probe_keys_runs(rf_amd_batch *b, const void *d_keys, uint32_t k
 int rf_amd_batch_probe_hashes_runs(rf_amd_batch *b, const uint32_t *d_hashes, const uint64_t *h_counts,
                                    uint64_t *d_found, void *stream);
 
-/* Host-buffer forms (synchronous; inputs staged through the engine's pinned buffer), for
- * callers that hold no device memory, e.g. the routing_filter.h shim
- * (shim/routing_filter_amd.c): build batch b from its keys_total host hashes, and probe n
- * host hashes (filter h_filter_id[i], or filter 0 when NULL) into h_found. */
+/* Host-buffer forms (synchronous), for callers that hold no device memory, e.g. the
+ * routing_filter.h shim (shim/routing_filter_amd.c): build batch b from its keys_total host
+ * hashes (staged through the engine's pinned buffer, on the engine stream), and probe n host
+ * hashes (filter h_filter_id[i], or filter 0 when NULL; ids >= the batch's filters find
+ * nothing) into h_found.
+ * Lookups (this and the two calls below) are ONE kernel launch per call on one of the
+ * engine's lookup slots (own stream, pinned device-mapped buffers, a completion word the
+ * host polls): small calls are read by the kernel straight from pinned host memory, large
+ * ones copied in once; results are written by the kernel into pinned host memory. They are
+ * thread-safe and concurrent callers run concurrently. Batches must be built (a build issued
+ * on the engine stream is waited for). */
 int rf_amd_batch_build_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes);
 int rf_amd_batch_probe_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes, const uint32_t *h_filter_id,
                                    uint64_t n, uint64_t *h_found);
-/* lookups against many resident filters in ONE round trip (one H2D, a probe per group, one
- * D2H, one synchronisation): group g probes counts[g] consecutive hashes of h_hashes against
- * filter filter_index[g] (NULL: 0) of batches[g]. The batch form of trunk_merge_lookup's
- * per-bundle routing_filter_lookup calls (src/trunk.c:6008-6075; routing_filter.h:87-92) and
- * of routing_filter_lookup_async states (:130-155) flushed together. */
+/* lookups against many resident filters -- of any batches of the engine -- in ONE launch:
+ * probe i looks up h_hashes[i] in filter filter_index[g] (NULL: 0) of batches[g], where
+ * g = h_group[i] (NULL: 0); g >= num_groups finds nothing. The form of a flush of queued
+ * routing_filter_lookup_async states (src/routing_filter.h:130-155) and of trunk_merge_lookup's
+ * per-bundle routing_filter_lookup calls (src/trunk.c:6008-6075; routing_filter.h:87-92)
+ * gathered together. All groups share fingerprint_size and log_index_size. */
+int rf_amd_probe_filters_host(rf_amd_engine *e, rf_amd_batch *const *batches, const uint32_t *filter_index,
+                              uint32_t num_groups, const uint32_t *h_hashes, const uint32_t *h_group,
+                              uint64_t n, uint64_t *h_found);
+/* the same with the probes grouped: group g probes counts[g] consecutive hashes */
 int rf_amd_probe_many_hashes_host(rf_amd_engine *e, rf_amd_batch *const *batches,
                                   const uint32_t *filter_index, const uint64_t *counts,
                                   uint32_t num_groups, const uint32_t *h_hashes, uint64_t *h_found);
-/* device-allocation pool of the engine (batch work buffers are recycled across batches) */
+/* device-allocation pool of the engine (batch work buffers are recycled across batches; up
+ * to RF_AMD_POOL_MIB MiB stay pooled, by default a quarter of the device memory free at
+ * engine creation and at most 16 GiB); trim hands pooled blocks back to the device until at
+ * most keep_bytes stay pooled */
 int rf_amd_engine_pool_stats(rf_amd_engine *e, uint64_t *pooled_bytes, uint64_t *hits, uint64_t *misses);
+int rf_amd_engine_pool_trim(rf_amd_engine *e, uint64_t keep_bytes);
+/* the engine's stream (NULL-stream arguments, host-buffer builds and imports run there) and
+ * its synchronisation (only that stream, not the device) */
+void *rf_amd_engine_stream(rf_amd_engine *e);
+int   rf_amd_engine_sync(rf_amd_engine *e);
+/* Residency control for callers that keep many built batches (the shim's registry):
+ * device_bytes = the device memory the batch holds; trim drops its build work buffers,
+ * keeping pages, slots, probe lines and plans (lookups, image reads, estimates and use as an
+ * old filter through an image decode keep working; incremental adds lose the in-place read
+ * of its sorted entries). Stream-ordered on `stream` (NULL = engine's), like destroy_on. */
+uint64_t rf_amd_batch_device_bytes(const rf_amd_batch *b);
+int      rf_amd_batch_trim(rf_amd_batch *b, void *stream);
 
 /* synchronising accessors */
 int rf_amd_batch_info(rf_amd_batch *b, uint32_t f, rf_amd_filter_info *out);

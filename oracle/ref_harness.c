@@ -33,6 +33,7 @@
 #include "splinterdb/default_data_config.h"
 
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <sys/mman.h>
 #include <sys/uio.h>
@@ -532,8 +533,13 @@ rfr_lookup_keys_async_many(rfr_stack      *s,
          found[i] = UINT64_MAX;
       }
    }
+   /* a state can be seen DONE just before its callback runs (on the completing thread):
+      every state that yielded gets exactly one callback, so wait for those */
+   while (__atomic_load_n(&cb, __ATOMIC_ACQUIRE) < *running) {
+      cache_cleanup((cache *)&s->cc);
+   }
    free(st);
-   return cb;
+   return __atomic_load_n(&cb, __ATOMIC_ACQUIRE);
 }
 
 /* the shim's flush counters (weak: absent from the reference's own library) */
@@ -549,6 +555,97 @@ rfr_async_stats(uint64 *batches, uint64 *probes)
    }
    routing_filter_amd_async_stats(batches, probes);
    return 1;
+}
+
+/* the shim's other counters and knobs (weak: absent from the reference's own library) */
+__attribute__((weak)) void
+routing_filter_amd_add_stats(uint64 *batches, uint64 *filters);
+__attribute__((weak)) void
+routing_filter_amd_registry_stats(uint64 *bytes, uint64 *evictions, uint64 *trims);
+__attribute__((weak)) void
+routing_filter_amd_async_config(uint64 batch, uint64 window_us);
+__attribute__((weak)) void
+routing_filter_amd_flush(void);
+__attribute__((weak)) void
+routing_filter_amd_registry_set_limit(uint64 mib);
+
+int
+rfr_registry_set_limit(uint64 mib)
+{
+   if (!routing_filter_amd_registry_set_limit) {
+      return 0;
+   }
+   routing_filter_amd_registry_set_limit(mib);
+   return 1;
+}
+
+/* out[0..4] = add batches, filters added, registry bytes, evictions, trims; 0 without a shim */
+int
+rfr_shim_stats(uint64 *out)
+{
+   memset(out, 0, 5 * sizeof(uint64));
+   if (!routing_filter_amd_add_stats) {
+      return 0;
+   }
+   routing_filter_amd_add_stats(&out[0], &out[1]);
+   routing_filter_amd_registry_stats(&out[2], &out[3], &out[4]);
+   return 1;
+}
+
+int
+rfr_async_config(uint64 batch, uint64 window_us)
+{
+   if (!routing_filter_amd_async_config) {
+      return 0;
+   }
+   routing_filter_amd_async_config(batch, window_us);
+   return 1;
+}
+
+int
+rfr_async_flush(void)
+{
+   if (!routing_filter_amd_flush) {
+      return 0;
+   }
+   routing_filter_amd_flush();
+   return 1;
+}
+
+/*
+ * n routing_filter_lookup_async states, each started once (first call) and left queued;
+ * then routing_filter_amd_flush() answers them all, and each must then be DONE on its next
+ * call with its callback fired exactly once. For the "one launch per flush" check: the
+ * caller sets the shim's completion thread to a batch and window it cannot reach first.
+ * Returns callbacks fired, or UINT64_MAX if a state was not done after the flush.
+ */
+uint64
+rfr_lookup_keys_async_flush(rfr_stack      *s,
+                            routing_filter *filters,
+                            const uint32   *filter_id,
+                            const uint8    *keys,
+                            uint32          key_len,
+                            uint64          n,
+                            uint64         *found)
+{
+   routing_filter_lookup_async_state *st = calloc(n ? n : 1, sizeof(*st));
+   uint64                             cb = 0;
+   for (uint64 i = 0; i < n; i++) {
+      key k = key_create(FALSE, key_len, keys + i * key_len);
+      routing_filter_lookup_async_state_init(&st[i], (cache *)&s->cc, &s->rcfg,
+                                             filters[filter_id ? filter_id[i] : 0], k, &found[i],
+                                             count_callback, &cb);
+      routing_filter_lookup_async(&st[i]);
+   }
+   rfr_async_flush();
+   uint64 ret = 0;
+   for (uint64 i = 0; i < n; i++) {
+      if (routing_filter_lookup_async(&st[i]) != ASYNC_STATUS_DONE) {
+         ret = UINT64_MAX;
+      }
+   }
+   free(st);
+   return ret ? ret : __atomic_load_n(&cb, __ATOMIC_ACQUIRE);
 }
 
 /* the shim's batched lookups (weak: absent from the reference's own library) */
@@ -894,4 +991,313 @@ rfr_bench_chain(rfr_stack      *s,
    b.keep    = keep;
    double t  = run_threads(&b, threads, chain_worker);
    return atomic_load(&b.err) ? -1.0 : t;
+}
+
+/* ---- the stack's pieces, for units that call the reference's own test bodies ------------- */
+cache *
+rfr_cache(rfr_stack *s)
+{
+   return (cache *)&s->cc;
+}
+
+routing_config *
+rfr_routing_config(rfr_stack *s)
+{
+   return &s->rcfg;
+}
+
+platform_heap_id
+rfr_heap(rfr_stack *s)
+{
+   return s->hid;
+}
+
+/* platform_default_log into a file for the duration of a test body (one at a time) */
+static FILE                *g_log_file;
+static platform_log_handle *g_log_saved;
+
+int
+rfr_log_begin(const char *log_path)
+{
+   g_log_file = fopen(log_path, "w");
+   if (!g_log_file) {
+      return -1;
+   }
+   g_log_saved = platform_get_stdout_stream();
+   platform_set_log_streams(g_log_file, stderr);
+   return 0;
+}
+
+void
+rfr_log_end(void)
+{
+   fflush(g_log_file);
+   platform_set_log_streams(g_log_saved, stderr);
+   fclose(g_log_file);
+   g_log_file = NULL;
+}
+
+/* ---- callback-driven async lookups, as tests/functional/test_async.c drives them --------- */
+/*
+ * A pool of max_inflight contexts (test_async.c:20-106: avail_q / ready_q). Each key is
+ * submitted on a free context with a callback that moves the context to the ready queue
+ * (test_async_callback, :25-30); a context is called again ONLY after its callback fired
+ * (async_ctxt_process_ready, :168-196). A state whose call returns DONE is finished and its
+ * context reused. Protocol violations are counted in stats[3]: a callback for a context not
+ * waiting, a state both called back and returned DONE by the same call, a state called back
+ * whose next call does not return DONE, or more than one callback per submission.
+ * stats: [0] first calls that returned RUNNING, [1] callbacks, [2] lookups finished,
+ * [3] violations. Returns 0, or -1 when no progress was made for timeout_s seconds (a state
+ * whose callback never fires).
+ */
+typedef struct rfr_actx {
+   routing_filter_lookup_async_state st;
+   uint64                            i;
+   _Atomic uint32                    cbs;   /* callbacks of the current submission */
+   _Atomic int                       phase; /* 0 free, 1 submitted */
+   struct rfr_actx                  *next;
+   struct rfr_adrive                *d;
+} rfr_actx;
+
+typedef struct rfr_adrive {
+   pthread_mutex_t mu;
+   rfr_actx       *ready;
+   _Atomic uint64  callbacks, violations;
+} rfr_adrive;
+
+static void
+actx_callback(void *arg)
+{
+   rfr_actx   *c = arg;
+   rfr_adrive *d = c->d;
+   atomic_fetch_add(&d->callbacks, 1);
+   if (atomic_fetch_add(&c->cbs, 1) != 0 || atomic_load(&c->phase) != 1) {
+      atomic_fetch_add(&d->violations, 1);
+      return;
+   }
+   pthread_mutex_lock(&d->mu);
+   c->next  = d->ready;
+   d->ready = c;
+   pthread_mutex_unlock(&d->mu);
+}
+
+int
+rfr_lookup_keys_async_driven(rfr_stack      *s,
+                             routing_filter *filters,
+                             const uint32   *filter_id,
+                             const uint8    *keys,
+                             uint32          key_len,
+                             uint64          n,
+                             uint64         *found,
+                             uint32          max_inflight,
+                             uint64         *stats,
+                             double          timeout_s)
+{
+   rfr_adrive d;
+   pthread_mutex_init(&d.mu, NULL);
+   d.ready = NULL;
+   atomic_store(&d.callbacks, 0);
+   atomic_store(&d.violations, 0);
+   rfr_actx *ctx   = calloc(max_inflight, sizeof(*ctx));
+   rfr_actx *avail = NULL;
+   for (uint32 k = 0; k < max_inflight; k++) {
+      ctx[k].d    = &d;
+      ctx[k].next = avail;
+      avail       = &ctx[k];
+   }
+   uint64 next = 0, done = 0, running = 0;
+   double last = now_s();
+   int    ret  = 0;
+#define FINISH(c)                                                                              \
+   do {                                                                                        \
+      found[(c)->i] = SUCCESS((c)->st.__async_result) ? found[(c)->i] : UINT64_MAX;            \
+      atomic_store(&(c)->phase, 0);                                                            \
+      (c)->next = avail;                                                                       \
+      avail     = (c);                                                                         \
+      done++;                                                                                  \
+      last = now_s();                                                                          \
+   } while (0)
+   while (done < n) {
+      while (avail && next < n) {
+         rfr_actx *c = avail;
+         avail       = c->next;
+         c->i        = next++;
+         atomic_store(&c->cbs, 0);
+         atomic_store(&c->phase, 1);
+         key k = key_create(FALSE, key_len, keys + c->i * key_len);
+         routing_filter_lookup_async_state_init(&c->st, (cache *)&s->cc, &s->rcfg,
+                                                filters[filter_id ? filter_id[c->i] : 0], k,
+                                                &found[c->i], actx_callback, c);
+         if (routing_filter_lookup_async(&c->st) == ASYNC_STATUS_DONE) {
+            /* done without waiting: no callback may fire for it */
+            if (atomic_load(&c->cbs) != 0) {
+               atomic_fetch_add(&d.violations, 1);
+            }
+            FINISH(c);
+         } else {
+            running++;
+         }
+      }
+      pthread_mutex_lock(&d.mu);
+      rfr_actx *r = d.ready;
+      d.ready     = NULL;
+      pthread_mutex_unlock(&d.mu);
+      while (r) {
+         rfr_actx *c = r;
+         r           = r->next;
+         if (routing_filter_lookup_async(&c->st) == ASYNC_STATUS_DONE) {
+            FINISH(c);
+         } else {
+            atomic_fetch_add(&d.violations, 1); /* called back, yet not resumable */
+         }
+      }
+      if (done < n && now_s() - last > timeout_s) {
+         ret = -1;
+         break;
+      }
+      cache_cleanup((cache *)&s->cc);
+   }
+#undef FINISH
+   /* every callback owed has fired before the contexts go away */
+   double t0 = now_s();
+   while (atomic_load(&d.callbacks) < running && now_s() - t0 < timeout_s) {
+      sched_yield();
+   }
+   stats[0] = running;
+   stats[1] = atomic_load(&d.callbacks);
+   stats[2] = done;
+   stats[3] = atomic_load(&d.violations);
+   if (ret == 0 && stats[1] < running) {
+      ret = -1;
+   }
+   if (ret == 0) {
+      free(ctx);
+   } /* else leak the contexts: a late callback may still write them */
+   pthread_mutex_destroy(&d.mu);
+   return ret;
+}
+
+/* ---- many threads at once: adds (incremental chains) and lookups ------------------------- */
+/*
+ * threads x rounds chains, as SplinterDB's TASK_TYPE_NORMAL workers compact different
+ * branches at the same time (src/trunk.c:3932, :4168): thread t builds chain t -- round r
+ * hashes keys[(t * rounds + r) * n ...] with data_key_hash and routing_filter_add's them
+ * onto round r - 1 under value r -- keeping every filter in out[t * rounds + r]. Then each
+ * thread looks up its nprobe probe keys (probe + t * nprobe * key_len) in its last filter,
+ * synchronously (found_sync) and through routing_filter_lookup_async states it polls
+ * (found_async). Threads start together; add_s[t] = thread t's time for its adds.
+ * Returns 0, or the first failing status.
+ */
+typedef struct rfr_mt {
+   rfr_stack       *s;
+   const uint8     *keys;
+   const uint8     *probe;
+   uint32           key_len, threads, rounds;
+   uint64           n, nprobe;
+   routing_filter  *out;
+   uint64          *found_sync, *found_async;
+   double          *add_s;
+   _Atomic uint32   next_tid, arrived;
+   _Atomic int      err;
+} rfr_mt;
+
+static void *
+mt_worker(void *arg)
+{
+   rfr_mt      *m = arg;
+   const uint32 t = atomic_fetch_add(&m->next_tid, 1);
+   platform_register_thread();
+   uint32 *fps = malloc(sizeof(uint32) * (m->n ? m->n : 1));
+   atomic_fetch_add(&m->arrived, 1);
+   while (atomic_load(&m->arrived) < m->threads) {
+      sched_yield();
+   }
+   double t0 = now_s();
+   for (uint32 r = 0; r < m->rounds; r++) {
+      const uint8 *kb = m->keys + ((uint64)t * m->rounds + r) * m->n * m->key_len;
+      for (uint64 j = 0; j < m->n; j++) {
+         fps[j] = data_key_hash(&m->s->data_cfg, key_create(FALSE, m->key_len, kb + j * m->key_len),
+                                m->s->rcfg.seed);
+      }
+      routing_filter  empty = NULL_ROUTING_FILTER;
+      routing_filter *old   = r ? &m->out[(uint64)t * m->rounds + r - 1] : &empty;
+      platform_status rc    = routing_filter_add((cache *)&m->s->cc, &m->s->rcfg, old,
+                                              &m->out[(uint64)t * m->rounds + r], fps, m->n, (uint16)r);
+      if (!SUCCESS(rc)) {
+         atomic_store(&m->err, rc.r);
+         break;
+      }
+   }
+   m->add_s[t] = now_s() - t0;
+   free(fps);
+   if (atomic_load(&m->err) == 0) {
+      routing_filter *last = &m->out[(uint64)t * m->rounds + m->rounds - 1];
+      const uint8    *pb   = m->probe + (uint64)t * m->nprobe * m->key_len;
+      uint64         *fs   = m->found_sync + (uint64)t * m->nprobe;
+      uint64         *fa   = m->found_async + (uint64)t * m->nprobe;
+      for (uint64 i = 0; i < m->nprobe; i++) {
+         key             k  = key_create(FALSE, m->key_len, pb + i * m->key_len);
+         platform_status rc = routing_filter_lookup((cache *)&m->s->cc, &m->s->rcfg, last, k, &fs[i]);
+         if (!SUCCESS(rc)) {
+            fs[i] = UINT64_MAX;
+         }
+      }
+      routing_filter_lookup_async_state *st = calloc(m->nprobe ? m->nprobe : 1, sizeof(*st));
+      for (uint64 i = 0; i < m->nprobe; i++) {
+         key k = key_create(FALSE, m->key_len, pb + i * m->key_len);
+         routing_filter_lookup_async_state_init(&st[i], (cache *)&m->s->cc, &m->s->rcfg, *last, k,
+                                                &fa[i], NULL, NULL);
+         routing_filter_lookup_async(&st[i]);
+      }
+      for (uint64 i = 0; i < m->nprobe; i++) {
+         while (routing_filter_lookup_async(&st[i]) != ASYNC_STATUS_DONE) {
+            cache_cleanup((cache *)&m->s->cc);
+         }
+         if (!SUCCESS(st[i].__async_result)) {
+            fa[i] = UINT64_MAX;
+         }
+      }
+      free(st);
+   }
+   platform_deregister_thread();
+   return NULL;
+}
+
+int
+rfr_mt_chains(rfr_stack      *s,
+              const uint8    *keys,
+              uint32          key_len,
+              uint32          threads,
+              uint32          rounds,
+              uint64          n,
+              const uint8    *probe,
+              uint64          nprobe,
+              routing_filter *out,
+              uint64         *found_sync,
+              uint64         *found_async,
+              double         *add_s)
+{
+   rfr_mt m;
+   memset(&m, 0, sizeof(m));
+   m.s           = s;
+   m.keys        = keys;
+   m.probe       = probe;
+   m.key_len     = key_len;
+   m.threads     = threads;
+   m.rounds      = rounds;
+   m.n           = n;
+   m.nprobe      = nprobe;
+   m.out         = out;
+   m.found_sync  = found_sync;
+   m.found_async = found_async;
+   m.add_s       = add_s;
+   pthread_t *th = malloc(sizeof(pthread_t) * threads);
+   for (uint32 t = 0; t < threads; t++) {
+      pthread_create(&th[t], NULL, mt_worker, &m);
+   }
+   for (uint32 t = 0; t < threads; t++) {
+      pthread_join(th[t], NULL);
+   }
+   free(th);
+   return atomic_load(&m.err);
 }

@@ -18,6 +18,10 @@ LIB_PATH = os.path.join(HERE, "_ref", "libref_rf.so")
 # the same harness and page stack with shim/routing_filter_amd.c (the MI355X drop-in) in
 # place of routing_filter.c
 SHIM_PATH = os.path.join(HERE, "_ref", "libshim_rf.so")
+# each of the two stacks with the reference's tests/functional/filter_test.c test bodies
+# (oracle/ref_filter_test.c #includes it unmodified)
+FT_REF_PATH = os.path.join(HERE, "_ref", "libfilter_test_ref.so")
+FT_SHIM_PATH = os.path.join(HERE, "_ref", "libfilter_test_shim.so")
 
 
 class RoutingFilter(ctypes.Structure):
@@ -94,6 +98,23 @@ def lib(path=LIB_PATH):
         L.rfr_print.restype = None
         L.rfr_read_page.argtypes = [vp, u64, vp]
         L.rfr_read_page.restype = None
+        L.rfr_lookup_keys_async_driven.argtypes = [vp, vp, vp, vp, u32, u64, vp, u32, vp, ctypes.c_double]
+        L.rfr_lookup_keys_async_driven.restype = i32
+        L.rfr_mt_chains.argtypes = [vp, vp, u32, u32, u32, u64, vp, u64, vp, vp, vp, vp]
+        L.rfr_mt_chains.restype = i32
+        L.rfr_shim_stats.argtypes = [vp]
+        L.rfr_shim_stats.restype = i32
+        L.rfr_registry_set_limit.argtypes = [u64]
+        L.rfr_registry_set_limit.restype = i32
+        L.rfr_async_config.argtypes = [u64, u64]
+        L.rfr_async_config.restype = i32
+        L.rfr_lookup_keys_async_flush.argtypes = [vp, vp, vp, vp, u32, u64, vp]
+        L.rfr_lookup_keys_async_flush.restype = u64
+        if hasattr(L, "rfr_filter_test_basic"):  # the filter_test libraries only
+            L.rfr_filter_test_basic.argtypes = [vp, u64, u64, u64, ctypes.c_char_p]
+            L.rfr_filter_test_basic.restype = i32
+            L.rfr_filter_test_perf.argtypes = [vp, u64, u64, u64, u64, ctypes.c_char_p]
+            L.rfr_filter_test_perf.restype = i32
         _libs[path] = L
     return _libs[path]
 
@@ -316,6 +337,85 @@ class Stack:
 
     def dec_ref(self, desc):
         self.L.rfr_dec_ref(self.h, ctypes.byref(desc))
+
+    def lookup_keys_async_driven(self, descs, keys, filter_id=None, key_len=24, max_inflight=64, timeout_s=30.0):
+        """len(keys) routing_filter_lookup_async lookups driven by callbacks as
+        tests/functional/test_async.c drives them (a state is called again only after its
+        callback fired; oracle/ref_harness.c rfr_lookup_keys_async_driven). Returns (found,
+        stats) with stats = {running, callbacks, done, violations}; raises on a stall."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = k.size // key_len
+        arr = (RoutingFilter * max(1, len(descs)))(*descs)
+        fid = None if filter_id is None else np.ascontiguousarray(filter_id, dtype=np.uint32)
+        out = np.zeros(n, dtype=np.uint64)
+        st = np.zeros(4, dtype=np.uint64)
+        r = self.L.rfr_lookup_keys_async_driven(self.h, ctypes.addressof(arr), None if fid is None else _p(fid),
+                                                _p(k), key_len, n, _p(out), max_inflight, _p(st), timeout_s)
+        stats = dict(zip(("running", "callbacks", "done", "violations"), (int(x) for x in st)))
+        if r:
+            raise RuntimeError(f"async lookups stalled: {stats}")
+        return out, stats
+
+    def lookup_keys_async_flush(self, descs, keys, filter_id=None, key_len=24):
+        """every state started once, then one routing_filter_amd_flush(); returns (found,
+        callbacks) -- callbacks None if a state was not done after the flush"""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = k.size // key_len
+        arr = (RoutingFilter * max(1, len(descs)))(*descs)
+        fid = None if filter_id is None else np.ascontiguousarray(filter_id, dtype=np.uint32)
+        out = np.zeros(n, dtype=np.uint64)
+        cb = self.L.rfr_lookup_keys_async_flush(self.h, ctypes.addressof(arr), None if fid is None else _p(fid),
+                                                _p(k), key_len, n, _p(out))
+        return out, (None if cb == (1 << 64) - 1 else int(cb))
+
+    def mt_chains(self, keys, threads, rounds, n, probe, nprobe, key_len=24):
+        """threads x rounds incremental chains built by `threads` concurrent threads
+        (oracle/ref_harness.c rfr_mt_chains), then each thread's nprobe lookups of its probe
+        keys, synchronous and async. Returns (filters [threads][rounds], found_sync,
+        found_async, per-thread add seconds)."""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        p = np.ascontiguousarray(probe, dtype=np.uint8).reshape(-1)
+        out = (RoutingFilter * (threads * rounds))()
+        fs = np.zeros(threads * nprobe, dtype=np.uint64)
+        fa = np.zeros(threads * nprobe, dtype=np.uint64)
+        add_s = np.zeros(threads, dtype=np.float64)
+        rc = self.L.rfr_mt_chains(self.h, _p(k), key_len, threads, rounds, n, _p(p), nprobe, out, _p(fs), _p(fa),
+                                  _p(add_s))
+        if rc:
+            raise RuntimeError(f"concurrent routing_filter_add: platform_status {rc}")
+        return [[out[t * rounds + r] for r in range(rounds)] for t in range(threads)], fs, fa, add_s
+
+    def shim_stats(self):
+        """the shim's add batches / filters, registry bytes / evictions / trims (None for
+        the reference's library)"""
+        out = np.zeros(5, dtype=np.uint64)
+        if not self.L.rfr_shim_stats(_p(out)):
+            return None
+        return dict(zip(("add_batches", "add_filters", "registry_bytes", "evictions", "trims"), (int(x) for x in out)))
+
+    def registry_set_limit(self, mib):
+        return bool(self.L.rfr_registry_set_limit(mib))
+
+    def async_config(self, batch, window_us):
+        return bool(self.L.rfr_async_config(batch, window_us))
+
+    def filter_test_basic(self, num_fingerprints, num_values, key_size=24):
+        """the reference's test_filter_basic (tests/functional/filter_test.c:22-148) on this
+        stack; returns (platform_status, its log text)"""
+        return self._filter_test(lambda path: self.L.rfr_filter_test_basic(
+            self.h, key_size, num_fingerprints, num_values, path))
+
+    def filter_test_perf(self, num_fingerprints, num_values, num_trees, key_size=24):
+        """the reference's test_filter_perf (filter_test.c:150-273); (status, log text)"""
+        return self._filter_test(lambda path: self.L.rfr_filter_test_perf(
+            self.h, key_size, num_fingerprints, num_values, num_trees, path))
+
+    def _filter_test(self, run):
+        import tempfile
+        with tempfile.NamedTemporaryFile(suffix=".log") as tmp:
+            rc = run(tmp.name.encode())
+            with open(tmp.name) as f:
+                return int(rc), f.read()
 
 
 def get_next_value(found_values, last_value):

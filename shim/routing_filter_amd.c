@@ -6,12 +6,13 @@
  * function routing_filter.h declares, with the reference's signatures, and runs the filter
  * work on the MI355X engine through its C ABI (include/rf_amd.h, librf_amd.so):
  *
- *   routing_filter_add                  routing_filter.h:78-85   build on the GPU, then the
- *                                        reference's page allocation sequence, page by page
+ *   routing_filter_add                  routing_filter.h:78-85   build on the GPU (concurrent
+ *                                        calls coalesced into one batch), then the reference's
+ *                                        page allocation sequence, page by page
  *   routing_filter_lookup               :87-92     hash via data_config (the application's
- *                                        callback, as the reference), probe on the GPU
- *   routing_filter_lookup_async         :130-155   per-key coroutine states coalesced into
- *                                        one GPU probe per filter (see "async" below)
+ *                                        callback, as the reference), one GPU round trip
+ *   routing_filter_lookup_async         :130-155   states queued and probed together, many
+ *                                        filters per launch (see "async" below)
  *   routing_filter_inc_ref / _dec_ref   :157-162   the reference's mini_allocator refcounts
  *   routing_filter_estimate_unique_*    :163-175   GPU decode + distinct count
  *   routing_filter_space_use_bytes      :177-178   mini_space_use_bytes
@@ -26,7 +27,8 @@
  * cache/allocator state the filter descriptor (addr, meta_head, num_fingerprints,
  * num_unique, value_size) and every written page byte equal the reference's; bytes the
  * reference leaves untouched on a data page are zero here (they are zero on a fresh cache
- * page there, SURVEY finding 4).
+ * page there, SURVEY finding 4). Each thread's allocation runs in its own call, in the
+ * reference's order, after the shared GPU build.
  *
  * Differences a caller can see: new_fp_arr is not shifted/sorted in place (no caller reads
  * it afterwards; the trunk frees it, src/trunk.c:2825-2826); inputs the reference treats as
@@ -34,18 +36,35 @@
  * STATUS_BAD_PARAM instead of corrupting memory; without a HIP device every call that needs
  * one returns ENODEV (there is no CPU fallback).
  *
- * Device residency. Each filter this process builds stays on the GPU (a probe-only batch:
- * pages, slots, probe lines) in a registry keyed by (cache, index-extent address), so lookups
- * and later incremental adds never re-read it; a filter not in the registry (built before
- * a restart) is read back through cache_get once and imported. dec_ref drops the device
- * copy when the reference's refcount reaches zero.
+ * Concurrent adds. SplinterDB calls routing_filter_add from many TASK_TYPE_NORMAL workers at
+ * once (src/trunk.c:3932, :4168). The first caller to find the engine idle becomes the
+ * combiner: it takes every add queued so far -- its own and those that arrived while the
+ * previous batch was building -- builds them as ONE multi-filter batch (rf_amd_batch_create
+ * with F filters), reads each image back and hands it to its caller, which then allocates
+ * its pages in the reference's order. No artificial wait: under load, batches form by
+ * themselves; a lone caller builds alone.
+ *
+ * Device residency. Each filter this process builds stays on the GPU -- its whole batch, so a
+ * later incremental add onto it reads the old entries in place instead of decoding the image
+ * -- in a registry keyed by (cache, index-extent address); lookups never re-read it. A
+ * filter not in the registry (built before a restart, or evicted) is read back through
+ * cache_get once and imported. The registry is bounded (RF_AMD_REGISTRY_MIB, default 32 GiB
+ * of device memory): past the bound the least recently used batches are first trimmed to
+ * their probe-only state, then evicted; batches in use by a running call are pinned and
+ * never released under it. dec_ref drops the device copy when the reference's refcount
+ * reaches zero.
  *
  * async. routing_filter_lookup_async's first call on a state hashes the key, queues the
- * state and returns ASYNC_STATUS_RUNNING. The queue is flushed -- one GPU probe per filter
- * for all queued states -- when it reaches RF_SHIM_ASYNC_BATCH states (default 1024), when
- * routing_filter_amd_flush() is called, or when a queued state is called again (its owner
- * is waiting). A flush stores each state's found_values, marks it done, and calls its
- * callback(callback_arg); its next call returns ASYNC_STATUS_DONE with STATUS_OK.
+ * state and returns ASYNC_STATUS_RUNNING without touching the state again (async.h:115-125:
+ * it may be completed on another thread at once). A completion thread probes the queued
+ * states -- ONE GPU launch for every filter they name -- when RF_SHIM_ASYNC_BATCH states
+ * (default 1024) are queued or the oldest has waited RF_SHIM_ASYNC_WINDOW_US (default 20 us),
+ * so every state completes without being called again. Completion stores found_values and
+ * the result, marks the state done, then calls its callback(callback_arg) -- from the
+ * completion thread, registered with the platform like any SplinterDB thread -- and the
+ * state's next call returns ASYNC_STATUS_DONE. A state called again while still queued (a
+ * polling owner) probes the queue in its own thread and returns ASYNC_STATUS_RUNNING: a call
+ * never both fires its state's callback and returns DONE.
  */
 #include "routing_filter.h"
 #include "mini_allocator.h"
@@ -58,6 +77,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include "rf_amd.h"
 #include "routing_filter_amd.h"
@@ -110,17 +131,59 @@ num_indices_of(const routing_config *cfg, uint32 num_fingerprints)
    return 1u << (lnb - cfg->log_index_size);
 }
 
+static uint64
+now_ns(void)
+{
+   struct timespec ts;
+   clock_gettime(CLOCK_MONOTONIC, &ts);
+   return (uint64)ts.tv_sec * 1000000000ull + (uint64)ts.tv_nsec;
+}
+
+static uint64
+env_u64(const char *name, uint64 dflt)
+{
+   const char *s = getenv(name);
+   return s ? (uint64)atoll(s) : dflt;
+}
+
 /* ---- registry of device-resident filters, keyed by (cache, index-extent address) -------- */
+/* An engine batch shared by the filters built (or imported) together. `entries` counts the
+ * registry entries naming it, `pins` the running calls using it; it is destroyed when both
+ * are zero. Its device bytes count against the registry bound while entries > 0. */
+typedef struct shim_batch {
+   rf_amd_batch *b;
+   uint32        entries;
+   uint32        pins;
+   uint64        bytes;
+   int           full; /* build work buffers kept (entries in place for incremental adds) */
+} shim_batch;
+
 typedef struct resident_filter {
    const cache            *cc;
    uint64                  addr;
-   rf_amd_batch           *batch;
-   struct resident_filter *next;
+   shim_batch             *sb;
+   uint32                  f;
+   struct resident_filter *next;                /* hash chain */
+   struct resident_filter *lru_prev, *lru_next; /* most recently used first */
 } resident_filter;
 
 #define REGISTRY_BUCKETS 4096
 static resident_filter *g_registry[REGISTRY_BUCKETS];
+static resident_filter  g_lru = {.lru_prev = &g_lru, .lru_next = &g_lru};
 static pthread_mutex_t  g_registry_mu = PTHREAD_MUTEX_INITIALIZER;
+static uint64           g_registry_bytes;
+static uint64           g_registry_evictions, g_registry_trims;
+
+static uint64 g_registry_limit; /* bytes; 0 = not yet read from RF_AMD_REGISTRY_MIB */
+
+static uint64
+registry_limit(void)
+{
+   if (!g_registry_limit) {
+      g_registry_limit = env_u64("RF_AMD_REGISTRY_MIB", 32768) << 20;
+   }
+   return g_registry_limit;
+}
 
 static uint64
 registry_bucket(const cache *cc, uint64 addr)
@@ -128,74 +191,252 @@ registry_bucket(const cache *cc, uint64 addr)
    return ((addr >> 12) ^ (uint64)(uintptr_t)cc) * 0x9E3779B97F4A7C15ull >> 52;
 }
 
-static rf_amd_batch *
-registry_find(const cache *cc, uint64 addr)
+static void
+lru_unlink(resident_filter *r)
 {
-   rf_amd_batch *b = NULL;
+   r->lru_prev->lru_next = r->lru_next;
+   r->lru_next->lru_prev = r->lru_prev;
+}
+
+static void
+lru_push_front(resident_filter *r)
+{
+   r->lru_next             = g_lru.lru_next;
+   r->lru_prev             = &g_lru;
+   g_lru.lru_next->lru_prev = r;
+   g_lru.lru_next          = r;
+}
+
+static shim_batch *
+shim_batch_new(rf_amd_batch *b, uint32 pins, int full)
+{
+   shim_batch *sb = malloc(sizeof(*sb));
+   platform_assert(sb != NULL);
+   sb->b       = b;
+   sb->entries = 0;
+   sb->pins    = pins;
+   sb->bytes   = rf_amd_batch_device_bytes(b);
+   sb->full    = full;
+   return sb;
+}
+
+/* releases of batches decided under the registry lock, done after it is dropped */
+typedef struct release_list {
+   shim_batch **sb;
+   uint32       n, cap;
+} release_list;
+
+static void
+release_run(release_list *rl)
+{
+   for (uint32 i = 0; i < rl->n; i++) {
+      rf_amd_batch_destroy_on(rl->sb[i]->b, NULL); /* stream-ordered, no device-wide wait */
+      free(rl->sb[i]);
+   }
+   free(rl->sb);
+   rl->sb = NULL;
+   rl->n = rl->cap = 0;
+}
+
+/* the caller holds g_registry_mu; sb loses one entry or pin */
+static void
+shim_batch_drop_locked(shim_batch *sb, int entry, release_list *rl)
+{
+   if (entry) {
+      platform_assert(sb->entries > 0);
+      if (--sb->entries == 0) {
+         g_registry_bytes -= sb->bytes;
+      }
+   } else {
+      platform_assert(sb->pins > 0);
+      sb->pins--;
+   }
+   if (sb->entries == 0 && sb->pins == 0) {
+      if (rl->n == rl->cap) {
+         rl->cap = rl->cap ? 2 * rl->cap : 8;
+         rl->sb  = realloc(rl->sb, sizeof(*rl->sb) * rl->cap);
+         platform_assert(rl->sb != NULL);
+      }
+      rl->sb[rl->n++] = sb;
+   }
+}
+
+static void
+registry_remove_locked(resident_filter *r, release_list *rl)
+{
+   for (resident_filter **pp = &g_registry[registry_bucket(r->cc, r->addr)]; *pp; pp = &(*pp)->next) {
+      if (*pp == r) {
+         *pp = r->next;
+         break;
+      }
+   }
+   lru_unlink(r);
+   shim_batch *sb = r->sb;
+   free(r);
+   shim_batch_drop_locked(sb, 1, rl);
+}
+
+/* Keeps the registry under its bound: least recently used first, a batch that still holds
+ * its build buffers is trimmed to its probe-only state, then filters are evicted. Pinned
+ * batches are left alone. `keep` (may be NULL) is never evicted. */
+static void
+registry_evict_locked(const resident_filter *keep, uint64 limit, release_list *rl)
+{
+   resident_filter *r = g_lru.lru_prev;
+   while (g_registry_bytes > limit && r != &g_lru) {
+      resident_filter *prev = r->lru_prev;
+      shim_batch      *sb   = r->sb;
+      if (r != keep && sb->pins == 0) {
+         if (sb->full) {
+            rf_amd_batch_trim(sb->b, NULL);
+            const uint64 nb = rf_amd_batch_device_bytes(sb->b);
+            g_registry_bytes -= sb->bytes - nb;
+            sb->bytes = nb;
+            sb->full  = 0;
+            g_registry_trims++;
+         } else {
+            registry_remove_locked(r, rl);
+            g_registry_evictions++;
+         }
+      }
+      r = prev;
+   }
+}
+
+/* the filter's batch and index, pinned (registry_unpin when done), or NULL */
+static shim_batch *
+registry_find_pin(const cache *cc, uint64 addr, uint32 *f)
+{
+   shim_batch *sb = NULL;
    pthread_mutex_lock(&g_registry_mu);
    for (resident_filter *r = g_registry[registry_bucket(cc, addr)]; r; r = r->next) {
       if (r->cc == cc && r->addr == addr) {
-         b = r->batch;
+         sb = r->sb;
+         *f = r->f;
+         sb->pins++;
+         lru_unlink(r);
+         lru_push_front(r);
          break;
       }
    }
    pthread_mutex_unlock(&g_registry_mu);
-   return b;
+   return sb;
+}
+
+static void
+registry_unpin(shim_batch *sb)
+{
+   if (!sb) {
+      return;
+   }
+   release_list rl = {NULL, 0, 0};
+   pthread_mutex_lock(&g_registry_mu);
+   shim_batch_drop_locked(sb, 0, &rl);
+   pthread_mutex_unlock(&g_registry_mu);
+   release_run(&rl);
 }
 
 /*
- * Registers b for (cc, addr). replace = 0 (a filter imported from the cache): an entry
- * present already wins and is returned (the caller destroys b). replace = 1 (a filter just
- * built at addr): any entry there is stale -- its pages were freed and reallocated without
- * our dec_ref seeing it reach zero -- and is destroyed.
+ * Registers filter f of sb for (cc, addr), turning one of the caller's pins into the entry.
+ * replace = 0 (a filter imported from the cache): an entry present already wins; the
+ * caller's pin moves to that entry's batch, which is returned (*f updated). replace = 1 (a
+ * filter just built at addr): any entry there is stale -- its pages were freed and
+ * reallocated without our dec_ref seeing it reach zero -- and is dropped.
  */
-static rf_amd_batch *
-registry_insert(const cache *cc, uint64 addr, rf_amd_batch *b, int replace)
+static shim_batch *
+registry_insert(const cache *cc, uint64 addr, shim_batch *sb, uint32 *f, int replace, int keep_pin)
 {
-   rf_amd_batch *stale = NULL;
+   release_list rl = {NULL, 0, 0};
    pthread_mutex_lock(&g_registry_mu);
    resident_filter **head = &g_registry[registry_bucket(cc, addr)];
    for (resident_filter *r = *head; r; r = r->next) {
       if (r->cc == cc && r->addr == addr) {
          if (!replace) {
-            rf_amd_batch *have = r->batch;
+            shim_batch *have = r->sb;
+            *f               = r->f;
+            have->pins++;
+            shim_batch_drop_locked(sb, 0, &rl); /* ours is not needed */
+            if (!keep_pin) {
+               shim_batch_drop_locked(have, 0, &rl);
+            }
+            lru_unlink(r);
+            lru_push_front(r);
             pthread_mutex_unlock(&g_registry_mu);
+            release_run(&rl);
             return have;
          }
-         stale    = r->batch;
-         r->batch = b;
-         pthread_mutex_unlock(&g_registry_mu);
-         rf_amd_batch_destroy(stale);
-         return b;
+         registry_remove_locked(r, &rl);
+         break;
       }
    }
    resident_filter *r = malloc(sizeof(*r));
    platform_assert(r != NULL);
-   r->cc    = cc;
-   r->addr  = addr;
-   r->batch = b;
-   r->next  = *head;
-   *head    = r;
+   r->cc   = cc;
+   r->addr = addr;
+   r->sb   = sb;
+   r->f    = *f;
+   r->next = *head;
+   *head   = r;
+   lru_push_front(r);
+   if (sb->entries++ == 0) {
+      g_registry_bytes += sb->bytes;
+   }
+   if (!keep_pin) {
+      shim_batch_drop_locked(sb, 0, &rl);
+   }
+   registry_evict_locked(r, registry_limit(), &rl);
    pthread_mutex_unlock(&g_registry_mu);
-   return b;
+   release_run(&rl);
+   return sb;
 }
 
 static void
 registry_drop(const cache *cc, uint64 addr)
 {
-   rf_amd_batch *b = NULL;
+   release_list rl = {NULL, 0, 0};
    pthread_mutex_lock(&g_registry_mu);
-   for (resident_filter **pp = &g_registry[registry_bucket(cc, addr)]; *pp; pp = &(*pp)->next) {
-      if ((*pp)->cc == cc && (*pp)->addr == addr) {
-         resident_filter *r = *pp;
-         *pp                = r->next;
-         b                  = r->batch;
-         free(r);
+   for (resident_filter *r = g_registry[registry_bucket(cc, addr)]; r; r = r->next) {
+      if (r->cc == cc && r->addr == addr) {
+         registry_remove_locked(r, &rl);
          break;
       }
    }
    pthread_mutex_unlock(&g_registry_mu);
-   rf_amd_batch_destroy(b);
+   release_run(&rl);
+}
+
+/* every unpinned filter out (device memory ran out) */
+static void
+registry_evict_all(void)
+{
+   release_list rl = {NULL, 0, 0};
+   pthread_mutex_lock(&g_registry_mu);
+   registry_evict_locked(NULL, 0, &rl);
+   pthread_mutex_unlock(&g_registry_mu);
+   release_run(&rl);
+   rf_amd_engine_sync(engine());
+   rf_amd_engine_pool_trim(engine(), 0);
+}
+
+void
+routing_filter_amd_registry_set_limit(uint64 mib)
+{
+   release_list rl = {NULL, 0, 0};
+   pthread_mutex_lock(&g_registry_mu);
+   g_registry_limit = mib << 20;
+   registry_evict_locked(NULL, g_registry_limit, &rl);
+   pthread_mutex_unlock(&g_registry_mu);
+   release_run(&rl);
+}
+
+void
+routing_filter_amd_registry_stats(uint64 *bytes, uint64 *evictions, uint64 *trims)
+{
+   pthread_mutex_lock(&g_registry_mu);
+   *bytes     = g_registry_bytes;
+   *evictions = g_registry_evictions;
+   *trims     = g_registry_trims;
+   pthread_mutex_unlock(&g_registry_mu);
 }
 
 /* ---- a filter read back through the cache (the image of a filter built elsewhere) ------ */
@@ -266,11 +507,13 @@ rf_read_image(cache                *cc,
    return STATUS_OK;
 }
 
-/* the filter's device-resident probe-only batch (imported from the cache if needed) */
+/* The filter's device-resident batch and index, pinned: from the registry, or imported from
+ * the cache (probe-only). An import that finds the device full evicts the registry and
+ * retries once, so a lookup does not fail while evictable filters hold the memory. */
 static platform_status
-resident(cache *cc, const routing_config *cfg, const routing_filter *f, rf_amd_batch **out)
+resident_pin(cache *cc, const routing_config *cfg, const routing_filter *f, shim_batch **out, uint32 *fi)
 {
-   *out = registry_find(cc, f->addr);
+   *out = registry_find_pin(cc, f->addr, fi);
    if (*out) {
       return STATUS_OK;
    }
@@ -286,14 +529,16 @@ resident(cache *cc, const routing_config *cfg, const routing_filter *f, rf_amd_b
    rf_amd_config c = amd_config(cfg);
    rf_amd_batch *b = NULL;
    int           r = rf_amd_batch_import(e, &c, 1, &img.info, img.pages, img.slots, 0, &b);
+   if (r == RF_AMD_ENOMEM) {
+      registry_evict_all();
+      r = rf_amd_batch_import(e, &c, 1, &img.info, img.pages, img.slots, 0, &b);
+   }
    rf_amd_image_free(&img);
    if (r) {
       return status_of(r);
    }
-   *out = registry_insert(cc, f->addr, b, 0);
-   if (*out != b) {
-      rf_amd_batch_destroy(b);
-   }
+   *fi  = 0;
+   *out = registry_insert(cc, f->addr, shim_batch_new(b, 1, 0), fi, 0, 1);
    return STATUS_OK;
 }
 
@@ -305,7 +550,206 @@ unlock_and_unget_page(cache *cc, page_handle *page)
    cache_unget(cc, page);
 }
 
-/* ---- routing_filter_add --------------------------------------------------------------- */
+/* ---- routing_filter_add: concurrent calls coalesced into one GPU batch ----------------- */
+typedef struct add_req {
+   rf_amd_config      c;
+   shim_batch        *old_sb; /* pinned by the caller, or NULL */
+   uint32             old_f;
+   const uint32      *hashes;
+   uint32             n;
+   uint16             value;
+   /* results */
+   int                rc;
+   rf_amd_filter_info info;
+   uint8             *pages;
+   uint64            *slots;
+   shim_batch        *sb; /* the built batch, pinned once for this request */
+   uint32             f;
+   int                done;
+   struct add_req    *next;
+} add_req;
+
+static pthread_mutex_t g_add_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t  g_add_cv = PTHREAD_COND_INITIALIZER;
+static add_req        *g_add_head, *g_add_tail;
+static int             g_add_busy;
+static uint64          g_add_batches, g_add_filters;
+
+/* builds k requests of one config as one batch; a batch that cannot be created (one
+ * request's geometry, or memory) is retried request by request so each gets its own error */
+static void
+run_adds(rf_amd_engine *e, add_req **rq, uint32 k)
+{
+   uint32        *num_new = malloc(sizeof(uint32) * k);
+   uint16        *value   = malloc(sizeof(uint16) * k);
+   rf_amd_batch **old     = malloc(sizeof(*old) * k);
+   uint32        *old_idx = malloc(sizeof(uint32) * k);
+   platform_assert(num_new && value && old && old_idx);
+   uint64 total = 0;
+   int    any_old = 0;
+   for (uint32 i = 0; i < k; i++) {
+      num_new[i] = rq[i]->n;
+      value[i]   = rq[i]->value;
+      old[i]     = rq[i]->old_sb ? rq[i]->old_sb->b : NULL;
+      old_idx[i] = rq[i]->old_f;
+      any_old |= old[i] != NULL;
+      total += rq[i]->n;
+   }
+   rf_amd_batch *b = NULL;
+   int           r = rf_amd_batch_create(e, &rq[0]->c, k, num_new, value, any_old ? old : NULL,
+                               any_old ? old_idx : NULL, &b);
+   if (r == RF_AMD_ENOMEM) {
+      registry_evict_all();
+      r = rf_amd_batch_create(e, &rq[0]->c, k, num_new, value, any_old ? old : NULL, any_old ? old_idx : NULL, &b);
+   }
+   free(num_new);
+   free(value);
+   free(old);
+   free(old_idx);
+   if (r && k > 1) {
+      for (uint32 i = 0; i < k; i++) {
+         run_adds(e, rq + i, 1);
+      }
+      return;
+   }
+   if (r) {
+      rq[0]->rc = r;
+      return;
+   }
+   uint32 *h = NULL;
+   if (k == 1) {
+      h = (uint32 *)rq[0]->hashes; /* not modified */
+   } else {
+      h = malloc(sizeof(uint32) * (total ? total : 1));
+      platform_assert(h != NULL);
+      uint64 at = 0;
+      for (uint32 i = 0; i < k; i++) {
+         memcpy(h + at, rq[i]->hashes, sizeof(uint32) * rq[i]->n);
+         at += rq[i]->n;
+      }
+   }
+   r = rf_amd_batch_build_hashes_host(b, h);
+   if (k > 1) {
+      free(h);
+   }
+   rf_amd_filter_info *infos = malloc(sizeof(*infos) * k);
+   platform_assert(infos != NULL);
+   if (!r) {
+      r = rf_amd_batch_infos(b, infos, rf_amd_engine_stream(e));
+   }
+   const uint64 ps = rq[0]->c.page_size;
+   for (uint32 i = 0; i < k && !r; i++) {
+      add_req *q = rq[i];
+      q->info    = infos[i];
+      if (q->info.error) {
+         q->rc = RF_AMD_EINVAL; /* a block over a page: undefined behaviour in the reference */
+         continue;
+      }
+      q->pages = malloc(ps * q->info.num_pages + 16);
+      q->slots = malloc(sizeof(uint64) * q->info.num_indices);
+      platform_assert(q->pages && q->slots);
+      r = rf_amd_batch_read_image_async(b, i, q->pages, ps * q->info.num_pages, q->slots,
+                                        q->info.num_indices, NULL);
+   }
+   if (!r) {
+      r = rf_amd_engine_sync(e);
+   }
+   free(infos);
+   if (r) {
+      for (uint32 i = 0; i < k; i++) {
+         rq[i]->rc = r;
+      }
+      rf_amd_batch_destroy_on(b, NULL);
+      return;
+   }
+   uint32 ok = 0;
+   for (uint32 i = 0; i < k; i++) {
+      ok += rq[i]->rc == 0;
+   }
+   if (ok == 0) {
+      rf_amd_batch_destroy_on(b, NULL);
+      return;
+   }
+   shim_batch *sb = shim_batch_new(b, ok, 1);
+   for (uint32 i = 0; i < k; i++) {
+      if (rq[i]->rc == 0) {
+         rq[i]->sb = sb;
+         rq[i]->f  = i;
+      }
+   }
+   __atomic_fetch_add(&g_add_batches, 1, __ATOMIC_RELAXED);
+   __atomic_fetch_add(&g_add_filters, k, __ATOMIC_RELAXED);
+}
+
+/* the combiner's pass over the requests it took: one batch per distinct config */
+static void
+run_add_list(rf_amd_engine *e, add_req *list)
+{
+   uint32 n = 0;
+   for (add_req *q = list; q; q = q->next) {
+      n++;
+   }
+   add_req **rq = malloc(sizeof(*rq) * n);
+   platform_assert(rq != NULL);
+   uint32 m = 0;
+   for (add_req *q = list; q; q = q->next) {
+      rq[m++] = q;
+   }
+   for (uint32 s = 0; s < n;) {
+      uint32 t = s + 1; /* gather the requests sharing rq[s]'s config to the front */
+      for (uint32 i = s + 1; i < n; i++) {
+         if (memcmp(&rq[i]->c, &rq[s]->c, sizeof(rf_amd_config)) == 0) {
+            add_req *x = rq[t];
+            rq[t++]    = rq[i];
+            rq[i]      = x;
+         }
+      }
+      run_adds(e, rq + s, t - s);
+      s = t;
+   }
+   free(rq);
+}
+
+/* queue the request; build it (and whatever else is queued) if the engine is idle, else wait
+ * for the combiner that takes it */
+static void
+add_submit(rf_amd_engine *e, add_req *q)
+{
+   pthread_mutex_lock(&g_add_mu);
+   q->next = NULL;
+   if (g_add_tail) {
+      g_add_tail->next = q;
+   } else {
+      g_add_head = q;
+   }
+   g_add_tail = q;
+   while (!q->done) {
+      if (!g_add_busy) {
+         g_add_busy    = 1;
+         add_req *list = g_add_head;
+         g_add_head = g_add_tail = NULL;
+         pthread_mutex_unlock(&g_add_mu);
+         run_add_list(e, list);
+         pthread_mutex_lock(&g_add_mu);
+         for (add_req *x = list; x; x = x->next) {
+            x->done = 1;
+         }
+         g_add_busy = 0;
+         pthread_cond_broadcast(&g_add_cv);
+      } else {
+         pthread_cond_wait(&g_add_cv, &g_add_mu);
+      }
+   }
+   pthread_mutex_unlock(&g_add_mu);
+}
+
+void
+routing_filter_amd_add_stats(uint64 *batches, uint64 *filters)
+{
+   *batches = __atomic_load_n(&g_add_batches, __ATOMIC_RELAXED);
+   *filters = __atomic_load_n(&g_add_filters, __ATOMIC_RELAXED);
+}
+
 platform_status
 routing_filter_add(cache                *cc,
                    const routing_config *cfg,
@@ -324,54 +768,38 @@ routing_filter_add(cache                *cc,
    if (nfp == 0 || nfp > routing_filter_max_fingerprints(cfg->cache_cfg, cfg)) {
       return STATUS_BAD_PARAM; /* the reference: __builtin_clz(0) / index-extent overflow */
    }
-   rf_amd_batch  *ob = NULL;
-   platform_status rc;
+   add_req q;
+   memset(&q, 0, sizeof(q));
+   q.c      = amd_config(cfg);
+   q.hashes = new_fp_arr;
+   q.n      = (uint32)num_new_fp;
+   q.value  = value;
    if (old_filter->addr != 0) {
       mini_prefetch(cc, PAGE_TYPE_FILTER, old_filter->meta_head); /* as :356 */
-      rc = resident(cc, cfg, old_filter, &ob);
+      platform_status rc = resident_pin(cc, cfg, old_filter, &q.old_sb, &q.old_f);
       if (!SUCCESS(rc)) {
          return rc;
       }
    }
 
-   /* the image, on the GPU */
-   rf_amd_config c    = amd_config(cfg);
-   uint32        n32  = (uint32)num_new_fp;
-   uint32        zero = 0;
-   rf_amd_batch *b    = NULL;
-   int           r    = rf_amd_batch_create(e, &c, 1, &n32, &value, ob ? &ob : NULL, ob ? &zero : NULL, &b);
-   if (r) {
-      return status_of(r);
+   /* the image, on the GPU (coalesced with concurrent adds) */
+   add_submit(e, &q);
+   registry_unpin(q.old_sb);
+   if (q.rc) {
+      free(q.pages);
+      free(q.slots);
+      registry_unpin(q.sb);
+      return status_of(q.rc);
    }
-   rf_amd_filter_info info;
-   r = rf_amd_batch_build_hashes_host(b, new_fp_arr);
-   if (!r) {
-      r = rf_amd_batch_info(b, 0, &info);
-   }
-   if (!r && info.error) {
-      r = RF_AMD_EINVAL; /* a block over a page: undefined behaviour in the reference */
-   }
-   const uint64 ps    = cache_config_page_size(cfg->cache_cfg);
-   uint8       *pages = NULL;
-   uint64      *slots = NULL;
-   if (!r) {
-      pages = malloc(ps * info.num_pages);
-      slots = malloc(sizeof(uint64) * info.num_indices);
-      r     = (pages && slots) ? rf_amd_batch_read_image(b, 0, pages, ps * info.num_pages, slots,
-                                                       info.num_indices)
-                               : RF_AMD_ENOMEM;
-   }
-   if (r) {
-      free(pages);
-      free(slots);
-      rf_amd_batch_destroy(b);
-      return status_of(r);
-   }
+   const rf_amd_filter_info info  = q.info;
+   const uint8             *pages = q.pages;
+   const uint64            *slots = q.slots;
+   const uint64             ps    = cache_config_page_size(cfg->cache_cfg);
 
    /* the reference's page allocation sequence, :429-456 */
    allocator *al = cache_get_allocator(cc);
    uint64     meta_head;
-   rc = allocator_alloc(al, &meta_head, PAGE_TYPE_FILTER);
+   platform_status rc = allocator_alloc(al, &meta_head, PAGE_TYPE_FILTER);
    platform_assert_status_ok(rc);
    filter->meta_head = meta_head;
    mini_allocator mini;
@@ -410,23 +838,15 @@ routing_filter_add(cache                *cc,
    }
    mini_release(&mini);
    free(page_addr);
-   free(pages);
-   free(slots);
+   free(q.pages);
+   free(q.slots);
 
    filter->num_fingerprints = (uint32)nfp;
    filter->num_unique       = info.num_unique;
    filter->value_size       = info.value_size;
 
-   /* keep the filter on the device (probe-only copy of pages, slots and probe lines) */
-   void              *d_pages = NULL, *d_slots = NULL;
-   rf_amd_batch      *keep    = NULL;
-   rf_amd_filter_info one     = info;
-   if (rf_amd_batch_image_ptrs(b, 0, &d_pages, &d_slots) == 0
-       && rf_amd_batch_import(e, &c, 1, &one, d_pages, d_slots, 1, &keep) == 0)
-   {
-      registry_insert(cc, filter->addr, keep, 1);
-   }
-   rf_amd_batch_destroy(b);
+   /* keep the filter on the device, its whole batch (the pin becomes the registry entry) */
+   registry_insert(cc, filter->addr, q.sb, &q.f, 1, 0);
    return STATUS_OK;
 }
 
@@ -442,200 +862,275 @@ routing_filter_lookup(cache                *cc,
       *found_values = 0;
       return STATUS_OK;
    }
-   uint32        h = data_key_hash(cfg->data_cfg, target, cfg->seed);
-   rf_amd_batch *b;
-   platform_status rc = resident(cc, cfg, filter, &b);
+   uint32          h = data_key_hash(cfg->data_cfg, target, cfg->seed);
+   shim_batch     *sb;
+   uint32          f;
+   platform_status rc = resident_pin(cc, cfg, filter, &sb, &f);
    if (!SUCCESS(rc)) {
       return rc;
    }
-   return status_of(rf_amd_batch_probe_hashes_host(b, &h, NULL, 1, found_values));
+   rc = status_of(rf_amd_probe_filters_host(engine(), &sb->b, &f, 1, &h, NULL, 1, found_values));
+   registry_unpin(sb);
+   return rc;
 }
 
-/* async: a queue of waiting states; the resume marker says "queued, not yet probed" */
-static char                                g_queued_marker;
+/* ---- grouping of lookups by filter: an open-addressing map (cache, addr) -> group ---------- */
+typedef struct group_map {
+   uint64       *key_addr;
+   const cache **key_cc;
+   uint32       *gid;
+   uint64        mask;
+} group_map;
+
+static void
+group_map_init(group_map *m, uint64 n)
+{
+   uint64 cap = 16;
+   while (cap < 2 * n) {
+      cap <<= 1;
+   }
+   m->key_addr = malloc(sizeof(uint64) * cap);
+   m->key_cc   = malloc(sizeof(*m->key_cc) * cap);
+   m->gid      = malloc(sizeof(uint32) * cap);
+   platform_assert(m->key_addr && m->key_cc && m->gid);
+   memset(m->gid, 0xff, sizeof(uint32) * cap);
+   m->mask = cap - 1;
+}
+
+static void
+group_map_deinit(group_map *m)
+{
+   free(m->key_addr);
+   free(m->key_cc);
+   free(m->gid);
+}
+
+/* the group of (cc, addr); *is_new when this call created it as group `next` */
+static uint32
+group_map_get(group_map *m, const cache *cc, uint64 addr, uint32 next, int *is_new)
+{
+   uint64 s = registry_bucket(cc, addr) & m->mask;
+   for (;; s = (s + 1) & m->mask) {
+      if (m->gid[s] == UINT32_MAX) {
+         m->key_addr[s] = addr;
+         m->key_cc[s]   = cc;
+         m->gid[s]      = next;
+         *is_new        = 1;
+         return next;
+      }
+      if (m->key_addr[s] == addr && m->key_cc[s] == cc) {
+         *is_new = 0;
+         return m->gid[s];
+      }
+   }
+}
+
+/*
+ * n lookups: hashes h[i] against filters[i] (each given by a representative descriptor and
+ * cache), in ONE GPU launch over every filter they name. Per lookup: found[i] and rc[i].
+ */
+static void
+lookup_many(cache *const          *ccs,
+            const routing_config *const *cfgs,
+            const routing_filter *const *filters,
+            const uint32         *h,
+            uint64                n,
+            uint64               *found,
+            platform_status      *rc)
+{
+   group_map m;
+   group_map_init(&m, n);
+   uint32          *gid    = malloc(sizeof(uint32) * (n ? n : 1));
+   uint32          *pgid   = malloc(sizeof(uint32) * (n ? n : 1));
+   shim_batch     **gsb    = malloc(sizeof(*gsb) * (n ? n : 1));
+   rf_amd_batch   **gb     = malloc(sizeof(*gb) * (n ? n : 1));
+   uint32          *gf     = malloc(sizeof(uint32) * (n ? n : 1));
+   uint32          *gprobe = malloc(sizeof(uint32) * (n ? n : 1));
+   platform_status *grc    = malloc(sizeof(*grc) * (n ? n : 1));
+   platform_assert(gid && pgid && gsb && gb && gf && gprobe && grc);
+   uint32 ng = 0, np = 0; /* groups, groups that probe */
+   for (uint64 i = 0; i < n; i++) {
+      int is_new;
+      gid[i] = group_map_get(&m, ccs[i], filters[i]->addr, ng, &is_new);
+      if (is_new) {
+         uint32 fi = 0;
+         grc[ng]   = resident_pin(ccs[i], cfgs[i], filters[i], &gsb[ng], &fi);
+         if (SUCCESS(grc[ng])) {
+            gb[np]     = gsb[ng]->b;
+            gf[np]     = fi;
+            gprobe[ng] = np++;
+         } else {
+            gsb[ng]    = NULL;
+            gprobe[ng] = UINT32_MAX; /* finds nothing; the state gets grc */
+         }
+         ng++;
+      }
+      pgid[i] = gprobe[gid[i]];
+   }
+   platform_status prc = status_of(rf_amd_probe_filters_host(engine(), gb, gf, np, h, pgid, n, found));
+   for (uint64 i = 0; i < n; i++) {
+      rc[i] = SUCCESS(grc[gid[i]]) ? prc : grc[gid[i]];
+      if (!SUCCESS(rc[i])) {
+         found[i] = 0;
+      }
+   }
+   for (uint32 g = 0; g < ng; g++) {
+      registry_unpin(gsb[g]);
+   }
+   group_map_deinit(&m);
+   free(gid);
+   free(pgid);
+   free(gsb);
+   free(gb);
+   free(gf);
+   free(gprobe);
+   free(grc);
+}
+
+/* ---- async: queued states, completed by a completion thread ------------------------------ */
+static char g_queued_marker;
 #define ASYNC_STATE_QUEUED ((async_state)&g_queued_marker)
-static pthread_mutex_t                     g_async_mu = PTHREAD_MUTEX_INITIALIZER;
-static routing_filter_lookup_async_state **g_async_q;
-static uint64                              g_async_n, g_async_cap;
-static uint64                              g_async_batches, g_async_probes;
+typedef routing_filter_lookup_async_state rf_state;
 
-static uint64
-async_batch_limit(void)
-{
-   const char *s = getenv("RF_SHIM_ASYNC_BATCH");
-   return s ? (uint64)atoll(s) : 1024;
-}
+static struct {
+   pthread_mutex_t mu;
+   pthread_cond_t  cv;
+   rf_state      **q;
+   uint64          n, cap;
+   uint64          t_first; /* enqueue time of the oldest queued state (ns) */
+   int             urgent;
+} g_aq = {.mu = PTHREAD_MUTEX_INITIALIZER};
+static pthread_once_t g_aq_once = PTHREAD_ONCE_INIT;
+static uint64         g_async_batches, g_async_probes;
+static uint64         g_async_limit, g_async_window_ns;
 
-static int
-cmp_state_filter(const void *a, const void *b)
+/* probe and complete n states (their filters in one launch); callbacks fire last per state */
+static void
+complete_states(rf_state **q, uint64 n)
 {
-   const routing_filter_lookup_async_state *x = *(routing_filter_lookup_async_state *const *)a;
-   const routing_filter_lookup_async_state *y = *(routing_filter_lookup_async_state *const *)b;
-   return x->filter.addr < y->filter.addr ? -1 : (x->filter.addr > y->filter.addr ? 1 : 0);
-}
-
-/* probe every queued state: one GPU probe per distinct filter */
-void
-routing_filter_amd_flush(void)
-{
-   pthread_mutex_lock(&g_async_mu);
-   routing_filter_lookup_async_state **q = g_async_q;
-   uint64                              n = g_async_n;
-   g_async_q                               = NULL;
-   g_async_n = g_async_cap = 0;
-   pthread_mutex_unlock(&g_async_mu);
    if (n == 0) {
       return;
    }
-   qsort(q, n, sizeof(*q), cmp_state_filter); /* stable grouping is enough: order unused */
-   uint32          *h      = malloc(sizeof(uint32) * n);
-   uint64          *found  = malloc(sizeof(uint64) * n);
-   rf_amd_batch   **groups = malloc(sizeof(*groups) * n);
-   uint64          *counts = malloc(sizeof(uint64) * n);
-   platform_status *grc    = malloc(sizeof(*grc) * n);
-   platform_assert(h && found && groups && counts && grc);
-   /* every distinct filter's states form one group; all groups go to the GPU in one round
-      trip (rf_amd_probe_many_hashes_host) */
-   uint32 ng = 0, nok = 0;
-   for (uint64 s = 0; s < n;) {
-      uint64 t = s;
-      while (t < n && q[t]->filter.addr == q[s]->filter.addr) {
-         t++;
-      }
-      rf_amd_batch   *b;
-      platform_status rc = resident(q[s]->cc, q[s]->cfg, &q[s]->filter, &b);
-      grc[s]             = rc;
-      if (SUCCESS(rc)) { /* probed groups first, in queue order */
-         for (uint64 i = s; i < t; i++) {
-            h[nok + (i - s)] = q[i]->fp; /* the full 32-bit hash, stored when queued */
-         }
-         groups[ng] = b;
-         counts[ng] = t - s;
-         ng++;
-         nok += t - s;
-      }
-      s = t;
+   cache               **ccs   = malloc(sizeof(*ccs) * n);
+   const routing_config **cfgs = malloc(sizeof(*cfgs) * n);
+   const routing_filter **fl   = malloc(sizeof(*fl) * n);
+   uint32               *h     = malloc(sizeof(uint32) * n);
+   uint64               *found = malloc(sizeof(uint64) * n);
+   platform_status      *rc    = malloc(sizeof(*rc) * n);
+   platform_assert(ccs && cfgs && fl && h && found && rc);
+   for (uint64 i = 0; i < n; i++) {
+      ccs[i]  = q[i]->cc;
+      cfgs[i] = q[i]->cfg;
+      fl[i]   = &q[i]->filter;
+      h[i]    = q[i]->fp; /* the full 32-bit hash, stored when queued */
    }
-   platform_status prc =
-      status_of(rf_amd_probe_many_hashes_host(engine(), groups, NULL, counts, ng, h, found));
-   uint64 at = 0;
-   for (uint64 s = 0; s < n;) {
-      uint64 t = s;
-      while (t < n && q[t]->filter.addr == q[s]->filter.addr) {
-         t++;
+   lookup_many(ccs, cfgs, fl, h, n, found, rc);
+   for (uint64 i = 0; i < n; i++) {
+      rf_state         *st  = q[i];
+      async_callback_fn cb  = st->callback;
+      void             *arg = st->callback_arg;
+      *st->found_values     = found[i];
+      st->__async_result    = rc[i];
+      /* from here the owner may resume (and reuse) the state: it is not touched again */
+      __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
+      if (cb) {
+         cb(arg);
       }
-      platform_status rc = SUCCESS(grc[s]) ? prc : grc[s];
-      for (uint64 i = s; i < t; i++) {
-         routing_filter_lookup_async_state *st = q[i];
-         *st->found_values = SUCCESS(rc) ? found[at + (i - s)] : 0;
-         st->__async_result = rc;
-         async_callback_fn cb  = st->callback;
-         void             *arg = st->callback_arg;
-         __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
-         if (cb) {
-            cb(arg);
-         }
-      }
-      if (SUCCESS(grc[s])) {
-         at += t - s;
-      }
-      s = t;
    }
    __atomic_fetch_add(&g_async_batches, 1, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_probes, n, __ATOMIC_RELAXED);
+   free(ccs);
+   free(cfgs);
+   free(fl);
    free(h);
    free(found);
-   free(groups);
-   free(counts);
-   free(grc);
+   free(rc);
+}
+
+/* takes the whole queue (the caller holds g_aq.mu) */
+static rf_state **
+aq_take_locked(uint64 *n)
+{
+   rf_state **q = g_aq.q;
+   *n           = g_aq.n;
+   g_aq.q       = NULL;
+   g_aq.n = g_aq.cap = 0;
+   g_aq.urgent       = 0;
+   return q;
+}
+
+static void *
+completion_main(void *arg)
+{
+   (void)arg;
+   platform_ensure_thread_registered(); /* callbacks and cache_get (imports) run here */
+   prctl(PR_SET_TIMERSLACK, 1UL, 0UL, 0UL, 0UL); /* microsecond waits, not the 50 us default slack */
+   pthread_mutex_lock(&g_aq.mu);
+   for (;;) {
+      while (g_aq.n == 0) {
+         pthread_cond_wait(&g_aq.cv, &g_aq.mu);
+      }
+      while (g_aq.n > 0 && g_aq.n < g_async_limit && !g_aq.urgent) {
+         const uint64 deadline = g_aq.t_first + g_async_window_ns;
+         if (now_ns() >= deadline) {
+            break;
+         }
+         struct timespec ts = {.tv_sec = deadline / 1000000000ull, .tv_nsec = deadline % 1000000000ull};
+         pthread_cond_timedwait(&g_aq.cv, &g_aq.mu, &ts);
+      }
+      uint64     n;
+      rf_state **q = aq_take_locked(&n);
+      pthread_mutex_unlock(&g_aq.mu);
+      complete_states(q, n);
+      free(q);
+      pthread_mutex_lock(&g_aq.mu);
+   }
+   return NULL;
+}
+
+static void
+aq_init(void)
+{
+   g_async_limit     = env_u64("RF_SHIM_ASYNC_BATCH", 1024);
+   g_async_window_ns = env_u64("RF_SHIM_ASYNC_WINDOW_US", 20) * 1000;
+   if (g_async_limit == 0) {
+      g_async_limit = 1;
+   }
+   pthread_condattr_t ca;
+   pthread_condattr_init(&ca);
+   pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
+   pthread_cond_init(&g_aq.cv, &ca);
+   pthread_condattr_destroy(&ca);
+   pthread_attr_t at;
+   pthread_attr_init(&at);
+   pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+   pthread_t t;
+   platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
+   pthread_attr_destroy(&at);
+}
+
+/* probe every state queued so far, in the caller's thread */
+void
+routing_filter_amd_flush(void)
+{
+   pthread_once(&g_aq_once, aq_init);
+   pthread_mutex_lock(&g_aq.mu);
+   uint64     n;
+   rf_state **q = aq_take_locked(&n);
+   pthread_mutex_unlock(&g_aq.mu);
+   complete_states(q, n);
    free(q);
 }
 
-typedef struct lookup_ref {
-   uint64 addr; /* the filter's index extent */
-   uint64 i;    /* position in the caller's arrays */
-} lookup_ref;
-
-static int
-cmp_lookup_ref(const void *a, const void *b)
+void
+routing_filter_amd_async_config(uint64 batch, uint64 window_us)
 {
-   const lookup_ref *x = a, *y = b;
-   if (x->addr != y->addr) {
-      return x->addr < y->addr ? -1 : 1;
-   }
-   return x->i < y->i ? -1 : (x->i > y->i ? 1 : 0);
-}
-
-/* n lookups (filters[i], keys[i]) in one GPU round trip: the batch form of the per-bundle
- * routing_filter_lookup calls of trunk_merge_lookup (src/trunk.c:6008-6075). found[i] equals
- * what routing_filter_lookup(cc, cfg, &filters[i], keys[i], &found[i]) would return. */
-platform_status
-routing_filter_amd_lookup_batch(cache                *cc,
-                                const routing_config *cfg,
-                                routing_filter       *filters,
-                                const key            *keys,
-                                uint64                n,
-                                uint64               *found)
-{
-   if (n == 0) {
-      return STATUS_OK;
-   }
-   lookup_ref      *order  = malloc(sizeof(*order) * n);
-   uint32          *h      = malloc(sizeof(uint32) * n);
-   uint64          *fo     = malloc(sizeof(uint64) * n);
-   rf_amd_batch   **groups = malloc(sizeof(*groups) * n);
-   uint64          *counts = malloc(sizeof(uint64) * n);
-   platform_assert(order && h && fo && groups && counts);
-   /* group the lookups by filter */
-   for (uint64 i = 0; i < n; i++) {
-      order[i].addr = filters[i].addr;
-      order[i].i    = i;
-   }
-   qsort(order, n, sizeof(*order), cmp_lookup_ref);
-   platform_status rc = STATUS_OK;
-   uint32          ng = 0;
-   uint64          m  = 0;
-   for (uint64 s = 0; s < n && SUCCESS(rc);) {
-      uint64 t = s;
-      while (t < n && order[t].addr == order[s].addr) {
-         t++;
-      }
-      if (order[s].addr == 0) { /* NULL filter finds nothing (:1003-1006) */
-         for (uint64 i = s; i < t; i++) {
-            found[order[i].i] = 0;
-         }
-      } else {
-         rf_amd_batch *b;
-         rc = resident(cc, cfg, &filters[order[s].i], &b);
-         if (SUCCESS(rc)) {
-            for (uint64 i = s; i < t; i++) {
-               h[m + (i - s)] = data_key_hash(cfg->data_cfg, keys[order[i].i], cfg->seed);
-            }
-            groups[ng] = b;
-            counts[ng] = t - s;
-            ng++;
-            m += t - s;
-         }
-      }
-      s = t;
-   }
-   if (SUCCESS(rc)) {
-      rc = status_of(rf_amd_probe_many_hashes_host(engine(), groups, NULL, counts, ng, h, fo));
-   }
-   if (SUCCESS(rc)) {
-      uint64 at = 0;
-      for (uint64 i = 0; i < n; i++) {
-         if (order[i].addr != 0) {
-            found[order[i].i] = fo[at++];
-         }
-      }
-   }
-   free(order);
-   free(h);
-   free(fo);
-   free(groups);
-   free(counts);
-   return rc;
+   pthread_once(&g_aq_once, aq_init);
+   pthread_mutex_lock(&g_aq.mu);
+   g_async_limit     = batch ? batch : 1;
+   g_async_window_ns = window_us * 1000;
+   pthread_cond_signal(&g_aq.cv); /* the completion thread re-reads them */
+   pthread_mutex_unlock(&g_aq.mu);
 }
 
 void
@@ -653,36 +1148,91 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
       return ASYNC_STATUS_DONE;
    }
    if (at == ASYNC_STATE_QUEUED) {
-      /* the owner is waiting on it: probe everything queued so far, this state included */
+      /* a polling owner: probe what is queued now, in this thread (this state among them,
+         unless the completion thread already holds it). RUNNING either way -- the state's
+         callback may have fired; the next call returns DONE */
       routing_filter_amd_flush();
-      at = __atomic_load_n(&state->__async_state_stack[0], __ATOMIC_ACQUIRE);
-      return at == ASYNC_STATE_DONE ? ASYNC_STATUS_DONE : ASYNC_STATUS_RUNNING;
+      return ASYNC_STATUS_RUNNING;
    }
    /* ASYNC_STATE_INIT (:898-905) */
    if (state->filter.addr == 0) {
-      *state->found_values = 0;
-      state->__async_result = STATUS_OK;
+      *state->found_values          = 0;
+      state->__async_result         = STATUS_OK;
       state->__async_state_stack[0] = ASYNC_STATE_DONE;
       return ASYNC_STATUS_DONE;
    }
-   state->fp = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
+   pthread_once(&g_aq_once, aq_init);
+   state->fp                     = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
    state->__async_state_stack[0] = ASYNC_STATE_QUEUED;
-   uint64 limit = async_batch_limit();
-   pthread_mutex_lock(&g_async_mu);
-   if (g_async_n == g_async_cap) {
-      g_async_cap = g_async_cap ? 2 * g_async_cap : 256;
-      g_async_q   = realloc(g_async_q, sizeof(*g_async_q) * g_async_cap);
-      platform_assert(g_async_q != NULL);
+   pthread_mutex_lock(&g_aq.mu);
+   if (g_aq.n == g_aq.cap) {
+      g_aq.cap = g_aq.cap ? 2 * g_aq.cap : 1024;
+      g_aq.q   = realloc(g_aq.q, sizeof(*g_aq.q) * g_aq.cap);
+      platform_assert(g_aq.q != NULL);
    }
-   g_async_q[g_async_n++] = state;
-   int full               = g_async_n >= limit;
-   pthread_mutex_unlock(&g_async_mu);
-   if (full) {
-      routing_filter_amd_flush();
+   g_aq.q[g_aq.n++] = state;
+   if (g_aq.n == 1) {
+      g_aq.t_first = now_ns();
+      pthread_cond_signal(&g_aq.cv);
+   } else if (g_aq.n == g_async_limit) {
+      pthread_cond_signal(&g_aq.cv);
    }
-   return __atomic_load_n(&state->__async_state_stack[0], __ATOMIC_ACQUIRE) == ASYNC_STATE_DONE
-             ? ASYNC_STATUS_DONE
-             : ASYNC_STATUS_RUNNING;
+   pthread_mutex_unlock(&g_aq.mu);
+   /* the state may already be complete (another thread): it is not read again here */
+   return ASYNC_STATUS_RUNNING;
+}
+
+/* n lookups (filters[i], keys[i]) in one GPU launch -- the batch form of the per-bundle
+ * routing_filter_lookup calls of trunk_merge_lookup (src/trunk.c:6008-6075). found[i] equals
+ * what routing_filter_lookup(cc, cfg, &filters[i], keys[i], &found[i]) would return. */
+platform_status
+routing_filter_amd_lookup_batch(cache                *cc,
+                                const routing_config *cfg,
+                                routing_filter       *filters,
+                                const key            *keys,
+                                uint64                n,
+                                uint64               *found)
+{
+   if (n == 0) {
+      return STATUS_OK;
+   }
+   cache               **ccs   = malloc(sizeof(*ccs) * n);
+   const routing_config **cfgs = malloc(sizeof(*cfgs) * n);
+   const routing_filter **fl   = malloc(sizeof(*fl) * n);
+   uint32               *h     = malloc(sizeof(uint32) * n);
+   uint64               *fo    = malloc(sizeof(uint64) * n);
+   uint64               *idx   = malloc(sizeof(uint64) * n);
+   platform_status      *rc    = malloc(sizeof(*rc) * n);
+   platform_assert(ccs && cfgs && fl && h && fo && idx && rc);
+   uint64 m = 0;
+   for (uint64 i = 0; i < n; i++) {
+      if (filters[i].addr == 0) { /* NULL filter finds nothing (:1003-1006) */
+         found[i] = 0;
+         continue;
+      }
+      ccs[m]  = cc;
+      cfgs[m] = cfg;
+      fl[m]   = &filters[i];
+      h[m]    = data_key_hash(cfg->data_cfg, keys[i], cfg->seed);
+      idx[m]  = i;
+      m++;
+   }
+   lookup_many(ccs, cfgs, fl, h, m, fo, rc);
+   platform_status ret = STATUS_OK;
+   for (uint64 j = 0; j < m; j++) {
+      found[idx[j]] = fo[j];
+      if (!SUCCESS(rc[j]) && SUCCESS(ret)) {
+         ret = rc[j];
+      }
+   }
+   free(ccs);
+   free(cfgs);
+   free(fl);
+   free(h);
+   free(fo);
+   free(idx);
+   free(rc);
+   return ret;
 }
 
 /* ---- reference counts, estimates, space -------------------------------------------------- */
@@ -735,19 +1285,28 @@ routing_filter_estimate_unique_fp(cache                *cc,
    }
    *num_unique_fp = 0;
    platform_assert(num_filters <= MAX_FILTERS);
-   rf_amd_batch *batches[MAX_FILTERS];
-   uint32        index[MAX_FILTERS];
+   shim_batch     *sbs[MAX_FILTERS];
+   rf_amd_batch   *batches[MAX_FILTERS];
+   uint32          index[MAX_FILTERS];
+   platform_status rc = STATUS_OK;
    for (uint64 i = 0; i < num_filters; i++) {
+      sbs[i]     = NULL;
       batches[i] = NULL;
       index[i]   = 0;
-      if (filter[i].addr != 0) {
-         platform_status rc = resident(cc, cfg, &filter[i], &batches[i]);
-         if (!SUCCESS(rc)) {
-            return rc;
+      if (filter[i].addr != 0 && SUCCESS(rc)) {
+         rc = resident_pin(cc, cfg, &filter[i], &sbs[i], &index[i]);
+         if (SUCCESS(rc)) {
+            batches[i] = sbs[i]->b;
          }
       }
    }
-   return status_of(rf_amd_batch_estimate_unique_fp(batches, index, num_filters, num_unique_fp));
+   if (SUCCESS(rc)) {
+      rc = status_of(rf_amd_batch_estimate_unique_fp(batches, index, num_filters, num_unique_fp));
+   }
+   for (uint64 i = 0; i < num_filters; i++) {
+      registry_unpin(sbs[i]);
+   }
+   return rc;
 }
 
 uint64
@@ -783,10 +1342,12 @@ routing_filter_verify(cache          *cc,
    uint64 *found = malloc(sizeof(uint64) * (n ? n : 1));
    platform_assert(found != NULL);
    if (n && filter->addr != 0) {
-      rf_amd_batch   *b;
-      platform_status rc = resident(cc, cfg, filter, &b);
+      shim_batch     *sb;
+      uint32          f;
+      platform_status rc = resident_pin(cc, cfg, filter, &sb, &f);
       platform_assert_status_ok(rc);
-      platform_assert(rf_amd_batch_probe_hashes_host(b, h, NULL, n, found) == 0);
+      platform_assert(rf_amd_probe_filters_host(engine(), &sb->b, &f, 1, h, NULL, n, found) == 0);
+      registry_unpin(sb);
    } else {
       memset(found, 0, sizeof(uint64) * n);
    }

@@ -55,7 +55,8 @@ static int fail(int rc, const std::string& msg) {
 // its ~25 work buffers here instead of calling hipMalloc. Sizes are rounded up to classes
 // of 1/8 of a power of two (at most 12.5 % slack); a block returns to the pool when its
 // batch is destroyed unless the pool already holds RF_AMD_POOL_MIB MiB (default: a quarter
-// of the device memory, at least 32 GiB).
+// of the device memory free at engine creation, at most 16 GiB; rf_amd_engine_pool_trim
+// hands blocks back).
 // rf_amd_batch_destroy synchronises the device first; rf_amd_batch_destroy_on instead
 // parks the blocks behind an event on the caller's stream (stream-ordered release, as
 // hipFreeAsync): they become reusable once that event has completed.
@@ -145,11 +146,30 @@ struct HostStage {
   size_t cap = 0;
 };
 
+// A lookup channel of the host-buffer probe entry points (rf_amd_probe_filters_host and the
+// forms built on it). Callers on different threads take different slots, so their round
+// trips -- stream, pinned buffers, completion word -- run concurrently. A round trip is ONE
+// kernel launch: the kernel reads the probes from `h` (pinned, device-mapped) or, for large
+// calls, from `d` after one H2D copy, writes every result straight into `h`, and its last
+// workgroup stores the call's sequence number into `flag`, which the host polls.
+struct ProbeSlot {
+  hipStream_t st = nullptr;
+  uint8_t* h = nullptr;  // pinned coherent host memory: [hashes | groups ids | group table | results]
+  size_t hcap = 0;
+  uint8_t* d = nullptr;  // device copy of the inputs (copy mode)
+  size_t dcap = 0;
+  uint32_t* flag = nullptr;       // pinned coherent: the kernel's completion word
+  uint32_t* d_counter = nullptr;  // device: workgroups finished (k_probe_groups)
+  uint32_t seq = 0;
+};
+
 struct rf_amd_engine {
   int device;
   hipStream_t stream;
   DevPool pool;
   HostStage stage;
+  std::mutex slot_mu;
+  std::vector<ProbeSlot*> slots_all, slots_free;
 };
 
 struct DevBuf {
@@ -211,6 +231,7 @@ struct rf_amd_batch {
       d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n, d_pg_noline, d_cb_out;
   bool built = false;
   bool has_entries = false;  // built here: its sorted entries (d_part / d_sorted) are current
+  std::vector<uint32_t> err_host;  // per-filter build error bits once read back (empty: not yet)
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
   uint32_t ev_mask = EV_MASK_ALL;     // EV_MASK_PROBE: the probe's two events only
@@ -237,11 +258,13 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
   auto* e = new rf_amd_engine();
   e->device = device;
   {
-    // default: a quarter of the device's memory (72 GB on MI355X), at least 32 GiB
+    // default: a quarter of the memory free at engine creation, at most 16 GiB (one
+    // compaction round of 64 x 8M-fingerprint filters parks ~9 GB); other allocators of the
+    // process can reclaim it with rf_amd_engine_pool_trim
     const char* lim = getenv("RF_AMD_POOL_MIB");
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
-    const size_t dflt = std::max<size_t>((size_t)32768 << 20, total_b / 4);
+    const size_t dflt = std::min<size_t>((size_t)16384 << 20, free_b / 4);
     e->pool.limit = lim ? (size_t)atoll(lim) << 20 : dflt;
   }
   // a BLOCKING stream: ordered with the legacy null stream that torch and most callers use
@@ -258,6 +281,14 @@ extern "C" void rf_amd_engine_destroy(rf_amd_engine* e) {
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
   (void)hipStreamDestroy(e->stream);
+  for (ProbeSlot* s : e->slots_all) {
+    if (s->st) (void)hipStreamDestroy(s->st);
+    if (s->h) (void)hipHostFree(s->h);
+    if (s->d) (void)hipFree(s->d);
+    if (s->flag) (void)hipHostFree(s->flag);
+    if (s->d_counter) (void)hipFree(s->d_counter);
+    delete s;
+  }
   e->pool.drain();
   if (e->stage.h) (void)hipHostFree(e->stage.h);
   if (e->stage.d) (void)hipFree(e->stage.d);
@@ -626,12 +657,77 @@ extern "C" int rf_amd_batch_destroy_on(rf_amd_batch* b, void* stream) {
   return 0;
 }
 
+// Drops a built batch's work buffers (entries, maps, counters), keeping what lookups, image
+// reads, estimates and use as an old filter by image decode need: plans, outs, pages, slots,
+// probe lines, index map, probe runs. Stream-ordered like rf_amd_batch_destroy_on. A trimmed
+// batch no longer offers its entries in place to incremental adds (they decode its image).
+extern "C" int rf_amd_batch_trim(rf_amd_batch* b, void* stream) {
+  if (!b || !b->built) return fail(RF_AMD_EINVAL, "trim of an unbuilt batch");
+  HIPCHK(hipSetDevice(b->eng->device));
+  DevBuf* keep[] = {&b->d_plans, &b->d_pplans, &b->d_outs, &b->d_pages, &b->d_slots, &b->d_lines,
+                    &b->d_idx_filter, &b->d_runs, &b->d_wave_tab};
+  DevPool::Parked k{};
+  for (DevBuf* d : b->bufs()) {
+    if (!d->p || std::find(std::begin(keep), std::end(keep), d) != std::end(keep)) continue;
+    k.blocks.emplace_back(d->p, d->pool == &b->eng->pool ? d->n : 0);
+    d->p = nullptr;
+    d->n = 0;
+  }
+  b->has_entries = false;
+  if (k.blocks.empty()) return 0;
+  hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  hipError_t he = hipEventCreateWithFlags(&k.ev, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventRecord(k.ev, st);
+  if (he != hipSuccess) {  // cannot order the release: wait, then release
+    if (k.ev) (void)hipEventDestroy(k.ev);
+    (void)hipStreamSynchronize(st);
+    std::lock_guard<std::mutex> g(b->eng->pool.mu);
+    for (auto& blk : k.blocks) b->eng->pool.give_locked(blk.first, blk.second);
+    return 0;
+  }
+  b->eng->pool.park(std::move(k));
+  return 0;
+}
+
+// device bytes a batch holds (its buffers, pooled sizes)
+extern "C" uint64_t rf_amd_batch_device_bytes(const rf_amd_batch* b) {
+  if (!b) return 0;
+  uint64_t s = 0;
+  for (DevBuf* d : const_cast<rf_amd_batch*>(b)->bufs())
+    if (d->p) s += d->n;
+  return s;
+}
+
+// the engine's own stream (builds from host buffers, imports run there)
+extern "C" void* rf_amd_engine_stream(rf_amd_engine* e) { return e ? (void*)e->stream : nullptr; }
+extern "C" int rf_amd_engine_sync(rf_amd_engine* e) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
 extern "C" int rf_amd_engine_pool_stats(rf_amd_engine* e, uint64_t* pooled_bytes, uint64_t* hits, uint64_t* misses) {
   if (!e) return fail(RF_AMD_EINVAL, "null engine");
   std::lock_guard<std::mutex> g(e->pool.mu);
   if (pooled_bytes) *pooled_bytes = e->pool.pooled;
   if (hits) *hits = e->pool.hits;
   if (misses) *misses = e->pool.misses;
+  return 0;
+}
+
+// hands pooled device blocks back to the device until at most keep_bytes stay pooled (blocks
+// parked behind stream events are released once those complete)
+extern "C" int rf_amd_engine_pool_trim(rf_amd_engine* e, uint64_t keep_bytes) {
+  if (!e) return fail(RF_AMD_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(e->device));
+  std::lock_guard<std::mutex> g(e->pool.mu);
+  e->pool.reap_locked(false);
+  for (auto it = e->pool.free_blocks.begin(); it != e->pool.free_blocks.end() && e->pool.pooled > keep_bytes;) {
+    (void)hipFree(it->second);
+    e->pool.pooled -= it->first;
+    it = e->pool.free_blocks.erase(it);
+  }
   return 0;
 }
 
@@ -795,6 +891,169 @@ extern "C" int rf_amd_batch_build_hashes_host(rf_amd_batch* b, const uint32_t* h
   return 0;
 }
 
+// ---- host-buffer lookups over the engine's lookup slots (ProbeSlot) -----------------------
+extern "C" int rf_launch_probe_groups(void* stream, const uint32_t* in, const ProbeGroup* groups, uint32_t ng,
+                                      uint64_t n, uint64_t* found, uint32_t fp_size, uint32_t lis,
+                                      uint32_t* counter, uint32_t* done_flag, uint32_t seq);
+
+static ProbeSlot* slot_take(rf_amd_engine* e) {
+  {
+    std::lock_guard<std::mutex> g(e->slot_mu);
+    if (!e->slots_free.empty()) {
+      ProbeSlot* s = e->slots_free.back();
+      e->slots_free.pop_back();
+      return s;
+    }
+  }
+  auto* s = new ProbeSlot();
+  // non-blocking: a lookup does not wait for unrelated work on the legacy null stream
+  bool ok = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) == hipSuccess &&
+            hipHostMalloc((void**)&s->flag, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
+            hipMalloc((void**)&s->d_counter, 64) == hipSuccess &&
+            hipMemsetAsync(s->d_counter, 0, 64, s->st) == hipSuccess && hipStreamSynchronize(s->st) == hipSuccess;
+  if (!ok) {
+    if (s->st) (void)hipStreamDestroy(s->st);
+    if (s->flag) (void)hipHostFree(s->flag);
+    if (s->d_counter) (void)hipFree(s->d_counter);
+    delete s;
+    fail(RF_AMD_ENOMEM, "lookup slot allocation failed");
+    return nullptr;
+  }
+  *s->flag = 0;
+  std::lock_guard<std::mutex> g(e->slot_mu);
+  e->slots_all.push_back(s);
+  return s;
+}
+
+static void slot_give(rf_amd_engine* e, ProbeSlot* s) {
+  std::lock_guard<std::mutex> g(e->slot_mu);
+  e->slots_free.push_back(s);
+}
+
+static int slot_reserve(ProbeSlot* s, size_t hbytes, size_t dbytes) {
+  if (s->hcap < hbytes) {
+    if (s->h) (void)hipHostFree(s->h);
+    s->h = nullptr;
+    s->hcap = 0;
+    const size_t c = std::max<size_t>(hbytes, (size_t)1 << 16);
+    if (hipHostMalloc((void**)&s->h, c, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+      s->h = nullptr;
+      return fail(RF_AMD_ENOMEM, "pinned lookup buffer allocation failed");
+    }
+    s->hcap = c;
+  }
+  if (dbytes && s->dcap < dbytes) {
+    if (s->d) (void)hipFree(s->d);
+    s->d = nullptr;
+    s->dcap = 0;
+    const size_t c = std::max<size_t>(dbytes, (size_t)1 << 20);
+    if (hipMalloc((void**)&s->d, c) != hipSuccess) {
+      s->d = nullptr;
+      return fail(RF_AMD_ENOMEM, "device lookup buffer allocation failed");
+    }
+    s->dcap = c;
+  }
+  return 0;
+}
+
+// per-filter build error bits of a built batch, read back once (a batch is immutable once
+// built; a filter whose build failed finds nothing, as k_probe does through pplans.w)
+static int batch_errors(rf_amd_batch* b) {
+  if (!b->err_host.empty()) return 0;
+  std::vector<FilterOut> o(b->F);
+  HIPCHK(hipMemcpyAsync(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost, b->eng->stream));
+  HIPCHK(hipStreamSynchronize(b->eng->stream));
+  b->err_host.resize(b->F);
+  for (uint32_t f = 0; f < b->F; f++) b->err_host[f] = o[f].error;
+  return 0;
+}
+
+static ProbeGroup probe_group_of(const rf_amd_batch* b, uint32_t f) {
+  const FilterPlan& p = b->plans[f];
+  ProbeGroup g;
+  g.x = p.vs | (p.rem << 8) | (p.rvs << 16) | (p.lg_line << 24);
+  g.err = b->err_host[f];
+  g.lines = b->d_lines.as<uint4>() + 4ull * p.line_base;
+  g.pages = b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size;
+  g.slots = b->d_slots.as<uint64_t>() + p.idx_base;
+  return g;
+}
+
+// Probe modes of a round trip: inputs read by the kernel from pinned host memory (small
+// calls: no copy command) or copied to the device with one H2D first; results always written
+// by the kernel into pinned host memory; completion by polling the slot's flag word (or, with
+// RF_AMD_PROBE_WAIT=sync, hipStreamSynchronize). RF_AMD_PROBE_MODE=mapped|copy forces a mode.
+static int env_mode(const char* name, const char* a, const char* b) {
+  const char* v = getenv(name);
+  if (!v) return 0;
+  return !strcmp(v, a) ? 1 : (!strcmp(v, b) ? 2 : 0);
+}
+static const uint64_t MAPPED_MAX_PROBES = 2048;
+
+// The common body: n probes, probe i in group h_group[i] (NULL: group 0) of the ng-entry group
+// table, results into h_found. Waits for any work still queued on the engine stream (builds
+// issued there), then runs on a lookup slot of its own.
+static int probe_groups_host(rf_amd_engine* e, const rf_amd_config& cfg, const std::vector<ProbeGroup>& groups,
+                             const uint32_t* h_hashes, const uint32_t* h_group, uint64_t n, uint64_t* h_found) {
+  if (n == 0) return 0;
+  static const int mode = env_mode("RF_AMD_PROBE_MODE", "mapped", "copy");
+  static const int wait = env_mode("RF_AMD_PROBE_WAIT", "flag", "sync");
+  const uint32_t ng = (uint32_t)groups.size();
+  const size_t o_g = (8 * n + 15) & ~15ull, o_f = (o_g + sizeof(ProbeGroup) * ng + 63) & ~63ull;
+  const bool mapped = mode == 1 || (mode == 0 && n <= MAPPED_MAX_PROBES);
+  ProbeSlot* s = slot_take(e);
+  if (!s) return RF_AMD_ENOMEM;
+  struct Give {
+    rf_amd_engine* e;
+    ProbeSlot* s;
+    ~Give() { slot_give(e, s); }
+  } give{e, s};
+  if (int rc = slot_reserve(s, o_f + 8 * n, mapped ? 0 : o_f)) return rc;
+  memcpy(s->h, h_hashes, 4 * n);
+  uint32_t* hg = reinterpret_cast<uint32_t*>(s->h + 4 * n);
+  if (h_group) memcpy(hg, h_group, 4 * n);
+  else memset(hg, 0, 4 * n);
+  memcpy(s->h + o_g, groups.data(), sizeof(ProbeGroup) * ng);
+  if (hipStreamQuery(e->stream) == hipErrorNotReady) {  // order after builds still in flight
+    hipEvent_t ev;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev, e->stream));
+    HIPCHK(hipStreamWaitEvent(s->st, ev, 0));
+    (void)hipEventDestroy(ev);
+  }
+  const uint8_t* in = s->h;
+  if (!mapped) {
+    HIPCHK(hipMemcpyAsync(s->d, s->h, o_f, hipMemcpyHostToDevice, s->st));
+    in = s->d;
+  }
+  const uint32_t seq = ++s->seq ? s->seq : ++s->seq;  // never 0 (the flag's initial value)
+  uint64_t* found = reinterpret_cast<uint64_t*>(s->h + o_f);
+  (void)hipGetLastError();
+  if (int rc = rf_launch_probe_groups(s->st, reinterpret_cast<const uint32_t*>(in),
+                                      reinterpret_cast<const ProbeGroup*>(in + o_g), ng, n, found,
+                                      cfg.fingerprint_size, cfg.log_index_size, s->d_counter,
+                                      wait == 2 ? nullptr : s->flag, seq))
+    return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
+  if (wait == 2) {
+    HIPCHK(hipStreamSynchronize(s->st));
+  } else {
+    for (uint32_t spin = 1;; spin++) {
+      if (__atomic_load_n(s->flag, __ATOMIC_ACQUIRE) == seq) break;
+      __builtin_ia32_pause();
+      if ((spin & 4095) == 0) {  // a kernel that faulted never stores the flag
+        const hipError_t q = hipStreamQuery(s->st);
+        if (q == hipErrorNotReady) continue;
+        if (q != hipSuccess) return fail(RF_AMD_EINVAL, std::string("probe kernel: ") + hipGetErrorString(q));
+        if (__atomic_load_n(s->flag, __ATOMIC_ACQUIRE) != seq)
+          return fail(RF_AMD_EINVAL, "probe kernel finished without its completion flag");
+        break;
+      }
+    }
+  }
+  memcpy(h_found, found, 8 * n);
+  return 0;
+}
+
 extern "C" int rf_amd_batch_probe_hashes_host(rf_amd_batch* b, const uint32_t* h_hashes, const uint32_t* h_filter_id,
                                               uint64_t n, uint64_t* h_found) {
   if (!b || !b->built) return fail(RF_AMD_EINVAL, "probe on an unbuilt batch");
@@ -802,72 +1061,56 @@ extern "C" int rf_amd_batch_probe_hashes_host(rf_amd_batch* b, const uint32_t* h
   if (!h_hashes || !h_found) return fail(RF_AMD_EINVAL, "null probe buffer");
   rf_amd_engine* e = b->eng;
   HIPCHK(hipSetDevice(e->device));
-  std::lock_guard<std::mutex> g(e->stage.mu);
-  // [hashes 4n | filter ids 4n | found 8n], found 8-byte aligned
-  if (int rc = stage_reserve(e, 16ull * n + 16)) return rc;
-  uint8_t* hh = static_cast<uint8_t*>(e->stage.h);
-  uint8_t* dd = static_cast<uint8_t*>(e->stage.d);
-  const size_t o_fid = 4 * n, o_found = (8 * n + 7) & ~7ull;
-  memcpy(hh, h_hashes, 4 * n);
-  if (h_filter_id) {
-    memcpy(hh + o_fid, h_filter_id, 4 * n);
-    HIPCHK(hipMemcpyAsync(dd, hh, 8 * n, hipMemcpyHostToDevice, e->stream));
-  } else {
-    HIPCHK(hipMemcpyAsync(dd, hh, 4 * n, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipMemsetAsync(dd + o_fid, 0, 4 * n, e->stream));
-  }
-  if (int rc = do_probe(b, IN_HASH, dd, nullptr, 4, reinterpret_cast<const uint32_t*>(dd + o_fid), n,
-                        reinterpret_cast<uint64_t*>(dd + o_found), e->stream))
-    return rc;
-  HIPCHK(hipMemcpyAsync(hh + o_found, dd + o_found, 8 * n, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
-  memcpy(h_found, hh + o_found, 8 * n);
-  return 0;
+  if (int rc = batch_errors(b)) return rc;
+  std::vector<ProbeGroup> groups(h_filter_id ? b->F : 1);  // group = filter id (ids >= F find nothing)
+  for (uint32_t f = 0; f < groups.size(); f++) groups[f] = probe_group_of(b, f);
+  return probe_groups_host(e, b->cfg, groups, h_hashes, h_filter_id, n, h_found);
 }
 
-// Lookups against many resident filters in one round trip: group g probes counts[g] hashes
-// (consecutive in h_hashes) against filter filter_index[g] of batches[g]. One H2D of every
-// hash and filter id, one probe launch per group on the engine stream, one D2H, one
-// synchronisation -- the batch form of trunk_merge_lookup's per-bundle routing_filter_lookup
-// calls (src/trunk.c:6008-6075) and of a flush of queued routing_filter_lookup_async states.
+extern "C" int rf_amd_probe_filters_host(rf_amd_engine* e, rf_amd_batch* const* batches, const uint32_t* filter_index,
+                                         uint32_t num_groups, const uint32_t* h_hashes, const uint32_t* h_group,
+                                         uint64_t n, uint64_t* h_found) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (num_groups && !batches) return fail(RF_AMD_EINVAL, "null group arrays");
+  if (n == 0) return 0;
+  if (!h_hashes || !h_found) return fail(RF_AMD_EINVAL, "null probe buffer");
+  HIPCHK(hipSetDevice(e->device));
+  std::vector<ProbeGroup> groups(num_groups);
+  const rf_amd_config* cfg = nullptr;
+  for (uint32_t g = 0; g < num_groups; g++) {
+    rf_amd_batch* b = batches[g];
+    const uint32_t f = filter_index ? filter_index[g] : 0u;
+    if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "group on an unbuilt or foreign batch");
+    if (f >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
+    if (!cfg) cfg = &b->cfg;
+    else if (b->cfg.fingerprint_size != cfg->fingerprint_size || b->cfg.log_index_size != cfg->log_index_size)
+      return fail(RF_AMD_EINVAL, "groups of one lookup call must share fingerprint_size and log_index_size");
+    if (int rc = batch_errors(b)) return rc;
+    groups[g] = probe_group_of(b, f);
+  }
+  if (!cfg) {  // no filters: nothing found
+    memset(h_found, 0, 8 * n);
+    return 0;
+  }
+  return probe_groups_host(e, *cfg, groups, h_hashes, h_group, n, h_found);
+}
+
+// Lookups against many resident filters in ONE launch: group g probes counts[g] hashes
+// (consecutive in h_hashes) against filter filter_index[g] of batches[g] -- the batch form of
+// trunk_merge_lookup's per-bundle routing_filter_lookup calls (src/trunk.c:6008-6075) and of
+// a flush of queued routing_filter_lookup_async states.
 extern "C" int rf_amd_probe_many_hashes_host(rf_amd_engine* e, rf_amd_batch* const* batches,
                                              const uint32_t* filter_index, const uint64_t* counts,
                                              uint32_t num_groups, const uint32_t* h_hashes, uint64_t* h_found) {
   if (!e) return fail(RF_AMD_ENODEV, "no engine");
   if (num_groups && (!batches || !counts)) return fail(RF_AMD_EINVAL, "null group arrays");
   uint64_t n = 0;
-  for (uint32_t g = 0; g < num_groups; g++) {
-    rf_amd_batch* b = batches[g];
-    if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "group on an unbuilt or foreign batch");
-    if (filter_index && filter_index[g] >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
-    n += counts[g];
-  }
+  for (uint32_t g = 0; g < num_groups; g++) n += counts[g];
   if (n == 0) return 0;
-  if (!h_hashes || !h_found) return fail(RF_AMD_EINVAL, "null probe buffer");
-  HIPCHK(hipSetDevice(e->device));
-  std::lock_guard<std::mutex> lk(e->stage.mu);
-  if (int rc = stage_reserve(e, 16ull * n + 16)) return rc;
-  uint8_t* hh = static_cast<uint8_t*>(e->stage.h);
-  uint8_t* dd = static_cast<uint8_t*>(e->stage.d);
-  const size_t o_fid = 4 * n, o_found = (8 * n + 7) & ~7ull;
-  memcpy(hh, h_hashes, 4 * n);
-  uint32_t* hf = reinterpret_cast<uint32_t*>(hh + o_fid);
+  std::vector<uint32_t> gid(n);
   for (uint32_t g = 0, at = 0; g < num_groups; at += (uint32_t)counts[g], g++)
-    std::fill(hf + at, hf + at + counts[g], filter_index ? filter_index[g] : 0u);
-  HIPCHK(hipMemcpyAsync(dd, hh, 8 * n, hipMemcpyHostToDevice, e->stream));
-  uint64_t at = 0;
-  for (uint32_t g = 0; g < num_groups; g++) {
-    if (counts[g] == 0) continue;
-    if (int rc = do_probe(batches[g], IN_HASH, dd + 4 * at, nullptr, 4,
-                          reinterpret_cast<const uint32_t*>(dd + o_fid) + at, counts[g],
-                          reinterpret_cast<uint64_t*>(dd + o_found) + at, e->stream))
-      return rc;
-    at += counts[g];
-  }
-  HIPCHK(hipMemcpyAsync(hh + o_found, dd + o_found, 8 * n, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
-  memcpy(h_found, hh + o_found, 8 * n);
-  return 0;
+    std::fill(gid.begin() + at, gid.begin() + at + counts[g], g);
+  return rf_amd_probe_filters_host(e, batches, filter_index, num_groups, h_hashes, gid.data(), n, h_found);
 }
 
 static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
@@ -1050,6 +1293,8 @@ extern "C" int rf_amd_batch_infos(rf_amd_batch* b, rf_amd_filter_info* out, void
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost));
   }
+  b->err_host.resize(b->F);
+  for (uint32_t f = 0; f < b->F; f++) b->err_host[f] = o[f].error;
   for (uint32_t f = 0; f < b->F; f++) {
     const FilterPlan& p = b->plans[f];
     out[f].num_fingerprints = p.num_fp;
@@ -1196,6 +1441,7 @@ static int batch_import(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t F, 
     }
   }
   HIPCHK(hipStreamSynchronize(st));  // host vectors above are released on return
+  b->err_host.assign(F, 0u);  // imports carry no error bits (checked above)
   b->built = true;
   *out = b;
   return 0;

@@ -2910,6 +2910,64 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
   }
 }
 
+// ---- lookups against many resident filters in one launch ------------------------------
+// Probe i looks up hash in[i] in the filter of group in[n + i] (routing_filter_lookup,
+// src/routing_filter.c:985-1073, decoded exactly as k_probe: probe line, image walk when the
+// line overflowed). This is the latency path of the drop-in shim: a few to a few thousand
+// lookups over up to thousands of filters of different batches. Inputs, group table and
+// results may be device memory or pinned host memory read and written over PCIe. When
+// done_flag (pinned host memory) is set, every workgroup publishes its results system-wide
+// and the last one to finish stores `seq` there: the host waits by polling that word instead
+// of synchronising the stream (one HIP call fewer per round trip).
+__global__ __launch_bounds__(256) void k_probe_groups(const uint32_t* __restrict__ in,
+                                                      const ProbeGroup* __restrict__ groups, uint32_t ng,
+                                                      uint64_t n, uint64_t* __restrict__ found, uint32_t fp_size,
+                                                      uint32_t lis, uint32_t* __restrict__ counter,
+                                                      uint32_t* __restrict__ done_flag, uint32_t seq) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const uint32_t h = in[i], g = in[n + i];
+    uint64_t r = 0;
+    if (g < ng) {
+      const ProbeGroup G = groups[g];
+      const uint4 P = make_uint4(G.x, 0u, 0u, G.err);
+      if (!probe_line(P, h, G.lines, fp_size, r)) {  // overflowed line / no lines: walk the image
+        const uint32_t vs = G.x & 0xff, rem = (G.x >> 8) & 0xff, rvs = (G.x >> 16) & 0xff;
+        const uint32_t fp = h >> (32 - fp_size);
+        const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
+        const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+        r = probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, G.pages, G.slots[bucket >> lis], lis);
+      }
+    }
+    found[i] = r;
+  }
+  if (done_flag) {
+    // every wave's result stores have left before the workgroup signals (guide: producer
+    // stores -> vmcnt(0) -> barrier -> one lane's release fence -> vmcnt(0) -> flag)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t last = gridDim.x - 1;
+      if (last == 0 || atomicAdd(counter, 1u) == last) {
+        if (last) atomicExch(counter, 0u);  // ready for the slot's next launch (stream-ordered)
+        __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+extern "C" int rf_launch_probe_groups(void* stream, const uint32_t* in, const ProbeGroup* groups, uint32_t ng,
+                                      uint64_t n, uint64_t* found, uint32_t fp_size, uint32_t lis,
+                                      uint32_t* counter, uint32_t* done_flag, uint32_t seq) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_probe_groups, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, in, groups,
+                     ng, n, found, fp_size, lis, counter, done_flag, seq);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
 // ======================================================================================
 // launch wrappers (called from rf_engine.cpp)
 // ======================================================================================

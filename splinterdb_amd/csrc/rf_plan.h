@@ -84,6 +84,17 @@ struct EstFilter {
   uint32_t idx_first;     // prefix sum of num_idx over the filters before this one
 };
 
+// one resident filter of a multi-filter probe (k_probe_groups): the lookups of many batches'
+// filters -- the shim's queued routing_filter_lookup_async states, routing_filter_lookup
+// calls of different bundles -- go to the GPU in ONE launch; each probe names its group
+struct ProbeGroup {
+  uint32_t x;             // vs | rem << 8 | rvs << 16 | lg_line << 24 (the filter's pplans[f].x)
+  uint32_t err;           // nonzero: the filter's build failed, nothing is found
+  const uint4* lines;     // the filter's first probe line (lg_line != 0)
+  const uint8_t* pages;   // the filter's data pages
+  const uint64_t* slots;  // the filter's (relocatable) index slots
+};
+
 struct FilterOut {
   uint32_t num_unique;
   uint32_t num_pages;

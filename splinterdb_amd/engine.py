@@ -47,6 +47,8 @@ EXPORTED = [
     "rf_amd_batch_export", "rf_amd_batch_import", "rf_amd_route_scratch_bytes", "rf_amd_route_probes", "rf_amd_batch_probe_pairs", "rf_amd_unroute_found",
     "rf_amd_batch_build_hashes_host", "rf_amd_batch_probe_hashes_host", "rf_amd_engine_pool_stats",
     "rf_amd_filter_print_abs", "rf_amd_batch_infos", "rf_amd_batch_destroy_on", "rf_amd_probe_many_hashes_host",
+    "rf_amd_probe_filters_host", "rf_amd_engine_pool_trim", "rf_amd_engine_stream", "rf_amd_engine_sync",
+    "rf_amd_batch_device_bytes", "rf_amd_batch_trim",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -167,6 +169,14 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_infos.argtypes = [vp, ctypes.POINTER(RfFilterInfo), vp]
     L.rf_amd_batch_destroy_on.argtypes = [vp, vp]
     L.rf_amd_probe_many_hashes_host.argtypes = [vp, vp, vp, vp, u32, vp, vp]
+    L.rf_amd_probe_filters_host.argtypes = [vp, vp, vp, u32, vp, vp, u64, vp]
+    L.rf_amd_engine_pool_trim.argtypes = [vp, u64]
+    L.rf_amd_engine_stream.argtypes = [vp]
+    L.rf_amd_engine_stream.restype = vp
+    L.rf_amd_engine_sync.argtypes = [vp]
+    L.rf_amd_batch_device_bytes.argtypes = [vp]
+    L.rf_amd_batch_device_bytes.restype = u64
+    L.rf_amd_batch_trim.argtypes = [vp, vp]
     _lib = L
     return L
 

@@ -90,9 +90,9 @@ def test_incremental_chain_identical_to_reference(pair):
 
 def test_lookup_async_coalesced_equals_reference(pair):
     """20,000 routing_filter_lookup_async states over three filters, each started once and
-    then polled: the shim queues them (every first call returns ASYNC_STATUS_RUNNING) and
-    answers them in a few GPU probes; every found_values equals the reference coroutine's,
-    every callback fires once"""
+    then polled: the shim queues them (every first call returns ASYNC_STATUS_RUNNING) and its
+    completion thread answers them in a few GPU launches; every found_values equals the
+    reference coroutine's, every callback fires once"""
     ref, shim = pair
     descs_r, descs_s, allkeys = [], [], []
     for f, n in enumerate((50_000, 200_000, 7)):
@@ -114,10 +114,10 @@ def test_lookup_async_coalesced_equals_reference(pair):
     got, cb_s, run_s = shim.lookup_keys_async_many(descs_s, probe, fid)
     b1, p1 = shim.async_stats()
     assert (got == want).all()
-    # every state was queued and completed by a flush with its callback fired; the states
-    # whose arrival filled the queue (every 1024th) were flushed inside their own first call
-    assert cb_s == P and run_s == P - P // 1024
-    assert p1 - p0 == P and 0 < b1 - b0 <= P // 1024 + 1  # one GPU round trip per flush
+    # every state was queued (its first call returned RUNNING, never DONE) and completed by
+    # a flush with its callback fired exactly once
+    assert cb_s == P and run_s == P
+    assert p1 - p0 == P and 0 < b1 - b0 <= P  # one GPU launch per flush
     assert run_r == 0  # the reference's coroutine finds every page in the cache
     # and the synchronous form agrees with both
     for f in range(3):
@@ -182,3 +182,128 @@ def test_dec_ref_releases_and_other_filters_stay(pair):
     probe = K.random_keys(5000, seed=2)
     assert (ref.lookup_keys(b_r, probe) == shim.lookup_keys(b_s, probe)).all()
     assert (ref.lookup_keys(c_r, probe) == shim.lookup_keys(c_s, probe)).all()
+
+
+@pytest.mark.parametrize("inflight", [1, 64, 4096])
+def test_lookup_async_callback_driven(pair, inflight):
+    """routing_filter_lookup_async driven as tests/functional/test_async.c drives it: a state
+    is called again only after its callback fired (async_ctxt_process_ready, :168-196). Every
+    queued state must complete without being called again (the shim's completion thread), a
+    call never both fires its state's callback and returns DONE, each waiting state gets
+    exactly one callback, and every result equals the reference coroutine's"""
+    ref, shim = pair
+    descs_r, descs_s, allkeys = [], [], []
+    for f, n in enumerate((30_000, 5_000)):
+        keys = K.random_keys(n, seed=300 + f)
+        h = ref.hash_keys(keys)
+        descs_r.append(ref.add(h, value=f + 2))
+        descs_s.append(shim.add(h, value=f + 2))
+        allkeys.append(keys)
+    rng = np.random.default_rng(9)
+    P = 6000 if inflight == 1 else 20_000
+    fid = rng.integers(0, 2, size=P).astype(np.uint32)
+    probe = K.random_keys(P, seed=0xCB)
+    for i in np.nonzero(rng.random(P) < 0.6)[0]:
+        src = allkeys[fid[i]]
+        probe[i] = src[rng.integers(0, src.shape[0])]
+    want, st_r = ref.lookup_keys_async_driven(descs_r, probe, fid, max_inflight=inflight)
+    got, st_s = shim.lookup_keys_async_driven(descs_s, probe, fid, max_inflight=inflight)
+    assert (got == want).all()
+    assert st_r == {"running": 0, "callbacks": 0, "done": P, "violations": 0}  # all cached
+    assert st_s == {"running": P, "callbacks": P, "done": P, "violations": 0}, st_s
+
+
+def test_one_launch_per_flush_over_512_filters(pair):
+    """8,192 async states over 512 distinct filters, answered by ONE routing_filter_amd_flush:
+    one GPU launch (the engine's multi-filter probe, k_probe_groups) covers every filter,
+    and every result equals the reference's lookups"""
+    ref, shim = pair
+    descs_r, descs_s, allkeys = [], [], []
+    for f in range(512):
+        keys = K.ids_keys((np.uint64(f) << np.uint64(32)) + np.arange(500 + f, dtype=np.uint64))
+        h = ref.hash_keys(keys)
+        descs_r.append(ref.add(h, value=f % 40))
+        descs_s.append(shim.add(h, value=f % 40))
+        allkeys.append(keys)
+    rng = np.random.default_rng(11)
+    P = 8192
+    fid = rng.integers(0, 512, size=P).astype(np.uint32)
+    probe = K.random_keys(P, seed=0x512)
+    for i in np.nonzero(rng.random(P) < 0.5)[0]:
+        src = allkeys[fid[i]]
+        probe[i] = src[rng.integers(0, src.shape[0])]
+    want, _ = ref.lookup_batch(descs_r, probe, fid)
+    assert shim.async_config(1 << 40, 60_000_000)  # the completion thread stays out of it
+    try:
+        b0, p0 = shim.async_stats()
+        got, cb = shim.lookup_keys_async_flush(descs_s, probe, fid)
+        b1, p1 = shim.async_stats()
+    finally:
+        shim.async_config(1024, 20)
+    assert cb == P
+    assert (b1 - b0, p1 - p0) == (1, P)
+    assert (got == want).all()
+
+
+def test_concurrent_adds_and_lookups_from_8_threads(pair):
+    """8 registered threads at once, each growing its own filter by 3 incremental
+    routing_filter_add calls (2^17 keys each) and then looking up 4,000 keys synchronously
+    and through async states -- SplinterDB's TASK_TYPE_NORMAL workers compacting different
+    branches (src/trunk.c:3932, :4168). Concurrent adds are coalesced into shared GPU batches;
+    every filter's image equals the reference's single-threaded build of the same chain
+    (addresses depend on the threads' interleaving in both libraries, bytes do not), and
+    every lookup equals the reference's."""
+    ref, shim = pair
+    T, R, n, NP = 8, 3, 1 << 17, 4000
+    ids = np.arange(T * R * n, dtype=np.uint64) * np.uint64(2654435761) % np.uint64(1 << 40)
+    keys = K.ids_keys(ids)
+    rng = np.random.default_rng(5)
+    kt = keys.reshape(T, R * n, 24)
+    probe = np.concatenate([np.concatenate([kt[t][rng.integers(0, R * n, NP // 2)],
+                                            K.random_keys(NP // 2, seed=70 + t)]) for t in range(T)])
+    s0 = shim.shim_stats()
+    chains, fs, fa, add_s = shim.mt_chains(keys, T, R, n, probe, NP)
+    s1 = shim.shim_stats()
+    assert s1["add_filters"] - s0["add_filters"] == T * R
+    assert s1["add_batches"] - s0["add_batches"] <= T * R
+    kr = keys.reshape(T, R, n, 24)
+    for t in range(T):
+        old = None
+        for r in range(R):
+            old = ref.add(ref.hash_keys(kr[t, r]), value=r, old=old)
+            ir, is_ = ref.image(old), shim.image(chains[t][r])
+            assert (ir.num_unique, ir.num_pages) == (is_.num_unique, is_.num_pages), (t, r)
+            assert (ir.pages == is_.pages).all() and (ir.slots == is_.slots).all(), (t, r)
+        want = ref.lookup_keys(old, probe[t * NP:(t + 1) * NP])
+        assert (fs[t * NP:(t + 1) * NP] == want).all(), t
+        assert (fa[t * NP:(t + 1) * NP] == want).all(), t
+
+
+def test_registry_bound_evicts_and_reimports(pair):
+    """the shim keeps built filters on the device up to its bound (RF_AMD_REGISTRY_MIB):
+    shrinking the bound trims and evicts least recently used filters; lookups on evicted
+    filters re-import them from the cache and still equal the reference's"""
+    ref, shim = pair
+    descs_r, descs_s, allkeys = [], [], []
+    for f in range(24):
+        keys = K.random_keys(1 << 16, seed=900 + f)
+        h = ref.hash_keys(keys)
+        descs_r.append(ref.add(h, value=f % 7))
+        descs_s.append(shim.add(h, value=f % 7))
+        allkeys.append(keys)
+    s0 = shim.shim_stats()
+    assert shim.registry_set_limit(8)  # 8 MiB: a few probe-only filters
+    try:
+        s1 = shim.shim_stats()
+        assert s1["trims"] > s0["trims"] and s1["evictions"] > s0["evictions"]
+        assert s1["registry_bytes"] <= 8 << 20
+        for f in range(24):
+            probe = np.concatenate([allkeys[f][:500], K.random_keys(500, seed=f)])
+            assert (shim.lookup_keys(descs_s[f], probe) == ref.lookup_keys(descs_r[f], probe)).all(), f
+        # incremental adds onto evicted filters decode the re-imported image
+        h = ref.hash_keys(K.random_keys(5000, seed=0xE))
+        dr = ref.add(h, value=9, old=descs_r[0])
+        ds = shim.add(h, value=9, old=descs_s[0])
+        assert_same_pages(ref, shim, dr, ds, "onto evicted")
+    finally:
+        shim.registry_set_limit(32768)

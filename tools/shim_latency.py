@@ -1,8 +1,16 @@
 """Diagnostics: the drop-in shim's per-call costs on the GPU box, beside the reference's
 own routing_filter.c in the same page stack (oracle/_ref/libshim_rf.so vs libref_rf.so).
-Prints one JSON line: routing_filter_add of 2^20 hashes (fresh, onto an old filter),
-routing_filter_lookup of one key, routing_filter_amd_lookup_batch of 8,192 (filter, key)
-pairs over 8 filters, and 8,192 routing_filter_lookup_async states."""
+Prints one JSON line (ms, median of 5):
+  add_fresh_ms              routing_filter_add of 2^20 - 1 hashes
+  add_incremental_ms        the same onto an existing filter (old_filter, the trunk's case)
+  lookup_one_ms             routing_filter_lookup of one key
+  lookup_batch_8192_ms      routing_filter_amd_lookup_batch, 8,192 (filter, key) over 8 filters
+  lookup_async_8192_ms      8,192 routing_filter_lookup_async states over 8 filters, each
+                            started once, then polled (the shim: one completion thread)
+  async_driven_8192_ms      the same driven by callbacks, 64 in flight (test_async.c)
+  async_8192_512f_ms        8,192 states over 512 filters
+  mt_adds_8x_ms / 1x        8 threads each adding 2^20 - 1 hashes at once / one thread alone
+"""
 import json
 import os
 import sys
@@ -16,6 +24,7 @@ from splinterdb_amd import keys as K  # noqa: E402
 
 
 def med(f, reps=5):
+    f()
     ts = []
     for _ in range(reps):
         t = time.perf_counter()
@@ -27,19 +36,43 @@ def med(f, reps=5):
 out = {}
 n = (1 << 20) - 1
 for name, path in (("shim", R.SHIM_PATH), ("reference", R.LIB_PATH)):
-    with R.Stack(path=path, cache_mib=8192, disk_mib=65536) as s:
+    with R.Stack(path=path, cache_mib=16384, disk_mib=131072) as s:
         keys = [K.ids_keys((np.uint64(f) << np.uint64(32)) + np.arange(n, dtype=np.uint64)) for f in range(8)]
         hs = [s.hash_keys(k) for k in keys]
-        s.add(hs[0])  # warm
+        base = s.add(hs[0])
         r = {"add_fresh_ms": med(lambda: s.add(hs[0])),
-             "add_incremental_ms": med(lambda: s.add(hs[1], value=1, old=s.add(hs[0])))}
+             "add_incremental_ms": med(lambda: s.add(hs[1], value=1, old=base))}
         descs = [s.add(h, value=i % 8) for i, h in enumerate(hs)]
         rng = np.random.default_rng(1)
         P = 8192
         fid = rng.integers(0, 8, size=P).astype(np.uint32)
         probe = np.stack([keys[f][rng.integers(0, n)] for f in fid])
-        r["lookup_one_ms"] = med(lambda: s.lookup_keys(descs[0], probe[:1]))
+        r["lookup_one_ms"] = med(lambda: s.lookup_keys(descs[0], probe[:1]), reps=200)
         r["lookup_batch_8192_ms"] = med(lambda: s.lookup_batch(descs, probe, fid))
         r["lookup_async_8192_ms"] = med(lambda: s.lookup_keys_async_many(descs, probe, fid))
+        r["async_driven_8192_ms"] = med(lambda: s.lookup_keys_async_driven(descs, probe, fid, max_inflight=64))
+        many = [s.add(s.hash_keys(K.ids_keys((np.uint64(100 + f) << np.uint64(32)) +
+                                             np.arange(2000, dtype=np.uint64))), value=f % 30)
+                for f in range(512)]
+        fid512 = rng.integers(0, 512, size=P).astype(np.uint32)
+        r["async_8192_512f_ms"] = med(lambda: s.lookup_keys_async_many(many, probe, fid512))
+        T = 8
+        mkeys = K.ids_keys(np.arange(T * n, dtype=np.uint64) + np.uint64(1 << 40))
+        pr = K.random_keys(T * 16, seed=1)
+        ts8 = []
+        for _ in range(3):
+            t = time.perf_counter()
+            s.mt_chains(mkeys, T, 1, n, pr, 16)
+            ts8.append(time.perf_counter() - t)
+        ts1 = []
+        for _ in range(3):
+            t = time.perf_counter()
+            s.mt_chains(mkeys[: n], 1, 1, n, pr[:16], 16)
+            ts1.append(time.perf_counter() - t)
+        r["mt_adds_8x_ms"] = round(float(np.median(ts8)) * 1e3, 3)
+        r["mt_adds_1x_ms"] = round(float(np.median(ts1)) * 1e3, 3)
+        st = s.shim_stats()
+        if st:
+            r["shim_stats"] = st
         out[name] = r
 print(json.dumps(out))
