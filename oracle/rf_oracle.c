@@ -737,21 +737,23 @@ int rfo_estimate_unique_fp(const rfo_config *cfg, const rfo_filter *filters,
    return 0;
 }
 
-/* routing_filter_estimate_unique_keys_from_count, src/routing_filter.c:1119-1139 */
+/* routing_filter_estimate_unique_keys_from_count, src/routing_filter.c:1119-1139, evaluated as
+ * the reference's release build evaluates it (-O3 -ffast-math, Makefile:89,123-124): GCC
+ * reassociates the sum into two fused multiply-adds,
+ *   (fma(1/U - 1/s, 1/2, (1/s^2 - 1/U^2) * (1/12)) + fma(1/U^4 - 1/s^4, 1/120, log U)) - log s,
+ * and converts U * that through a 64-bit truncation. The order matters where the exact value
+ * is an integer: num_unique = 1 gives exactly 1 (H_U - H_{U-1} = 1/U) -- 1 in the reference's
+ * build, 0 in the source order. Checked against the reference for every fingerprint size 8-32
+ * (tests/test_ref_pinning.py). */
 uint32_t rfo_estimate_unique_keys_from_count(const rfo_config *cfg, uint64_t num_unique)
 {
-   double universe_size = (double)(1UL << cfg->fingerprint_size);
-   double unseen_fp = universe_size - (double)num_unique;
-   double universe_size_2 = universe_size * universe_size;
-   double universe_size_4 = universe_size_2 * universe_size_2;
-   double unseen_fp_2 = unseen_fp * unseen_fp;
-   double unseen_fp_4 = unseen_fp_2 * unseen_fp_2;
-   double harmonic_diff = log(universe_size) - log(unseen_fp) +
-                          1 / 2.0 * (1 / universe_size - 1 / unseen_fp) -
-                          1 / 12.0 * (1 / universe_size_2 - 1 / unseen_fp_2) +
-                          1 / 120.0 * (1 / universe_size_4 - 1 / unseen_fp_4);
-   uint32_t estimated_input_keys = (uint32_t)(universe_size * harmonic_diff);
-   return estimated_input_keys;
+   const double U = (double)(1UL << cfg->fingerprint_size);
+   const double s = U - (double)num_unique;
+   const double U2 = U * U, s2 = s * s;
+   const double lU = log(U), ls = log(s);
+   const double a = fma(1.0 / U - 1.0 / s, 0.5, (1.0 / s2 - 1.0 / U2) * (1.0 / 12.0));
+   const double b = fma(1.0 / (U2 * U2) - 1.0 / (s2 * s2), 1.0 / 120.0, lU);
+   return (uint32_t)(int64_t)(U * ((a + b) - ls));
 }
 
 /*

@@ -57,9 +57,11 @@
  * async. routing_filter_lookup_async's first call on a state hashes the key, queues the
  * state and returns ASYNC_STATUS_RUNNING without touching the state again (async.h:115-125:
  * it may be completed on another thread at once). A completion thread probes the queued
- * states -- ONE GPU launch for every filter they name -- when RF_SHIM_ASYNC_BATCH states
- * (default 1024) are queued or the oldest has waited RF_SHIM_ASYNC_WINDOW_US (default 20 us),
- * so every state completes without being called again. Completion stores found_values and
+ * states -- ONE GPU launch for every filter they name -- as soon as it is free, up to
+ * RF_SHIM_ASYNC_BATCH states
+ * (default 1024) -- in practice whatever arrived during the previous GPU round trip: batches
+ * size themselves (RF_SHIM_ASYNC_WINDOW_US, default 0, adds a wait for more) -- so every state
+ * completes without being called again. Completion stores found_values and
  * the result, marks the state done, then calls its callback(callback_arg) -- from the
  * completion thread, registered with the platform like any SplinterDB thread -- and the
  * state's next call returns ASYNC_STATUS_DONE. A state called again while still queued (a
@@ -282,24 +284,29 @@ registry_remove_locked(resident_filter *r, release_list *rl)
 static void
 registry_evict_locked(const resident_filter *keep, uint64 limit, release_list *rl)
 {
-   resident_filter *r = g_lru.lru_prev;
-   while (g_registry_bytes > limit && r != &g_lru) {
-      resident_filter *prev = r->lru_prev;
-      shim_batch      *sb   = r->sb;
-      if (r != keep && sb->pins == 0) {
-         if (sb->full) {
-            rf_amd_batch_trim(sb->b, NULL);
-            const uint64 nb = rf_amd_batch_device_bytes(sb->b);
-            g_registry_bytes -= sb->bytes - nb;
-            sb->bytes = nb;
-            sb->full  = 0;
-            g_registry_trims++;
-         } else {
-            registry_remove_locked(r, rl);
-            g_registry_evictions++;
+   /* pass 1 trims (least recently used first), pass 2 evicts */
+   for (int pass = 0; pass < 2; pass++) {
+      resident_filter *r = g_lru.lru_prev;
+      while (g_registry_bytes > limit && r != &g_lru) {
+         resident_filter *prev = r->lru_prev;
+         shim_batch      *sb   = r->sb;
+         if (r != keep && sb->pins == 0) {
+            if (pass == 0 && sb->full) {
+               rf_amd_batch_trim(sb->b, NULL);
+               const uint64 nb = rf_amd_batch_device_bytes(sb->b);
+               if (sb->entries) {
+                  g_registry_bytes -= sb->bytes - nb;
+               }
+               sb->bytes = nb;
+               sb->full  = 0;
+               g_registry_trims++;
+            } else if (pass == 1) {
+               registry_remove_locked(r, rl);
+               g_registry_evictions++;
+            }
          }
+         r = prev;
       }
-      r = prev;
    }
 }
 
@@ -988,44 +995,57 @@ lookup_many(cache *const          *ccs,
 }
 
 /* ---- async: queued states, completed by a completion thread ------------------------------ */
+/*
+ * Queued states form a lock-free stack (one compare-and-swap per enqueue, the link kept in
+ * the state's index_page local, which the shim's coroutine never uses otherwise). The
+ * completion thread takes the whole stack at once and answers it with one launch: batches
+ * size themselves -- what arrives during one GPU round trip goes out in the next. After a
+ * batch it spins briefly for more before sleeping on a condition variable; an enqueue onto
+ * an empty stack wakes it. RF_SHIM_ASYNC_WINDOW_US (default 0) makes it wait that long after
+ * the first arrival for up to RF_SHIM_ASYNC_BATCH states (default 1024) before taking them.
+ */
 static char g_queued_marker;
 #define ASYNC_STATE_QUEUED ((async_state)&g_queued_marker)
 typedef routing_filter_lookup_async_state rf_state;
 
-static struct {
-   pthread_mutex_t mu;
-   pthread_cond_t  cv;
-   rf_state      **q;
-   uint64          n, cap;
-   uint64          t_first; /* enqueue time of the oldest queued state (ns) */
-   int             urgent;
-} g_aq = {.mu = PTHREAD_MUTEX_INITIALIZER};
-static pthread_once_t g_aq_once = PTHREAD_ONCE_INIT;
-static uint64         g_async_batches, g_async_probes;
-static uint64         g_async_limit, g_async_window_ns;
+static rf_state      *g_aq_head;     /* the stack of queued states (atomic) */
+static uint64         g_aq_count;    /* states on it (atomic) */
+static int            g_aq_sleeping; /* the completion thread waits on g_aq_cv (atomic) */
+static pthread_mutex_t g_aq_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t  g_aq_cv;
+static pthread_once_t  g_aq_once = PTHREAD_ONCE_INIT;
+static uint64          g_async_batches, g_async_probes;
+static uint64          g_async_limit, g_async_window_ns;
 
-/* probe and complete n states (their filters in one launch); callbacks fire last per state */
+#define AQ_NEXT(st) (*(rf_state **)&(st)->index_page)
+
+/* probe and complete the n states of a taken stack (their filters in one launch); each
+ * state's callback fires after it is marked done */
 static void
-complete_states(rf_state **q, uint64 n)
+complete_states(rf_state *list, uint64 n)
 {
    if (n == 0) {
       return;
    }
+   rf_state             **q    = malloc(sizeof(*q) * n);
    cache               **ccs   = malloc(sizeof(*ccs) * n);
    const routing_config **cfgs = malloc(sizeof(*cfgs) * n);
    const routing_filter **fl   = malloc(sizeof(*fl) * n);
    uint32               *h     = malloc(sizeof(uint32) * n);
    uint64               *found = malloc(sizeof(uint64) * n);
    platform_status      *rc    = malloc(sizeof(*rc) * n);
-   platform_assert(ccs && cfgs && fl && h && found && rc);
-   for (uint64 i = 0; i < n; i++) {
-      ccs[i]  = q[i]->cc;
-      cfgs[i] = q[i]->cfg;
-      fl[i]   = &q[i]->filter;
-      h[i]    = q[i]->fp; /* the full 32-bit hash, stored when queued */
+   platform_assert(q && ccs && cfgs && fl && h && found && rc);
+   uint64 m = 0;
+   for (rf_state *st = list; st && m < n; st = AQ_NEXT(st)) {
+      q[m]   = st;
+      ccs[m] = st->cc;
+      cfgs[m] = st->cfg;
+      fl[m]  = &st->filter;
+      h[m]   = st->fp; /* the full 32-bit hash, stored when queued */
+      m++;
    }
-   lookup_many(ccs, cfgs, fl, h, n, found, rc);
-   for (uint64 i = 0; i < n; i++) {
+   lookup_many(ccs, cfgs, fl, h, m, found, rc);
+   for (uint64 i = 0; i < m; i++) {
       rf_state         *st  = q[i];
       async_callback_fn cb  = st->callback;
       void             *arg = st->callback_arg;
@@ -1038,7 +1058,8 @@ complete_states(rf_state **q, uint64 n)
       }
    }
    __atomic_fetch_add(&g_async_batches, 1, __ATOMIC_RELAXED);
-   __atomic_fetch_add(&g_async_probes, n, __ATOMIC_RELAXED);
+   __atomic_fetch_add(&g_async_probes, m, __ATOMIC_RELAXED);
+   free(q);
    free(ccs);
    free(cfgs);
    free(fl);
@@ -1047,16 +1068,18 @@ complete_states(rf_state **q, uint64 n)
    free(rc);
 }
 
-/* takes the whole queue (the caller holds g_aq.mu) */
-static rf_state **
-aq_take_locked(uint64 *n)
+/* takes every queued state: the stack's head and how many states it holds */
+static rf_state *
+aq_take(uint64 *n)
 {
-   rf_state **q = g_aq.q;
-   *n           = g_aq.n;
-   g_aq.q       = NULL;
-   g_aq.n = g_aq.cap = 0;
-   g_aq.urgent       = 0;
-   return q;
+   rf_state *list = __atomic_exchange_n(&g_aq_head, NULL, __ATOMIC_ACQUIRE);
+   uint64    c    = 0;
+   for (rf_state *st = list; st; st = AQ_NEXT(st)) {
+      c++;
+   }
+   __atomic_fetch_sub(&g_aq_count, c, __ATOMIC_RELAXED);
+   *n = c;
+   return list;
 }
 
 static void *
@@ -1065,25 +1088,37 @@ completion_main(void *arg)
    (void)arg;
    platform_ensure_thread_registered(); /* callbacks and cache_get (imports) run here */
    prctl(PR_SET_TIMERSLACK, 1UL, 0UL, 0UL, 0UL); /* microsecond waits, not the 50 us default slack */
-   pthread_mutex_lock(&g_aq.mu);
    for (;;) {
-      while (g_aq.n == 0) {
-         pthread_cond_wait(&g_aq.cv, &g_aq.mu);
-      }
-      while (g_aq.n > 0 && g_aq.n < g_async_limit && !g_aq.urgent) {
-         const uint64 deadline = g_aq.t_first + g_async_window_ns;
-         if (now_ns() >= deadline) {
-            break;
+      if (!__atomic_load_n(&g_aq_head, __ATOMIC_ACQUIRE)) {
+         /* a GPU round trip is ~10-20 us: spin that long for the next arrivals, then sleep */
+         const uint64 t0 = now_ns();
+         while (!__atomic_load_n(&g_aq_head, __ATOMIC_ACQUIRE) && now_ns() - t0 < 30000) {
+            __builtin_ia32_pause();
          }
-         struct timespec ts = {.tv_sec = deadline / 1000000000ull, .tv_nsec = deadline % 1000000000ull};
-         pthread_cond_timedwait(&g_aq.cv, &g_aq.mu, &ts);
+         pthread_mutex_lock(&g_aq_mu);
+         __atomic_store_n(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
+         while (!__atomic_load_n(&g_aq_head, __ATOMIC_SEQ_CST)) {
+            pthread_cond_wait(&g_aq_cv, &g_aq_mu);
+         }
+         __atomic_store_n(&g_aq_sleeping, 0, __ATOMIC_SEQ_CST);
+         pthread_mutex_unlock(&g_aq_mu);
       }
-      uint64     n;
-      rf_state **q = aq_take_locked(&n);
-      pthread_mutex_unlock(&g_aq.mu);
-      complete_states(q, n);
-      free(q);
-      pthread_mutex_lock(&g_aq.mu);
+      const uint64 window = __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED);
+      if (window) { /* optional coalescing window after the first arrival */
+         const uint64 deadline = now_ns() + window;
+         pthread_mutex_lock(&g_aq_mu);
+         while (__atomic_load_n(&g_aq_count, __ATOMIC_RELAXED) < __atomic_load_n(&g_async_limit, __ATOMIC_RELAXED)
+                && __atomic_load_n(&g_aq_head, __ATOMIC_ACQUIRE) && now_ns() < deadline
+                && __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED) == window)
+         {
+            struct timespec ts = {.tv_sec = deadline / 1000000000ull, .tv_nsec = deadline % 1000000000ull};
+            pthread_cond_timedwait(&g_aq_cv, &g_aq_mu, &ts);
+         }
+         pthread_mutex_unlock(&g_aq_mu);
+      }
+      uint64    n;
+      rf_state *list = aq_take(&n);
+      complete_states(list, n);
    }
    return NULL;
 }
@@ -1092,14 +1127,14 @@ static void
 aq_init(void)
 {
    g_async_limit     = env_u64("RF_SHIM_ASYNC_BATCH", 1024);
-   g_async_window_ns = env_u64("RF_SHIM_ASYNC_WINDOW_US", 20) * 1000;
+   g_async_window_ns = env_u64("RF_SHIM_ASYNC_WINDOW_US", 0) * 1000;
    if (g_async_limit == 0) {
       g_async_limit = 1;
    }
    pthread_condattr_t ca;
    pthread_condattr_init(&ca);
    pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
-   pthread_cond_init(&g_aq.cv, &ca);
+   pthread_cond_init(&g_aq_cv, &ca);
    pthread_condattr_destroy(&ca);
    pthread_attr_t at;
    pthread_attr_init(&at);
@@ -1109,28 +1144,31 @@ aq_init(void)
    pthread_attr_destroy(&at);
 }
 
+static void
+aq_wake(void)
+{
+   pthread_mutex_lock(&g_aq_mu);
+   pthread_cond_signal(&g_aq_cv);
+   pthread_mutex_unlock(&g_aq_mu);
+}
+
 /* probe every state queued so far, in the caller's thread */
 void
 routing_filter_amd_flush(void)
 {
    pthread_once(&g_aq_once, aq_init);
-   pthread_mutex_lock(&g_aq.mu);
-   uint64     n;
-   rf_state **q = aq_take_locked(&n);
-   pthread_mutex_unlock(&g_aq.mu);
-   complete_states(q, n);
-   free(q);
+   uint64    n;
+   rf_state *list = aq_take(&n);
+   complete_states(list, n);
 }
 
 void
 routing_filter_amd_async_config(uint64 batch, uint64 window_us)
 {
    pthread_once(&g_aq_once, aq_init);
-   pthread_mutex_lock(&g_aq.mu);
-   g_async_limit     = batch ? batch : 1;
-   g_async_window_ns = window_us * 1000;
-   pthread_cond_signal(&g_aq.cv); /* the completion thread re-reads them */
-   pthread_mutex_unlock(&g_aq.mu);
+   __atomic_store_n(&g_async_limit, batch ? batch : 1, __ATOMIC_RELAXED);
+   __atomic_store_n(&g_async_window_ns, window_us * 1000, __ATOMIC_RELAXED);
+   aq_wake(); /* a waiting completion thread re-reads them */
 }
 
 void
@@ -1151,7 +1189,9 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
       /* a polling owner: probe what is queued now, in this thread (this state among them,
          unless the completion thread already holds it). RUNNING either way -- the state's
          callback may have fired; the next call returns DONE */
-      routing_filter_amd_flush();
+      if (__atomic_load_n(&g_aq_head, __ATOMIC_RELAXED)) {
+         routing_filter_amd_flush();
+      }
       return ASYNC_STATUS_RUNNING;
    }
    /* ASYNC_STATE_INIT (:898-905) */
@@ -1164,21 +1204,17 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    pthread_once(&g_aq_once, aq_init);
    state->fp                     = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
    state->__async_state_stack[0] = ASYNC_STATE_QUEUED;
-   pthread_mutex_lock(&g_aq.mu);
-   if (g_aq.n == g_aq.cap) {
-      g_aq.cap = g_aq.cap ? 2 * g_aq.cap : 1024;
-      g_aq.q   = realloc(g_aq.q, sizeof(*g_aq.q) * g_aq.cap);
-      platform_assert(g_aq.q != NULL);
-   }
-   g_aq.q[g_aq.n++] = state;
-   if (g_aq.n == 1) {
-      g_aq.t_first = now_ns();
-      pthread_cond_signal(&g_aq.cv);
-   } else if (g_aq.n == g_async_limit) {
-      pthread_cond_signal(&g_aq.cv);
-   }
-   pthread_mutex_unlock(&g_aq.mu);
+   rf_state *old = __atomic_load_n(&g_aq_head, __ATOMIC_RELAXED);
+   do {
+      AQ_NEXT(state) = old;
+   } while (!__atomic_compare_exchange_n(&g_aq_head, &old, state, 1, __ATOMIC_SEQ_CST, __ATOMIC_RELAXED));
    /* the state may already be complete (another thread): it is not read again here */
+   const uint64 c = __atomic_add_fetch(&g_aq_count, 1, __ATOMIC_RELAXED);
+   if ((old == NULL && __atomic_load_n(&g_aq_sleeping, __ATOMIC_SEQ_CST))
+       || (c == __atomic_load_n(&g_async_limit, __ATOMIC_RELAXED) && __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED)))
+   {
+      aq_wake();
+   }
    return ASYNC_STATUS_RUNNING;
 }
 

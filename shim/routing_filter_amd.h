@@ -9,9 +9,9 @@
 
 /* probe every routing_filter_lookup_async state queued so far in the caller's thread (one
  * GPU launch over every filter they name), complete them and fire their callbacks. Queued
- * states also complete on their own: the shim's completion thread probes the queue once
- * RF_SHIM_ASYNC_BATCH states (default 1024) are queued or the oldest has waited
- * RF_SHIM_ASYNC_WINDOW_US (default 20) microseconds */
+ * states also complete on their own: the shim's completion thread takes the whole queue
+ * whenever it is free (what arrived during its previous GPU round trip), waiting up to
+ * RF_SHIM_ASYNC_WINDOW_US (default 0) microseconds for RF_SHIM_ASYNC_BATCH states */
 void
 routing_filter_amd_flush(void);
 

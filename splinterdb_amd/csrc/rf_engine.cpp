@@ -988,7 +988,9 @@ static int env_mode(const char* name, const char* a, const char* b) {
   if (!v) return 0;
   return !strcmp(v, a) ? 1 : (!strcmp(v, b) ? 2 : 0);
 }
-static const uint64_t MAPPED_MAX_PROBES = 2048;
+// measured on MI355X (profiles/r03_probe_latency.txt): reading the inputs over PCIe from the
+// kernel beats one H2D copy first up to at least 8,192 probes (17.7 vs 34.9 us per round trip)
+static const uint64_t MAPPED_MAX_PROBES = 32768;
 
 // The common body: n probes, probe i in group h_group[i] (NULL: group 0) of the ng-entry group
 // table, results into h_found. Waits for any work still queued on the engine stream (builds
@@ -1601,13 +1603,20 @@ extern "C" uint64_t rf_amd_max_fingerprints(const rf_amd_config* cfg) {
   return 2ull * addrs_per_extent * (1ull << cfg->log_index_size) - 1;
 }
 
+// src/routing_filter.c:1119-1139 as the reference's release build evaluates it (-O3
+// -ffast-math, Makefile:89,123-124: GCC reassociates the sum into two fused multiply-adds and
+// truncates through 64 bits). The order decides the result where the exact value is an
+// integer (num_unique = 1: exactly 1 there, 0 in source order); oracle/rf_oracle.c holds the
+// same restatement, pinned against the reference for fingerprint sizes 8-32.
 extern "C" uint32_t rf_amd_estimate_unique_keys_from_count(const rf_amd_config* cfg, uint64_t num_unique) {
+#pragma clang fp contract(off)
   const double U = (double)(1ull << cfg->fingerprint_size);
-  const double unseen = U - (double)num_unique;
-  const double U2 = U * U, U4 = U2 * U2, s2 = unseen * unseen, s4 = s2 * s2;
-  const double hd = log(U) - log(unseen) + 0.5 * (1 / U - 1 / unseen) - (1 / 12.0) * (1 / U2 - 1 / s2) +
-                    (1 / 120.0) * (1 / U4 - 1 / s4);
-  return (uint32_t)(U * hd);
+  const double s = U - (double)num_unique;
+  const double U2 = U * U, s2 = s * s;
+  const double lU = log(U), ls = log(s);
+  const double a = fma(1.0 / U - 1.0 / s, 0.5, (1.0 / s2 - 1.0 / U2) * (1.0 / 12.0));
+  const double b = fma(1.0 / (U2 * U2) - 1.0 / (s2 * s2), 1.0 / 120.0, lU);
+  return (uint32_t)(int64_t)(U * ((a + b) - ls));
 }
 
 extern "C" uint64_t rf_amd_space_use_bytes(const rf_amd_config* cfg, uint32_t num_pages) {

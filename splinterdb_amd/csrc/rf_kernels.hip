@@ -551,6 +551,33 @@ __device__ __forceinline__ void sort16(T (&x)[16]) {  // Batcher odd-even merge,
 #undef CE
 }
 
+// Sorts a[0, cnt) with the whole workgroup (NT threads; a in LDS or global memory): Batcher's
+// odd-even merge sort network over the next power of two, the elements past cnt taken as +inf
+// (every comparator is ascending, so those never swap and are skipped). O(cnt log^2 cnt)
+// comparisons in log(n)(log(n)+1)/2 barrier-separated stages: a bucket of 12K duplicates of a
+// few distinct (fingerprint, value) entries -- quadratic for the per-bin insertion sort this
+// replaces -- sorts in 105 stages.
+template <typename T, int NT>
+__device__ void oe_sort_group(T* a, uint32_t cnt) {
+  uint32_t n = 1;
+  while (n < cnt) n <<= 1;
+  for (uint32_t p = 1; p < n; p <<= 1) {
+    for (uint32_t k = p; k >= 1; k >>= 1) {
+      const uint32_t r = k & (p - 1);
+      for (uint32_t L = threadIdx.x; L + k < cnt; L += NT) {
+        if (L >= r && ((L - r) & (2 * k - 1)) < k && (L / (2 * p)) == ((L + k) / (2 * p))) {
+          const T x = a[L], y = a[L + k];
+          if (y < x) {
+            a[L] = y;
+            a[L + k] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // Finish a sorted coarse bucket held in `B` (LDS or global): write per-index counts and
 // starts, the compacted entries, and the num_unique contribution. Shared by K4 and K4b.
 struct CbCtx {
@@ -796,47 +823,31 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   }
   __syncthreads();
   if (s_nbig) {
+    // bins over 8 entries: those of at most 64 ranked by one wave each; larger ones
+    // (duplicate-heavy input) sorted one after another by the whole workgroup. More than
+    // BIG_LIST of them: every bin is visited (the list holds only the first BIG_LIST)
     const uint32_t nb = s_nbig;
-    if (nb <= BIG_LIST) {
-      const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
-      for (uint32_t q = wv; q < nb; q += SORT_NT / WAVE) {
-        const uint32_t b = s_big[q], st = s_bin[b], cnt = s_bin[b + 1] - st;
-        if (cnt <= WAVE) {
-          EntT mine = lane < cnt ? s_b[st + lane] : EntT(0);
-          uint32_t before = 0;
-          for (uint32_t j = 0; j < cnt; j++) {
-            const EntT y = s_b[st + j];  // same address in every lane: a broadcast
-            before += (y < mine || (y == mine && j < lane)) ? 1u : 0u;
-          }
-          __builtin_amdgcn_wave_barrier();  // all reads of the bin before any write
-          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-          if (lane < cnt) s_b[st + before] = mine;
-        } else if (lane == 0) {  // > 64 entries in one bucket: insertion sort
-          for (uint32_t i = st + 1; i < st + cnt; i++) {
-            const EntT y = s_b[i];
-            uint32_t j = i;
-            while (j > st && s_b[j - 1] > y) {
-              s_b[j] = s_b[j - 1];
-              j--;
-            }
-            s_b[j] = y;
-          }
+    const bool listed = nb <= BIG_LIST;
+    const uint32_t nq = listed ? nb : nbins;
+    const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+    for (uint32_t q = wv; q < nq; q += SORT_NT / WAVE) {
+      const uint32_t b = listed ? s_big[q] : q, st = s_bin[b], cnt = s_bin[b + 1] - st;
+      if (cnt > 8 && cnt <= WAVE) {
+        EntT mine = lane < cnt ? s_b[st + lane] : EntT(0);
+        uint32_t before = 0;
+        for (uint32_t j = 0; j < cnt; j++) {
+          const EntT y = s_b[st + j];  // same address in every lane: a broadcast
+          before += (y < mine || (y == mine && j < lane)) ? 1u : 0u;
         }
+        __builtin_amdgcn_wave_barrier();  // all reads of the bin before any write
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        if (lane < cnt) s_b[st + before] = mine;
       }
-    } else {  // many large bins (duplicate-heavy input): insertion sort each
-      for (uint32_t b = threadIdx.x; b < nbins; b += SORT_NT) {
-        const uint32_t st = s_bin[b], en = s_bin[b + 1];
-        if (en - st <= 8) continue;
-        for (uint32_t i = st + 1; i < en; i++) {
-          const EntT y = s_b[i];
-          uint32_t j = i;
-          while (j > st && s_b[j - 1] > y) {
-            s_b[j] = s_b[j - 1];
-            j--;
-          }
-          s_b[j] = y;
-        }
-      }
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < nq; q++) {  // workgroup-uniform
+      const uint32_t b = listed ? s_big[q] : q, st = s_bin[b], cnt = s_bin[b + 1] - st;
+      if (cnt > WAVE) oe_sort_group<EntT, SORT_NT>(s_b + st, cnt);
     }
     __syncthreads();
   }
@@ -844,6 +855,129 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
   DBG_PHASE(4);
+  if constexpr (DUAL) {
+    // 32-bit incremental builds: every entry's place in the merged, deduplicated order is
+    // computed directly and written straight to the output -- old entries are always kept,
+    // a new entry is dropped iff it equals the previous new one (src/routing_filter.c:465-494
+    // dedupes the new run before the merge, :546-597 merges old first on ties). A = the sorted
+    // new run s_b[0, nsort) (flagged odd), B = the old run s_b[nsort, n) (flagged even): a
+    // flagged comparison orders an old entry before a new one of equal e.
+    static_assert(sizeof(EntT) == 4, "DUAL entries are 32-bit");
+    const uint32_t na = nsort, nb = n - nsort;
+    uint32_t* Ak = reinterpret_cast<uint32_t*>(s_b);  // A, then its kept entries compacted
+    const uint32_t* B = Ak + nsort;
+    // (1) the new run: thread t owns A[t*ca, t*ca + ca); a new entry is kept unless it equals
+    // its predecessor in A
+    const uint32_t ca = (na + SORT_NT - 1) / SORT_NT;  // <= PER
+    const uint32_t a0 = threadIdx.x * ca;
+    uint32_t x[PER];
+    uint32_t kmask = 0, kc = 0;
+    {
+      uint32_t pa = (a0 > 0 && a0 <= na) ? Ak[a0 - 1] : 0u;  // flagged new values are odd: 0 matches none
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        const uint32_t a = a0 + k;
+        x[k] = 0;
+        if ((uint32_t)k < ca && a < na) {
+          x[k] = Ak[a];
+          if (a == 0 || x[k] != pa) {
+            kmask |= 1u << k;
+            kc++;
+          }
+          pa = x[k];
+        }
+      }
+    }
+    uint32_t nkept;
+    const uint32_t kbase = block_excl_scan<SORT_NT>(kc, s_tmp, &nkept);  // barriers: A is read
+    {
+      uint32_t r = kbase;
+#pragma unroll
+      for (int k = 0; k < PER; k++)
+        if (kmask >> k & 1u) Ak[r++] = x[k];  // r < nsort: B untouched
+    }
+    __syncthreads();
+    uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
+    const uint32_t FPNONE = 0xffffffffu >> P.vs;
+    auto fp_of = [&](uint32_t v) { return (v >> 1) >> P.vs; };
+    auto ix_of = [&](uint32_t v) { return ish >= 32 ? 0u : (((v >> 1) >> ish) & (ipc - 1)); };
+    auto lower = [](const uint32_t* arr, uint32_t len, uint32_t v) {  // elements < v
+      uint32_t lo = 0, hi = len;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (arr[m] < v) lo = m + 1; else hi = m;
+      }
+      return lo;
+    };
+    // num_unique (:558, :572-574): an entry counts when its fingerprint differs from its
+    // merged predecessor's in the same index (UINT32_MAX >> value_size at an index's start);
+    // the predecessor is the larger of the previous kept new entry and the previous old one
+    auto counts = [&](uint32_t v, bool hp, uint32_t p) -> uint32_t {
+      const uint32_t pfp = (hp && ix_of(p) == ix_of(v)) ? fp_of(p) : FPNONE;
+      return fp_of(v) != pfp ? 1u : 0u;
+    };
+    uint32_t uniq = 0;
+    // (2) kept new entries: merged position = kept rank + old entries before it
+    {
+      uint32_t r = kbase;
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        if (kmask >> k & 1u) {
+          const uint32_t v = x[k], j = lower(B, nb, v);
+          dst[r + j] = v >> 1;
+          bool hp = r > 0;
+          uint32_t p = hp ? Ak[r - 1] : 0u;
+          if (j > 0 && (!hp || B[j - 1] > p)) { p = B[j - 1]; hp = true; }
+          uniq += counts(v, hp, p);
+          r++;
+        }
+      }
+    }
+    // (3) old entries: thread t owns B[t*cbn, t*cbn + cbn) (odd stride: distinct LDS banks);
+    // merged position = own index + kept new entries before it (walked forward)
+    {
+      const uint32_t cbn = ((nb + SORT_NT - 1) / SORT_NT) | 1u;
+      const uint32_t j0 = threadIdx.x * cbn, j1 = min(j0 + cbn, nb);
+      if (j0 < nb) {
+        uint32_t i = lower(Ak, nkept, B[j0]);
+        for (uint32_t j = j0; j < j1; j++) {
+          const uint32_t v = B[j];
+          while (i < nkept && Ak[i] < v) i++;
+          dst[j + i] = v >> 1;
+          bool hp = j > 0;
+          uint32_t p = hp ? B[j - 1] : 0u;
+          if (i > 0 && (!hp || Ak[i - 1] > p)) { p = Ak[i - 1]; hp = true; }
+          uniq += counts(v, hp, p);
+        }
+      }
+    }
+    // (4) per index: bounds, and its smallest old entry (the num_unique put-back quirk, K5)
+    auto first_of = [&](const uint32_t* arr, uint32_t len, uint32_t l) {  // first entry of index >= l
+      uint32_t lo = 0, hi = len;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (ix_of(arr[m]) < l) lo = m + 1; else hi = m;
+      }
+      return lo;
+    };
+    for (uint32_t l = threadIdx.x; l < ipc; l += SORT_NT) {
+      const uint32_t as = first_of(Ak, nkept, l), bs = first_of(B, nb, l);
+      const uint32_t ae = l + 1 < ipc ? first_of(Ak, nkept, l + 1) : nkept;
+      const uint32_t be = l + 1 < ipc ? first_of(B, nb, l + 1) : nb;
+      idx_cnt[c.idx0 + l] = (ae - as) + (be - bs);
+      idx_start[c.idx0 + l] = c.cb_rel + as + bs;
+      first_old[c.idx0 + l] = be > bs ? B[bs] >> 1 : 0xffffffffu;
+      has_old[c.idx0 + l] = be > bs ? 1u : 0u;
+    }
+    uint32_t tot_uniq;
+    block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
+    if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
+    DBG_PHASE(5);
+    DBG_PHASE(6);
+    DBG_PHASE(7);
+    DBG_PHASE(8);
+    return;
+  }
   // dedupe + compaction: thread t owns the contiguous run [t*drun, t*drun + drun), drun =
   // ceil(n / SORT_NT) made odd (lanes drun words apart fall on distinct LDS banks) and
   // capped at PER: every thread takes a share of a small bucket, not half of them PER each
@@ -1038,8 +1172,11 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
       tmp[atomicAdd(&s_cur[bsh >= 32 ? 0u : ((e >> bsh) & bmask)], 1u)] = x;
     }
     __syncthreads();
+    // order inside each bin: small bins by one thread each (insertion sort of at most 64),
+    // larger ones (duplicate-heavy) by the whole workgroup, one after another
     for (uint32_t b = threadIdx.x; b < nbins; b += BIG_NT) {
       const uint32_t s = s_bin[b], e = s_bin[b + 1];
+      if (e - s > WAVE) continue;
       for (uint32_t i = s + 1; i < e; i++) {
         const EntT x = tmp[i];
         uint32_t j = i;
@@ -1049,6 +1186,11 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
         }
         tmp[j] = x;
       }
+    }
+    __syncthreads();
+    for (uint32_t b = 0; b < nbins; b++) {  // workgroup-uniform
+      const uint32_t s = s_bin[b], cnt = s_bin[b + 1] - s;
+      if (cnt > WAVE) oe_sort_group<EntT, BIG_NT>(tmp + s, cnt);
     }
     __syncthreads();
     if (threadIdx.x == 0) s_run = 0;

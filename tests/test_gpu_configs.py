@@ -195,3 +195,37 @@ def test_bench_two_ranks_equal_one_process(tmp_path, workload, filters):
     with open(f"{d1}.rank0") as fh:
         one = json.load(fh)
     assert len(one) == total and two == one
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_shape_sampled_against_reference(ref):
+    """BASELINE C5 at bench.py's shape: 8 filters x 2^21 variable-length (8-100 B) keys built
+    in one batch from device-resident bytes, then bench.py's probe stream (K.c5_inputs:
+    Zipf(0.99) positives + 10 % negatives, shuffled over the filters). Filters 0 and 5 must be
+    byte-identical to the reference's own routing_filter_add of the same keys (its
+    data_key_hash over the bytes), and 100k probes of each equal to its routing_filter_lookup."""
+    if ref is None:
+        pytest.skip("oracle/_ref/libref_rf.so not built")
+    F, n = 8, 1 << 21
+    w = K.c5_inputs(F, n, seed=0x5EED)
+    cfg = E.routing_config_init()
+    b = E.FilterBatch(cfg, [n] * F)
+    b.build_var_keys(dev(w["bytes"]), dev(w["offs"].view(np.int64)))
+    P = int(w["probe_fid"].size)
+    found = torch.empty(P, dtype=torch.int64, device="cuda:0")
+    b.probe_var_keys(dev(w["probe_bytes"]), dev(w["probe_offs"].view(np.int64)), dev(w["probe_fid"].view(np.int32)),
+                     P, found)
+    torch.cuda.synchronize()
+    got = found.cpu().numpy().view(np.uint64)
+    assert ((got[w["positive"]] & np.uint64(1)) == 1).all()
+    offs = w["offs"]
+    for f in (0, 5):
+        lo, hi = int(offs[f * n]), int(offs[(f + 1) * n])
+        desc = ref.add(ref.hash_var_keys(w["bytes"][lo:hi], offs[f * n:(f + 1) * n + 1] - np.uint64(lo)))
+        ir, img = ref.image(desc), b.image(f)
+        assert (img.num_unique, img.num_pages) == (ir.num_unique, ir.num_pages), f
+        assert (img.pages == ir.pages).all() and (img.slots == ir.slots).all(), f
+        sel = np.nonzero(w["probe_fid"] == f)[0][:100_000]
+        pb, po = K.gather_var(w["probe_bytes"], w["probe_offs"], sel)
+        assert (got[sel] == ref.lookup_var_keys(desc, pb, po)).all(), f
+        ref.dec_ref(desc)

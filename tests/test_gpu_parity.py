@@ -493,3 +493,54 @@ def test_sparse_blocks_at_max_indices(oracle):
         assert (img.num_unique, img.num_pages) == (of.num_unique, of.num_pages), distinct
         assert (img.pages == of.pages()).all(), distinct
         assert (img.slots == of.slots()[: of.num_indices]).all(), distinct
+
+
+def _clustered_hashes(rng, n_rand, n_clu, lnb, fp_size=26):
+    """n_rand uniform hashes + n_clu whose fingerprints all fall in ONE filter bucket with
+    random remainders (many distinct entries in one bucket, in random order)"""
+    rem = fp_size - lnb
+    bucket = int(rng.integers(0, 1 << lnb))
+    fp = (np.uint64(bucket) << np.uint64(rem)) | rng.integers(0, 1 << rem, size=n_clu, dtype=np.uint64)
+    low = rng.integers(0, 1 << (32 - fp_size), size=n_clu, dtype=np.uint64)
+    clu = ((fp << np.uint64(32 - fp_size)) | low).astype(np.uint32)
+    h = np.concatenate([rng.integers(0, 1 << 32, size=n_rand, dtype=np.uint64).astype(np.uint32), clu])
+    return rng.permutation(h).astype(np.uint32)
+
+
+@pytest.mark.parametrize("n_rand,n_clu", [(8000, 12000), (16000, 4000)])
+def test_big_bucket_of_distinct_entries_sorts_fast(oracle, n_rand, n_clu):
+    """One filter bucket holding 12,000 (resp. 4,000) entries with random remainders: the
+    coarse bucket overflows LDS (K4b, 12,000) or stays in LDS (4,000). Such a bucket used to
+    be ordered by a per-bucket insertion sort -- quadratic, seconds at 12K; the whole
+    workgroup now sorts it with an odd-even merge network. Bit-exact against the oracle, and
+    fresh plus incremental builds finish in well under a second."""
+    import time
+    rng = np.random.default_rng(n_clu)
+    cfg = E.routing_config_init()
+    ocfg = oracle.make_config()
+    n = n_rand + n_clu  # 20,000: log_num_buckets 14
+    h = _clustered_hashes(rng, n_rand, n_clu, 14)
+    b = E.FilterBatch(cfg, [n], [2])
+    b.build_hashes(dev(h))  # warm: the kernels load once
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    b.build_hashes(dev(h))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    img = b.image(0)
+    of = oracle.filter_add(ocfg, h, value=2)
+    assert (img.num_unique, img.num_pages) == (of.num_unique, of.num_pages)
+    assert (img.pages == of.pages()).all() and (img.slots == of.slots()[: of.num_indices]).all()
+    assert dt < 0.2, dt
+    # incremental: the new entries cluster in the same kind of bucket (only the new run is sorted)
+    h2 = _clustered_hashes(rng, n_rand // 2, n_clu, 15)
+    b2 = E.FilterBatch(cfg, [h2.size], [5], old=[(b, 0)])
+    t = time.perf_counter()
+    b2.build_hashes(dev(h2))
+    torch.cuda.synchronize()
+    dt2 = time.perf_counter() - t
+    img2 = b2.image(0)
+    of2 = oracle.filter_add(ocfg, h2, value=5, old=of)
+    assert (img2.num_unique, img2.num_pages) == (of2.num_unique, of2.num_pages)
+    assert (img2.pages == of2.pages()).all() and (img2.slots == of2.slots()[: of2.num_indices]).all()
+    assert dt2 < 0.5, dt2

@@ -239,7 +239,7 @@ def test_one_launch_per_flush_over_512_filters(pair):
         got, cb = shim.lookup_keys_async_flush(descs_s, probe, fid)
         b1, p1 = shim.async_stats()
     finally:
-        shim.async_config(1024, 20)
+        shim.async_config(1024, 0)
     assert cb == P
     assert (b1 - b0, p1 - p0) == (1, P)
     assert (got == want).all()

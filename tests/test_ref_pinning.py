@@ -263,19 +263,25 @@ def test_header_inlines_match_python_mirror():
 def test_estimate_unique_keys_from_count_matches_reference(stacks, oracle):
     """routing_filter_estimate_unique_keys_from_count (src/routing_filter.c:1119-1139) is the
     one floating-point function on the path: a double harmonic-number difference truncated
-    to uint32. Tolerance: 1 key. The reference's release build (-O3 -ffast-math, its
-    Makefile:89) reassociates the logs, so for tiny counts it truncates 0.99999 up to 1
-    where a strict-IEEE build (the restatement, the engine's host helper) gives 0; at every
-    realistic count the two agree exactly."""
-    for fps, lis in ((26, 8), (20, 9), (32, 8)):
+    to uint32. The reference's release build (-O3 -ffast-math, its Makefile:89) reassociates
+    the sum into two fused multiply-adds, which decides the truncation where the exact value
+    is an integer (num_unique = 1 -> exactly 1: 1 there, 0 in source order). The restatement
+    (oracle/rf_oracle.c) and the engine's host helper (librf_amd.so, no GPU call) evaluate it
+    in the reference build's order: bit-exact (tolerance 0) on every count tried."""
+    import ctypes
+    from splinterdb_amd import engine as E
+    L = E.load_library()
+    rng = np.random.default_rng(12)
+    for fps, lis in ((26, 8), (20, 9), (32, 8), (24, 8), (30, 10), (18, 6)):
         s = stacks(fps, lis)
         ocfg = oracle.make_config(fingerprint_size=fps, log_index_size=lis)
-        for u in (0, 1, 2, 3, 1000, 992680, 4254486, (1 << (fps - 1)), (1 << fps) - 2):
-            got = oracle.lib().rfo_estimate_unique_keys_from_count(ocfg, u)
+        ecfg = E.routing_config_init(fingerprint_size=fps, log_index_size=lis).c()
+        us = list(range(0, 2000)) + [992680, 4254486, (1 << (fps - 1)), (1 << fps) - 2] + \
+            [int(x) for x in rng.integers(0, (1 << fps) - 1, size=2000, dtype=np.uint64)]
+        for u in us:
             want = s.estimate_unique_keys_from_count(u)
-            assert abs(int(got) - int(want)) <= 1, (fps, u, got, want)
-            if u >= 1000:
-                assert got == want, (fps, u)
+            assert oracle.lib().rfo_estimate_unique_keys_from_count(ocfg, u) == want, (fps, u)
+            assert L.rf_amd_estimate_unique_keys_from_count(ctypes.byref(ecfg), u) == want, (fps, u)
 
 
 # ---- the reference's static helpers, called one by one -----------------------------------
