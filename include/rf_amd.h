@@ -120,6 +120,14 @@ int rf_amd_batch_probe_hashes_runs(rf_amd_batch *b, const uint32_t *d_hashes, co
  * thread-safe and concurrent callers run concurrently. Batches must be built (a build issued
  * on the engine stream is waited for). */
 int rf_amd_batch_build_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes);
+/* the same in two steps, for callers that fill the pinned staging buffer themselves (e.g.
+ * each thread of a coalesced add copying its own fingerprints, in parallel): stage_begin
+ * takes the engine's staging buffer (filter f's hashes at its run offset, runs in filter
+ * order) and returns its host address; stage_build uploads it, builds, waits and releases
+ * it; stage_abort releases it without building. */
+int  rf_amd_batch_stage_begin(rf_amd_batch *b, uint32_t **h_stage);
+int  rf_amd_batch_stage_build(rf_amd_batch *b);
+void rf_amd_batch_stage_abort(rf_amd_batch *b);
 int rf_amd_batch_probe_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes, const uint32_t *h_filter_id,
                                    uint64_t n, uint64_t *h_found);
 /* lookups against many resident filters -- of any batches of the engine -- in ONE launch:

@@ -503,6 +503,24 @@ count_callback(void *arg)
  * callbacks fired; *running = states whose first call returned ASYNC_STATUS_RUNNING.
  * filter_id[i] picks the filter of key i from filters[].
  */
+/* phases of the last rfr_lookup_keys_async_many call (ns): starting every state, polling */
+static uint64 g_many_ns[2];
+
+void
+rfr_async_many_phases(uint64 *out)
+{
+   out[0] = g_many_ns[0];
+   out[1] = g_many_ns[1];
+}
+
+static uint64
+mono_ns(void)
+{
+   struct timespec ts;
+   clock_gettime(CLOCK_MONOTONIC, &ts);
+   return (uint64)ts.tv_sec * 1000000000ull + (uint64)ts.tv_nsec;
+}
+
 uint64
 rfr_lookup_keys_async_many(rfr_stack      *s,
                            routing_filter *filters,
@@ -516,6 +534,7 @@ rfr_lookup_keys_async_many(rfr_stack      *s,
    routing_filter_lookup_async_state *st = calloc(n ? n : 1, sizeof(*st));
    uint64                             cb = 0;
    *running                              = 0;
+   const uint64                       t0 = mono_ns();
    for (uint64 i = 0; i < n; i++) {
       key k = key_create(FALSE, key_len, keys + i * key_len);
       routing_filter_lookup_async_state_init(&st[i], (cache *)&s->cc, &s->rcfg,
@@ -525,6 +544,7 @@ rfr_lookup_keys_async_many(rfr_stack      *s,
          (*running)++;
       }
    }
+   const uint64 t1 = mono_ns();
    for (uint64 i = 0; i < n; i++) {
       while (routing_filter_lookup_async(&st[i]) != ASYNC_STATUS_DONE) {
          cache_cleanup((cache *)&s->cc);
@@ -533,6 +553,8 @@ rfr_lookup_keys_async_many(rfr_stack      *s,
          found[i] = UINT64_MAX;
       }
    }
+   g_many_ns[0] = t1 - t0;
+   g_many_ns[1] = mono_ns() - t1;
    /* a state can be seen DONE just before its callback runs (on the completing thread):
       every state that yielded gets exactly one callback, so wait for those */
    while (__atomic_load_n(&cb, __ATOMIC_ACQUIRE) < *running) {
@@ -579,16 +601,21 @@ rfr_registry_set_limit(uint64 mib)
    return 1;
 }
 
-/* out[0..4] = add batches, filters added, registry bytes, evictions, trims; 0 without a shim */
+__attribute__((weak)) uint64
+routing_filter_amd_async_probe_ns(void);
+
+/* out[0..5] = add batches, filters added, registry bytes, evictions, trims, ns spent probing
+ * queued async states; 0 without a shim */
 int
 rfr_shim_stats(uint64 *out)
 {
-   memset(out, 0, 5 * sizeof(uint64));
+   memset(out, 0, 6 * sizeof(uint64));
    if (!routing_filter_amd_add_stats) {
       return 0;
    }
    routing_filter_amd_add_stats(&out[0], &out[1]);
    routing_filter_amd_registry_stats(&out[2], &out[3], &out[4]);
+   out[5] = routing_filter_amd_async_probe_ns();
    return 1;
 }
 

@@ -102,6 +102,8 @@ def lib(path=LIB_PATH):
         L.rfr_lookup_keys_async_driven.restype = i32
         L.rfr_mt_chains.argtypes = [vp, vp, u32, u32, u32, u64, vp, u64, vp, vp, vp, vp]
         L.rfr_mt_chains.restype = i32
+        L.rfr_async_many_phases.argtypes = [vp]
+        L.rfr_async_many_phases.restype = None
         L.rfr_shim_stats.argtypes = [vp]
         L.rfr_shim_stats.restype = i32
         L.rfr_registry_set_limit.argtypes = [u64]
@@ -388,10 +390,17 @@ class Stack:
     def shim_stats(self):
         """the shim's add batches / filters, registry bytes / evictions / trims (None for
         the reference's library)"""
-        out = np.zeros(5, dtype=np.uint64)
+        out = np.zeros(6, dtype=np.uint64)
         if not self.L.rfr_shim_stats(_p(out)):
             return None
-        return dict(zip(("add_batches", "add_filters", "registry_bytes", "evictions", "trims"), (int(x) for x in out)))
+        return dict(zip(("add_batches", "add_filters", "registry_bytes", "evictions", "trims", "async_probe_ns"),
+                        (int(x) for x in out)))
+
+    def async_many_phases(self):
+        """(start, poll) nanoseconds of the last lookup_keys_async_many call"""
+        out = np.zeros(2, dtype=np.uint64)
+        self.L.rfr_async_many_phases(_p(out))
+        return int(out[0]), int(out[1])
 
     def registry_set_limit(self, mib):
         return bool(self.L.rfr_registry_set_limit(mib))

@@ -574,6 +574,10 @@ typedef struct add_req {
    uint32             f;
    int                done;
    struct add_req    *next;
+   /* staging: where this request's fingerprints go in the engine's pinned buffer; whichever
+      thread claims the copy first (the request's own thread, or the combiner) makes it */
+   uint32            *stage_dst;
+   int                claim, copied; /* atomic */
 } add_req;
 
 static pthread_mutex_t g_add_mu = PTHREAD_MUTEX_INITIALIZER;
@@ -581,6 +585,16 @@ static pthread_cond_t  g_add_cv = PTHREAD_COND_INITIALIZER;
 static add_req        *g_add_head, *g_add_tail;
 static int             g_add_busy;
 static uint64          g_add_batches, g_add_filters;
+
+/* copies a request's fingerprints into its staging slot, unless another thread has claimed it */
+static void
+add_copy(add_req *q)
+{
+   if (q->stage_dst && __atomic_exchange_n(&q->claim, 1, __ATOMIC_ACQ_REL) == 0) {
+      memcpy(q->stage_dst, q->hashes, sizeof(uint32) * q->n);
+      __atomic_store_n(&q->copied, 1, __ATOMIC_RELEASE);
+   }
+}
 
 /* builds k requests of one config as one batch; a batch that cannot be created (one
  * request's geometry, or memory) is retried request by request so each gets its own error */
@@ -623,22 +637,30 @@ run_adds(rf_amd_engine *e, add_req **rq, uint32 k)
       rq[0]->rc = r;
       return;
    }
-   uint32 *h = NULL;
-   if (k == 1) {
-      h = (uint32 *)rq[0]->hashes; /* not modified */
-   } else {
-      h = malloc(sizeof(uint32) * (total ? total : 1));
-      platform_assert(h != NULL);
+   /* the fingerprints go straight into the engine's pinned staging buffer, each request's
+      copy made by its own waiting thread or by this one, whichever claims it first */
+   uint32 *stage = NULL;
+   r             = rf_amd_batch_stage_begin(b, &stage);
+   if (!r) {
+      pthread_mutex_lock(&g_add_mu);
       uint64 at = 0;
       for (uint32 i = 0; i < k; i++) {
-         memcpy(h + at, rq[i]->hashes, sizeof(uint32) * rq[i]->n);
+         rq[i]->stage_dst = stage + at;
          at += rq[i]->n;
       }
+      pthread_cond_broadcast(&g_add_cv);
+      pthread_mutex_unlock(&g_add_mu);
+      for (uint32 i = 0; i < k; i++) {
+         add_copy(rq[i]);
+      }
+      for (uint32 i = 0; i < k; i++) {
+         while (!__atomic_load_n(&rq[i]->copied, __ATOMIC_ACQUIRE)) {
+            __builtin_ia32_pause();
+         }
+      }
+      r = rf_amd_batch_stage_build(b);
    }
-   r = rf_amd_batch_build_hashes_host(b, h);
-   if (k > 1) {
-      free(h);
-   }
+   (void)total;
    rf_amd_filter_info *infos = malloc(sizeof(*infos) * k);
    platform_assert(infos != NULL);
    if (!r) {
@@ -745,6 +767,11 @@ add_submit(rf_amd_engine *e, add_req *q)
          pthread_cond_broadcast(&g_add_cv);
       } else {
          pthread_cond_wait(&g_add_cv, &g_add_mu);
+         if (q->stage_dst && !__atomic_load_n(&q->claim, __ATOMIC_ACQUIRE)) {
+            pthread_mutex_unlock(&g_add_mu); /* our share of the staging copy */
+            add_copy(q);
+            pthread_mutex_lock(&g_add_mu);
+         }
       }
    }
    pthread_mutex_unlock(&g_add_mu);
@@ -1014,7 +1041,7 @@ static int            g_aq_sleeping; /* the completion thread waits on g_aq_cv (
 static pthread_mutex_t g_aq_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t  g_aq_cv;
 static pthread_once_t  g_aq_once = PTHREAD_ONCE_INIT;
-static uint64          g_async_batches, g_async_probes;
+static uint64          g_async_batches, g_async_probes, g_async_probe_ns;
 static uint64          g_async_limit, g_async_window_ns;
 
 #define AQ_NEXT(st) (*(rf_state **)&(st)->index_page)
@@ -1044,7 +1071,9 @@ complete_states(rf_state *list, uint64 n)
       h[m]   = st->fp; /* the full 32-bit hash, stored when queued */
       m++;
    }
+   const uint64 t0 = now_ns();
    lookup_many(ccs, cfgs, fl, h, m, found, rc);
+   __atomic_fetch_add(&g_async_probe_ns, now_ns() - t0, __ATOMIC_RELAXED);
    for (uint64 i = 0; i < m; i++) {
       rf_state         *st  = q[i];
       async_callback_fn cb  = st->callback;
@@ -1102,6 +1131,22 @@ completion_main(void *arg)
          }
          __atomic_store_n(&g_aq_sleeping, 0, __ATOMIC_SEQ_CST);
          pthread_mutex_unlock(&g_aq_mu);
+      }
+      /* a burst of submissions (a caller starting its in-flight states) goes out as one launch:
+         wait until no state has arrived for a microsecond, at most 4 */
+      {
+         uint64 c0 = __atomic_load_n(&g_aq_count, __ATOMIC_RELAXED);
+         const uint64 t0 = now_ns();
+         uint64       tc = t0, t = t0;
+         while (t - t0 < 4000 && t - tc < 1000) {
+            __builtin_ia32_pause();
+            t = now_ns();
+            const uint64 c1 = __atomic_load_n(&g_aq_count, __ATOMIC_RELAXED);
+            if (c1 != c0) {
+               c0 = c1;
+               tc = t;
+            }
+         }
       }
       const uint64 window = __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED);
       if (window) { /* optional coalescing window after the first arrival */
@@ -1176,6 +1221,12 @@ routing_filter_amd_async_stats(uint64 *batches, uint64 *probes)
 {
    *batches = __atomic_load_n(&g_async_batches, __ATOMIC_RELAXED);
    *probes  = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED);
+}
+
+uint64
+routing_filter_amd_async_probe_ns(void)
+{
+   return __atomic_load_n(&g_async_probe_ns, __ATOMIC_RELAXED);
 }
 
 async_status

@@ -24,6 +24,10 @@ routing_filter_amd_async_config(uint64 batch, uint64 window_us);
 void
 routing_filter_amd_async_stats(uint64 *batches, uint64 *probes);
 
+/* nanoseconds spent so far probing queued states (grouping, residency, the GPU round trip) */
+uint64
+routing_filter_amd_async_probe_ns(void);
+
 /* routing_filter_add calls coalesced: GPU batches built and filters they held */
 void
 routing_filter_amd_add_stats(uint64 *batches, uint64 *filters);

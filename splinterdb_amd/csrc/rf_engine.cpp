@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -170,6 +171,10 @@ struct rf_amd_engine {
   HostStage stage;
   std::mutex slot_mu;
   std::vector<ProbeSlot*> slots_all, slots_free;
+  // builds issued on `stream` (do_build) and the count last seen finished: a lookup slot
+  // queries the engine stream only when a build may still be in flight (a HIP call less on
+  // the lookup round trip)
+  std::atomic<uint64_t> builds_issued{0}, builds_seen_idle{0};
 };
 
 struct DevBuf {
@@ -822,6 +827,7 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
     int rc = rf_launch_old_decode(&a);
     if (rc) return fail(RF_AMD_EINVAL, std::string("old decode launch: ") + hipGetErrorString((hipError_t)rc));
   }
+  if (st == b->eng->stream) b->eng->builds_issued.fetch_add(1, std::memory_order_acq_rel);
   int rc = rf_launch_build(&a);
   if (rc) return fail(RF_AMD_EINVAL, std::string("build launch: ") + hipGetErrorString((hipError_t)rc));
   b->built = true;
@@ -874,6 +880,39 @@ static int stage_reserve(rf_amd_engine* e, size_t bytes) {
 // Host-buffer forms for callers that hold no device memory (the routing_filter.h shim,
 // shim/routing_filter_amd.c): inputs are staged through the engine's pinned buffer on the
 // engine stream, and the call returns once the results are complete.
+// Two-step form of rf_amd_batch_build_hashes_host for callers that fill the staging buffer
+// themselves, e.g. from several threads at once (the shim's coalesced adds: each adding
+// thread copies its own fingerprints): stage_begin takes the engine's pinned staging buffer,
+// sized for the batch's keys_total hashes (filter f's at its run offset), and returns it;
+// stage_build uploads it, builds, waits, and releases the buffer. Every stage_begin must be
+// followed by one stage_build (or stage_abort) on the same batch.
+extern "C" int rf_amd_batch_stage_begin(rf_amd_batch* b, uint32_t** h_stage) {
+  if (!b || !h_stage) return fail(RF_AMD_EINVAL, "null batch / out-param");
+  rf_amd_engine* e = b->eng;
+  HIPCHK(hipSetDevice(e->device));
+  e->stage.mu.lock();
+  if (int rc = stage_reserve(e, 4ull * b->keys_total + 16)) {
+    e->stage.mu.unlock();
+    return rc;
+  }
+  *h_stage = static_cast<uint32_t*>(e->stage.h);
+  return 0;
+}
+
+extern "C" int rf_amd_batch_stage_build(rf_amd_batch* b) {
+  rf_amd_engine* e = b->eng;
+  std::lock_guard<std::mutex> g(e->stage.mu, std::adopt_lock);  // taken by stage_begin
+  const size_t bytes = 4ull * b->keys_total;
+  if (bytes) HIPCHK(hipMemcpyAsync(e->stage.d, e->stage.h, bytes, hipMemcpyHostToDevice, e->stream));
+  if (int rc = do_build(b, IN_HASH, e->stage.d, nullptr, 4, e->stream)) return rc;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+extern "C" void rf_amd_batch_stage_abort(rf_amd_batch* b) {
+  if (b) b->eng->stage.mu.unlock();
+}
+
 extern "C" int rf_amd_batch_build_hashes_host(rf_amd_batch* b, const uint32_t* h_hashes) {
   if (!b) return fail(RF_AMD_EINVAL, "null batch");
   if (b->keys_total && !h_hashes) return fail(RF_AMD_EINVAL, "null hashes");
@@ -895,6 +934,7 @@ extern "C" int rf_amd_batch_build_hashes_host(rf_amd_batch* b, const uint32_t* h
 extern "C" int rf_launch_probe_groups(void* stream, const uint32_t* in, const ProbeGroup* groups, uint32_t ng,
                                       uint64_t n, uint64_t* found, uint32_t fp_size, uint32_t lis,
                                       uint32_t* counter, uint32_t* done_flag, uint32_t seq);
+extern "C" int rf_launch_probe_small(void* stream, const SmallProbe* a);
 
 static ProbeSlot* slot_take(rf_amd_engine* e) {
   {
@@ -995,13 +1035,35 @@ static const uint64_t MAPPED_MAX_PROBES = 32768;
 // The common body: n probes, probe i in group h_group[i] (NULL: group 0) of the ng-entry group
 // table, results into h_found. Waits for any work still queued on the engine stream (builds
 // issued there), then runs on a lookup slot of its own.
+// waits for a slot's kernel to publish `seq` (or fails if the stream errored without it)
+static int slot_wait(ProbeSlot* s, uint32_t seq, bool sync) {
+  if (sync) {
+    HIPCHK(hipStreamSynchronize(s->st));
+    return 0;
+  }
+  for (uint32_t spin = 1;; spin++) {
+    if (__atomic_load_n(s->flag, __ATOMIC_ACQUIRE) == seq) return 0;
+    __builtin_ia32_pause();
+    if ((spin & 4095) == 0) {  // a kernel that faulted never stores the flag
+      const hipError_t q = hipStreamQuery(s->st);
+      if (q == hipErrorNotReady) continue;
+      if (q != hipSuccess) return fail(RF_AMD_EINVAL, std::string("probe kernel: ") + hipGetErrorString(q));
+      if (__atomic_load_n(s->flag, __ATOMIC_ACQUIRE) != seq)
+        return fail(RF_AMD_EINVAL, "probe kernel finished without its completion flag");
+      return 0;
+    }
+  }
+}
+
 static int probe_groups_host(rf_amd_engine* e, const rf_amd_config& cfg, const std::vector<ProbeGroup>& groups,
                              const uint32_t* h_hashes, const uint32_t* h_group, uint64_t n, uint64_t* h_found) {
   if (n == 0) return 0;
   static const int mode = env_mode("RF_AMD_PROBE_MODE", "mapped", "copy");
   static const int wait = env_mode("RF_AMD_PROBE_WAIT", "flag", "sync");
+  static const bool small_ok = !getenv("RF_AMD_PROBE_SMALL") || atoi(getenv("RF_AMD_PROBE_SMALL")) != 0;
   const uint32_t ng = (uint32_t)groups.size();
   const size_t o_g = (8 * n + 15) & ~15ull, o_f = (o_g + sizeof(ProbeGroup) * ng + 63) & ~63ull;
+  const bool small = small_ok && wait != 2 && n <= SMALL_PROBES && ng <= SMALL_GROUPS;
   const bool mapped = mode == 1 || (mode == 0 && n <= MAPPED_MAX_PROBES);
   ProbeSlot* s = slot_take(e);
   if (!s) return RF_AMD_ENOMEM;
@@ -1010,48 +1072,60 @@ static int probe_groups_host(rf_amd_engine* e, const rf_amd_config& cfg, const s
     ProbeSlot* s;
     ~Give() { slot_give(e, s); }
   } give{e, s};
-  if (int rc = slot_reserve(s, o_f + 8 * n, mapped ? 0 : o_f)) return rc;
+  if (int rc = slot_reserve(s, small ? 8 * n : o_f + 8 * n, (small || mapped) ? 0 : o_f)) return rc;
+  const uint64_t issued = e->builds_issued.load(std::memory_order_acquire);
+  if (issued != e->builds_seen_idle.load(std::memory_order_acquire)) {
+    if (hipStreamQuery(e->stream) == hipErrorNotReady) {  // order after builds still in flight
+      hipEvent_t ev;
+      HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(ev, e->stream));
+      HIPCHK(hipStreamWaitEvent(s->st, ev, 0));
+      (void)hipEventDestroy(ev);
+    } else {
+      e->builds_seen_idle.store(issued, std::memory_order_release);  // every build up to `issued` is done
+    }
+  }
+  const uint32_t seq = ++s->seq ? s->seq : ++s->seq;  // never 0 (the flag's initial value)
+  (void)hipGetLastError();
+  if (small) {  // everything in the kernel arguments: no host-memory read before the probe
+    SmallProbe sp;
+    memset(&sp, 0, sizeof(sp));
+    sp.n = (uint32_t)n;
+    sp.ng = ng;
+    sp.fp_size = cfg.fingerprint_size;
+    sp.lis = cfg.log_index_size;
+    sp.seq = seq;
+    for (uint64_t i = 0; i < n; i++) {
+      sp.h[i] = h_hashes[i];
+      const uint32_t g = h_group ? h_group[i] : 0u;
+      sp.g[i] = (uint8_t)(g < ng ? g : 255u);
+    }
+    for (uint32_t g = 0; g < ng; g++) sp.groups[g] = groups[g];
+    sp.found = reinterpret_cast<uint64_t*>(s->h);
+    sp.done_flag = s->flag;
+    if (int rc = rf_launch_probe_small(s->st, &sp))
+      return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
+    if (int rc = slot_wait(s, seq, false)) return rc;
+    memcpy(h_found, s->h, 8 * n);
+    return 0;
+  }
   memcpy(s->h, h_hashes, 4 * n);
   uint32_t* hg = reinterpret_cast<uint32_t*>(s->h + 4 * n);
   if (h_group) memcpy(hg, h_group, 4 * n);
   else memset(hg, 0, 4 * n);
   memcpy(s->h + o_g, groups.data(), sizeof(ProbeGroup) * ng);
-  if (hipStreamQuery(e->stream) == hipErrorNotReady) {  // order after builds still in flight
-    hipEvent_t ev;
-    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(ev, e->stream));
-    HIPCHK(hipStreamWaitEvent(s->st, ev, 0));
-    (void)hipEventDestroy(ev);
-  }
   const uint8_t* in = s->h;
   if (!mapped) {
     HIPCHK(hipMemcpyAsync(s->d, s->h, o_f, hipMemcpyHostToDevice, s->st));
     in = s->d;
   }
-  const uint32_t seq = ++s->seq ? s->seq : ++s->seq;  // never 0 (the flag's initial value)
   uint64_t* found = reinterpret_cast<uint64_t*>(s->h + o_f);
-  (void)hipGetLastError();
   if (int rc = rf_launch_probe_groups(s->st, reinterpret_cast<const uint32_t*>(in),
                                       reinterpret_cast<const ProbeGroup*>(in + o_g), ng, n, found,
                                       cfg.fingerprint_size, cfg.log_index_size, s->d_counter,
                                       wait == 2 ? nullptr : s->flag, seq))
     return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
-  if (wait == 2) {
-    HIPCHK(hipStreamSynchronize(s->st));
-  } else {
-    for (uint32_t spin = 1;; spin++) {
-      if (__atomic_load_n(s->flag, __ATOMIC_ACQUIRE) == seq) break;
-      __builtin_ia32_pause();
-      if ((spin & 4095) == 0) {  // a kernel that faulted never stores the flag
-        const hipError_t q = hipStreamQuery(s->st);
-        if (q == hipErrorNotReady) continue;
-        if (q != hipSuccess) return fail(RF_AMD_EINVAL, std::string("probe kernel: ") + hipGetErrorString(q));
-        if (__atomic_load_n(s->flag, __ATOMIC_ACQUIRE) != seq)
-          return fail(RF_AMD_EINVAL, "probe kernel finished without its completion flag");
-        break;
-      }
-    }
-  }
+  if (int rc = slot_wait(s, seq, wait == 2)) return rc;
   memcpy(h_found, found, 8 * n);
   return 0;
 }

@@ -917,14 +917,17 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       return fp_of(v) != pfp ? 1u : 0u;
     };
     uint32_t uniq = 0;
-    // (2) kept new entries: merged position = kept rank + old entries before it
+    // (2) kept new entries (in registers): merged position = kept rank + old entries before
+    // it (a binary search of B)
+    uint32_t npos[PER];
     {
       uint32_t r = kbase;
 #pragma unroll
       for (int k = 0; k < PER; k++) {
+        npos[k] = 0;
         if (kmask >> k & 1u) {
           const uint32_t v = x[k], j = lower(B, nb, v);
-          dst[r + j] = v >> 1;
+          npos[k] = r + j;
           bool hp = r > 0;
           uint32_t p = hp ? Ak[r - 1] : 0u;
           if (j > 0 && (!hp || B[j - 1] > p)) { p = B[j - 1]; hp = true; }
@@ -934,16 +937,23 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       }
     }
     // (3) old entries: thread t owns B[t*cbn, t*cbn + cbn) (odd stride: distinct LDS banks);
-    // merged position = own index + kept new entries before it (walked forward)
+    // merged position = own index + kept new entries before it -- one binary search of Ak,
+    // then a walk. Values and positions stay in registers until every read of A and B is done.
+    const uint32_t cbn = ((nb + SORT_NT - 1) / SORT_NT) | 1u;  // <= PER
+    const uint32_t j0 = threadIdx.x * cbn;
+    uint32_t ov[PER], opos[PER];
     {
-      const uint32_t cbn = ((nb + SORT_NT - 1) / SORT_NT) | 1u;
-      const uint32_t j0 = threadIdx.x * cbn, j1 = min(j0 + cbn, nb);
-      if (j0 < nb) {
-        uint32_t i = lower(Ak, nkept, B[j0]);
-        for (uint32_t j = j0; j < j1; j++) {
+      uint32_t i = j0 < nb ? lower(Ak, nkept, B[j0]) : 0u;
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        const uint32_t j = j0 + k;
+        ov[k] = 0;
+        opos[k] = 0;
+        if ((uint32_t)k < cbn && j < nb) {
           const uint32_t v = B[j];
           while (i < nkept && Ak[i] < v) i++;
-          dst[j + i] = v >> 1;
+          ov[k] = v;
+          opos[k] = j + i;
           bool hp = j > 0;
           uint32_t p = hp ? B[j - 1] : 0u;
           if (i > 0 && (!hp || Ak[i - 1] > p)) { p = Ak[i - 1]; hp = true; }
@@ -969,6 +979,19 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       first_old[c.idx0 + l] = be > bs ? B[bs] >> 1 : 0xffffffffu;
       has_old[c.idx0 + l] = be > bs ? 1u : 0u;
     }
+    __syncthreads();  // every read of A and B is done: the merged order overwrites s_b
+    const uint32_t ntot = nkept + nb;
+    {
+      uint32_t r = 0;
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        if (kmask >> k & 1u) Ak[npos[k]] = x[k] >> 1;
+        if ((uint32_t)k < cbn && j0 + k < nb) Ak[opos[k]] = ov[k] >> 1;
+        (void)r;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ntot; i += SORT_NT) dst[i] = Ak[i];  // coalesced
     uint32_t tot_uniq;
     block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
     if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
@@ -3052,6 +3075,85 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
   }
 }
 
+// ---- persistent, software-pipelined probe (24-byte keys, probes in per-filter runs) -----
+// The same lookups as k_probe's WAVE_KEYS path, but each wave loops over its XCD's 64-probe
+// tiles and fetches tile k+1's keys (LDS-DMA into the other half of a two-tile buffer) while
+// tile k's hashes are computed and its probe lines are in flight: per wave one key fetch and
+// 64 line fetches overlap, where k_probe's one-tile waves wait for them one after the other
+// and rely on other waves for overlap. Full tiles only; the kernel's last wave takes a
+// partial final tile the simple way. Grid: a multiple of 8 workgroups, each XCD (blockIdx % 8,
+// the observed round-robin placement -- speed only) owns a contiguous eighth of the tiles,
+// as k_probe's xcd_chunk does.
+constexpr int PIPE_NT = 256;
+__global__ __launch_bounds__(PIPE_NT) void k_probe_pipe(const uint4* __restrict__ pplans,
+                                                        const FilterPlan* __restrict__ plans,
+                                                        const uint8_t* __restrict__ pages,
+                                                        const uint64_t* __restrict__ slots,
+                                                        const uint4* __restrict__ lines,
+                                                        const void* __restrict__ in0,
+                                                        const uint64_t* __restrict__ runs,
+                                                        const uint32_t* __restrict__ wave_tab, uint64_t n,
+                                                        uint64_t* __restrict__ found, uint32_t fp_size,
+                                                        uint32_t seed, uint32_t lis, uint32_t page_size,
+                                                        uint32_t num_filters) {
+  __shared__ v4u s_k[PIPE_NT / WAVE][2][96];
+  const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const uint64_t T = n / WAVE;  // full tiles
+  const uint32_t nxb = gridDim.x / 8, x = blockIdx.x % 8, lb = blockIdx.x / 8;
+  const uint64_t t_begin = T * x / 8, t_end = T * (x + 1) / 8;
+  const uint64_t W = (uint64_t)nxb * (PIPE_NT / WAVE), w = (uint64_t)lb * (PIPE_NT / WAVE) + wv;
+  const uint64_t nt = t_begin + w < t_end ? (t_end - t_begin - w + W - 1) / W : 0;
+  auto issue = [&](uint64_t t, uint32_t buf) {
+    const v4u* src = reinterpret_cast<const v4u*>(static_cast<const uint8_t*>(in0) + t * (WAVE * 24));
+#pragma unroll
+    for (uint32_t it = 0; it < 2; it++) {
+      const uint32_t j = lane + it * WAVE;
+      if (j < 96)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j),
+                                         (__attribute__((address_space(3))) void*)(&s_k[wv][buf][it * WAVE]), 16, 0, 2);
+    }
+  };
+  // one probe given its key words: filter, plan, line, decode (image walk if the line overflowed)
+  auto finish = [&](uint64_t i, uint32_t h) {
+    const uint32_t fid = tab_filter(wave_tab, runs, num_filters, i);
+    const uint4 pp = load_pplan(pplans, fid, num_filters);
+    const uint32_t fs = __builtin_amdgcn_readfirstlane(fid);
+    uint64_t r;
+    bool ok;
+    if (__builtin_amdgcn_ballot_w64(fid != fs) == 0) {
+      const uint4 U = make_uint4(__builtin_amdgcn_readfirstlane(pp.x), __builtin_amdgcn_readfirstlane(pp.y),
+                                 __builtin_amdgcn_readfirstlane(pp.z), __builtin_amdgcn_readfirstlane(pp.w));
+      ok = probe_line(U, h, lines, fp_size, r);
+    } else {
+      ok = probe_line(pp, h, lines, fp_size, r);
+    }
+    if (!ok) r = probe_walk(pp, h, fid, plans, pages, slots, fp_size, lis, page_size);
+    __builtin_nontemporal_store(r, found + i);
+  };
+  if (nt) issue(t_begin + w, 0);
+  for (uint64_t k = 0; k < nt; k++) {
+    const uint64_t t = t_begin + w + k * W;
+    const uint32_t buf = (uint32_t)(k & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k's keys have landed
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint2* k2 = reinterpret_cast<const uint2*>(s_k[wv][buf]) + 3 * lane;
+    const uint2 a = k2[0], b = k2[1], c = k2[2];
+    // every lane has its words before the next fetch may land in the other half... which no
+    // lane reads in this iteration; the half read here is refilled two iterations later
+    if (k + 1 < nt) issue(t + W, buf ^ 1u);
+    uint32_t kw[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    finish(t * WAVE + lane, xxh32_24(kw, seed));
+    __builtin_amdgcn_wave_barrier();  // all lanes' LDS reads of this half precede its refill
+  }
+  // a partial final tile: the last wave of XCD 7's range takes it, loading keys per lane
+  if (n % WAVE && x == 7 && lb == nxb - 1 && wv == PIPE_NT / WAVE - 1) {
+    const uint64_t i = T * WAVE + lane;
+    if (i < n) finish(i, hash_key<IN_KEYS24, true>(in0, nullptr, 24, seed, i));
+  }
+}
+
 // ---- lookups against many resident filters in one launch ------------------------------
 // Probe i looks up hash in[i] in the filter of group in[n + i] (routing_filter_lookup,
 // src/routing_filter.c:985-1073, decoded exactly as k_probe: probe line, image walk when the
@@ -3098,6 +3200,43 @@ __global__ __launch_bounds__(256) void k_probe_groups(const uint32_t* __restrict
       }
     }
   }
+}
+
+// The smallest calls -- a routing_filter_lookup of one key, a handful of async states -- pass
+// their hashes and filter descriptors in the kernel arguments (delivered with the dispatch):
+// the kernel reads nothing from host memory before its probe line, one wave answers, and its
+// lane 0 publishes the completion word once every result is visible system-wide.
+__global__ __launch_bounds__(WAVE) void k_probe_small(SmallProbe a) {
+  const uint32_t lane = threadIdx.x;
+  if (lane < a.n) {
+    const uint32_t h = a.h[lane], g = a.g[lane];
+    uint64_t r = 0;
+    if (g < a.ng) {
+      const ProbeGroup G = a.groups[g];
+      const uint4 P = make_uint4(G.x, 0u, 0u, G.err);
+      if (!probe_line(P, h, G.lines, a.fp_size, r)) {
+        const uint32_t vs = G.x & 0xff, rem = (G.x >> 8) & 0xff, rvs = (G.x >> 16) & 0xff;
+        const uint32_t fp = h >> (32 - a.fp_size);
+        const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
+        const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+        r = probe_stream(bucket & ((1u << a.lis) - 1), remainder, vs, rvs, G.pages, G.slots[bucket >> a.lis], a.lis);
+      }
+    }
+    a.found[lane] = r;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+extern "C" int rf_launch_probe_small(void* stream, const SmallProbe* a) {
+  hipLaunchKernelGGL(k_probe_small, dim3(1), dim3(WAVE), 0, (hipStream_t)stream, *a);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
 }
 
 extern "C" int rf_launch_probe_groups(void* stream, const uint32_t* in, const ProbeGroup* groups, uint32_t ng,
@@ -3356,6 +3495,23 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
   const int nt = probe_nt(kind);
   dim3 g((uint32_t)((n + (uint64_t)nt * ppl - 1) / ((uint64_t)nt * ppl))), b(nt);
   REC(EV_P_START);
+  // RF_AMD_PROBE_PIPE=1: the persistent, software-pipelined variant (k_probe_pipe) for the
+  // probe-run path of 24-byte keys (bench.py's C2-C4); grid = 8 workgroups per CU
+  // (read per launch, so an A/B in one process can flip it); value > 1: workgroups per CU
+  const char* pipe_env = getenv("RF_AMD_PROBE_PIPE");
+  const int pipe = pipe_env ? atoi(pipe_env) : 0;
+  if (pipe && kind == IN_KEYS24 && a.probe_runs && a.wave_tab && ((uintptr_t)in0 & 15) == 0 && n >= WAVE) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t grid = (uint32_t)((cus * (pipe > 1 ? pipe : 7) + 7) / 8 * 8);  // 91 SGPRs: 7 per CU
+    hipLaunchKernelGGL(k_probe_pipe, dim3(grid), dim3(PIPE_NT), 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages,
+                       a.slots, a.lines, in0, a.probe_runs, a.wave_tab, n, found, a.fp_size, a.seed, a.lis,
+                       a.page_size, a.num_filters);
+    CHECK_LAUNCH();
+    REC(EV_P_END);
+    return 0;
+  }
 #define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, a.wave_tab, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
 #if RF_DIAG
   if (kind == IN_KEYS24 && (a.occ || a.ppl)) {  // experiment variants: waves/SIMD cap, probes per lane

@@ -95,6 +95,17 @@ struct ProbeGroup {
   const uint64_t* slots;  // the filter's (relocatable) index slots
 };
 
+// a lookup call small enough to travel in the kernel arguments (k_probe_small)
+constexpr uint32_t SMALL_PROBES = 64, SMALL_GROUPS = 8;
+struct SmallProbe {
+  uint32_t n, ng, fp_size, lis, seq;
+  uint32_t h[SMALL_PROBES];
+  uint8_t g[SMALL_PROBES];
+  ProbeGroup groups[SMALL_GROUPS];
+  uint64_t* found;      // pinned host memory
+  uint32_t* done_flag;  // pinned host memory: seq once every result is visible
+};
+
 struct FilterOut {
   uint32_t num_unique;
   uint32_t num_pages;

@@ -48,7 +48,8 @@ EXPORTED = [
     "rf_amd_batch_build_hashes_host", "rf_amd_batch_probe_hashes_host", "rf_amd_engine_pool_stats",
     "rf_amd_filter_print_abs", "rf_amd_batch_infos", "rf_amd_batch_destroy_on", "rf_amd_probe_many_hashes_host",
     "rf_amd_probe_filters_host", "rf_amd_engine_pool_trim", "rf_amd_engine_stream", "rf_amd_engine_sync",
-    "rf_amd_batch_device_bytes", "rf_amd_batch_trim",
+    "rf_amd_batch_device_bytes", "rf_amd_batch_trim", "rf_amd_batch_stage_begin", "rf_amd_batch_stage_build",
+    "rf_amd_batch_stage_abort",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -177,6 +178,10 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_device_bytes.argtypes = [vp]
     L.rf_amd_batch_device_bytes.restype = u64
     L.rf_amd_batch_trim.argtypes = [vp, vp]
+    L.rf_amd_batch_stage_begin.argtypes = [vp, ctypes.POINTER(vp)]
+    L.rf_amd_batch_stage_build.argtypes = [vp]
+    L.rf_amd_batch_stage_abort.argtypes = [vp]
+    L.rf_amd_batch_stage_abort.restype = None
     _lib = L
     return L
 

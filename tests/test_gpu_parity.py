@@ -495,12 +495,14 @@ def test_sparse_blocks_at_max_indices(oracle):
         assert (img.slots == of.slots()[: of.num_indices]).all(), distinct
 
 
-def _clustered_hashes(rng, n_rand, n_clu, lnb, fp_size=26):
-    """n_rand uniform hashes + n_clu whose fingerprints all fall in ONE filter bucket with
-    random remainders (many distinct entries in one bucket, in random order)"""
+def _clustered_hashes(rng, n_rand, n_clu, lnb, fp_size=26, distinct=48):
+    """n_rand uniform hashes + n_clu whose fingerprints all fall in ONE filter bucket, drawn
+    from `distinct` remainders in random order: a bucket of thousands of copies of a few
+    dozen entries (duplicates collapse in the dedupe, so the index block still fits a page)"""
     rem = fp_size - lnb
     bucket = int(rng.integers(0, 1 << lnb))
-    fp = (np.uint64(bucket) << np.uint64(rem)) | rng.integers(0, 1 << rem, size=n_clu, dtype=np.uint64)
+    rems = rng.choice(1 << rem, size=distinct, replace=False).astype(np.uint64)
+    fp = (np.uint64(bucket) << np.uint64(rem)) | rems[rng.integers(0, distinct, size=n_clu)]
     low = rng.integers(0, 1 << (32 - fp_size), size=n_clu, dtype=np.uint64)
     clu = ((fp << np.uint64(32 - fp_size)) | low).astype(np.uint32)
     h = np.concatenate([rng.integers(0, 1 << 32, size=n_rand, dtype=np.uint64).astype(np.uint32), clu])
@@ -509,11 +511,12 @@ def _clustered_hashes(rng, n_rand, n_clu, lnb, fp_size=26):
 
 @pytest.mark.parametrize("n_rand,n_clu", [(8000, 12000), (16000, 4000)])
 def test_big_bucket_of_distinct_entries_sorts_fast(oracle, n_rand, n_clu):
-    """One filter bucket holding 12,000 (resp. 4,000) entries with random remainders: the
-    coarse bucket overflows LDS (K4b, 12,000) or stays in LDS (4,000). Such a bucket used to
-    be ordered by a per-bucket insertion sort -- quadratic, seconds at 12K; the whole
-    workgroup now sorts it with an odd-even merge network. Bit-exact against the oracle, and
-    fresh plus incremental builds finish in well under a second."""
+    """One filter bucket holding 12,000 (resp. 4,000) copies of 48 entries in random order:
+    the coarse bucket overflows LDS (K4b, 12,000) or stays in LDS (4,000). Such a bucket used
+    to be ordered by a per-bucket insertion sort -- quadratic in the copies out of order,
+    seconds at 12K; the whole workgroup now sorts it with an odd-even merge network.
+    Bit-exact against the oracle, and fresh plus incremental builds finish in well under a
+    second."""
     import time
     rng = np.random.default_rng(n_clu)
     cfg = E.routing_config_init()
@@ -544,3 +547,27 @@ def test_big_bucket_of_distinct_entries_sorts_fast(oracle, n_rand, n_clu):
     assert (img2.num_unique, img2.num_pages) == (of2.num_unique, of2.num_pages)
     assert (img2.pages == of2.pages()).all() and (img2.slots == of2.slots()[: of2.num_indices]).all()
     assert dt2 < 0.5, dt2
+
+
+@pytest.mark.parametrize("pipe", ["7", "8", "2"])
+def test_pipelined_probe_equals_k_probe(pipe, monkeypatch):
+    """k_probe_pipe (RF_AMD_PROBE_PIPE: persistent waves that fetch the next tile's keys while
+    this tile's probe lines are in flight) returns exactly k_probe's found_values: 17 filters
+    of uneven sizes (tiles spanning filter runs, a partial final tile), inserted and absent keys"""
+    cfg = E.routing_config_init()
+    sizes = [100_003 + 7919 * f for f in range(17)]
+    total = sum(sizes)
+    keys = dev(K.seq_keys(0, total))
+    b = E.FilterBatch(cfg, sizes)
+    b.build_keys(keys, 24)
+    neg = dev(K.seq_keys(10 * total, total))
+    for probe in (keys, neg):
+        out = []
+        for mode in ("0", pipe):
+            monkeypatch.setenv("RF_AMD_PROBE_PIPE", mode)
+            found = torch.full((total,), -1, dtype=torch.int64, device="cuda:0")
+            b.probe_keys_runs(probe, 24, sizes, found)
+            torch.cuda.synchronize()
+            out.append(found.cpu().numpy())
+        assert (out[0] == out[1]).all()
+    assert (out[0] != -1).all()

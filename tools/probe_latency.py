@@ -35,7 +35,7 @@ def med(fn, reps=20):
 
 
 out = {}
-for n in (1, 1024, 8192):
+for n in (1, 16, 1024, 8192):
     q = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
     found = np.zeros(n, dtype=np.uint64)
     out[f"one_filter_{n}"] = med(lambda: E._check(L.rf_amd_batch_probe_hashes_host(

@@ -3,7 +3,7 @@ own routing_filter.c in the same page stack (oracle/_ref/libshim_rf.so vs libref
 Prints one JSON line (ms, median of 5):
   add_fresh_ms              routing_filter_add of 2^20 - 1 hashes
   add_incremental_ms        the same onto an existing filter (old_filter, the trunk's case)
-  lookup_one_ms             routing_filter_lookup of one key
+  lookup_one_ms             one routing_filter_lookup call (per call, over 2,000 calls)
   lookup_batch_8192_ms      routing_filter_amd_lookup_batch, 8,192 (filter, key) over 8 filters
   lookup_async_8192_ms      8,192 routing_filter_lookup_async states over 8 filters, each
                             started once, then polled (the shim: one completion thread)
@@ -48,9 +48,20 @@ for name, path in (("shim", R.SHIM_PATH), ("reference", R.LIB_PATH)):
         P = 8192
         fid = rng.integers(0, 8, size=P).astype(np.uint32)
         probe = np.stack([keys[f][rng.integers(0, n)] for f in fid])
-        r["lookup_one_ms"] = med(lambda: s.lookup_keys(descs[0], probe[:1]), reps=200)
+        # one routing_filter_lookup call: 2,000 calls in a C loop (oracle/ref_harness.c
+        # rfr_lookup_keys), per call -- no Python in the timed path of each call
+        r["lookup_one_ms"] = round(med(lambda: s.lookup_keys(descs[0], probe[:2000]), reps=7) / 2000, 5)
         r["lookup_batch_8192_ms"] = med(lambda: s.lookup_batch(descs, probe, fid))
+        st0 = s.shim_stats() or {}
+        b0 = s.async_stats()
         r["lookup_async_8192_ms"] = med(lambda: s.lookup_keys_async_many(descs, probe, fid))
+        st1 = s.shim_stats() or {}
+        b1 = s.async_stats()
+        ph = s.async_many_phases()
+        r["lookup_async_8192_detail"] = {
+            "start_ms": round(ph[0] / 1e6, 3), "poll_ms": round(ph[1] / 1e6, 3),
+            "launches_per_call": round((b1[0] - b0[0]) / 6, 1),
+            "probe_ms_per_call": round((st1.get("async_probe_ns", 0) - st0.get("async_probe_ns", 0)) / 6e6, 3)}
         r["async_driven_8192_ms"] = med(lambda: s.lookup_keys_async_driven(descs, probe, fid, max_inflight=64))
         many = [s.add(s.hash_keys(K.ids_keys((np.uint64(100 + f) << np.uint64(32)) +
                                              np.arange(2000, dtype=np.uint64))), value=f % 30)
