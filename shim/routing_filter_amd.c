@@ -56,11 +56,11 @@
  *
  * async. routing_filter_lookup_async's first call on a state hashes the key, queues the
  * state and returns ASYNC_STATUS_RUNNING without touching the state again (async.h:115-125:
- * it may be completed on another thread at once). A completion thread probes the queued
- * states -- ONE GPU launch for every filter they name -- as soon as it is free, up to
- * RF_SHIM_ASYNC_BATCH states
- * (default 1024) -- in practice whatever arrived during the previous GPU round trip: batches
- * size themselves (RF_SHIM_ASYNC_WINDOW_US, default 0, adds a wait for more) -- so every state
+ * it may be completed on another thread at once). A completion thread (two by default) probes
+ * the queued states -- ONE GPU launch for every filter they name -- as soon as it is free:
+ * whatever arrived during the previous GPU round trip, batches size themselves
+ * (RF_SHIM_ASYNC_WINDOW_US, default 0, adds a wait for up to RF_SHIM_ASYNC_BATCH states,
+ * default 1024) -- so every state
  * completes without being called again. Completion stores found_values and
  * the result, marks the state done, then calls its callback(callback_arg) -- from the
  * completion thread, registered with the platform like any SplinterDB thread -- and the
@@ -1024,11 +1024,13 @@ lookup_many(cache *const          *ccs,
 /* ---- async: queued states, completed by a completion thread ------------------------------ */
 /*
  * Queued states form a lock-free stack (one compare-and-swap per enqueue, the link kept in
- * the state's index_page local, which the shim's coroutine never uses otherwise). The
+ * the state's index_page local, which the shim's coroutine never uses otherwise). A
  * completion thread takes the whole stack at once and answers it with one launch: batches
- * size themselves -- what arrives during one GPU round trip goes out in the next. After a
- * batch it spins briefly for more before sleeping on a condition variable; an enqueue onto
- * an empty stack wakes it. RF_SHIM_ASYNC_WINDOW_US (default 0) makes it wait that long after
+ * size themselves -- what arrives during one GPU round trip goes out in the next. There are
+ * RF_SHIM_ASYNC_THREADS of them (default 2), each on its own lookup slot, so a batch that
+ * arrives while another is on the GPU does not wait for it (callers that re-submit from
+ * callbacks keep two launches in flight). After a batch a thread spins briefly for more
+ * before sleeping on a condition variable; an enqueue onto an empty stack wakes one. RF_SHIM_ASYNC_WINDOW_US (default 0) makes it wait that long after
  * the first arrival for up to RF_SHIM_ASYNC_BATCH states (default 1024) before taking them.
  */
 static char g_queued_marker;
@@ -1037,12 +1039,12 @@ typedef routing_filter_lookup_async_state rf_state;
 
 static rf_state      *g_aq_head;     /* the stack of queued states (atomic) */
 static uint64         g_aq_count;    /* states on it (atomic) */
-static int            g_aq_sleeping; /* the completion thread waits on g_aq_cv (atomic) */
+static int            g_aq_sleeping; /* completion threads waiting on g_aq_cv (atomic) */
 static pthread_mutex_t g_aq_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t  g_aq_cv;
 static pthread_once_t  g_aq_once = PTHREAD_ONCE_INIT;
 static uint64          g_async_batches, g_async_probes, g_async_probe_ns;
-static uint64          g_async_limit, g_async_window_ns;
+static uint64          g_async_limit, g_async_window_ns, g_async_threads;
 
 #define AQ_NEXT(st) (*(rf_state **)&(st)->index_page)
 
@@ -1125,11 +1127,11 @@ completion_main(void *arg)
             __builtin_ia32_pause();
          }
          pthread_mutex_lock(&g_aq_mu);
-         __atomic_store_n(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
+         __atomic_add_fetch(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
          while (!__atomic_load_n(&g_aq_head, __ATOMIC_SEQ_CST)) {
             pthread_cond_wait(&g_aq_cv, &g_aq_mu);
          }
-         __atomic_store_n(&g_aq_sleeping, 0, __ATOMIC_SEQ_CST);
+         __atomic_sub_fetch(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
          pthread_mutex_unlock(&g_aq_mu);
       }
       /* a burst of submissions (a caller starting its in-flight states) goes out as one launch:
@@ -1173,6 +1175,10 @@ aq_init(void)
 {
    g_async_limit     = env_u64("RF_SHIM_ASYNC_BATCH", 1024);
    g_async_window_ns = env_u64("RF_SHIM_ASYNC_WINDOW_US", 0) * 1000;
+   g_async_threads   = env_u64("RF_SHIM_ASYNC_THREADS", 2);
+   if (g_async_threads == 0 || g_async_threads > 16) {
+      g_async_threads = 2;
+   }
    if (g_async_limit == 0) {
       g_async_limit = 1;
    }
@@ -1184,8 +1190,10 @@ aq_init(void)
    pthread_attr_t at;
    pthread_attr_init(&at);
    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
-   pthread_t t;
-   platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
+   for (uint64 k = 0; k < g_async_threads; k++) {
+      pthread_t t;
+      platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
+   }
    pthread_attr_destroy(&at);
 }
 
@@ -1213,7 +1221,9 @@ routing_filter_amd_async_config(uint64 batch, uint64 window_us)
    pthread_once(&g_aq_once, aq_init);
    __atomic_store_n(&g_async_limit, batch ? batch : 1, __ATOMIC_RELAXED);
    __atomic_store_n(&g_async_window_ns, window_us * 1000, __ATOMIC_RELAXED);
-   aq_wake(); /* a waiting completion thread re-reads them */
+   pthread_mutex_lock(&g_aq_mu); /* waiting completion threads re-read them */
+   pthread_cond_broadcast(&g_aq_cv);
+   pthread_mutex_unlock(&g_aq_mu);
 }
 
 void

@@ -628,7 +628,7 @@ __device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_
 // (s_b[nn, n)), and the dedupe pass reads the two sorted runs through a merge path. Old
 // flagged values are even and new ones odd, so no old value equals a new one and the merge
 // yields exactly the order a sort of all n would (old first on equal e).
-template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
+template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false, bool DIRECT = false>
 __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ cb_filter,
                                                      const uint32_t* __restrict__ cb_count,
@@ -855,7 +855,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
   DBG_PHASE(4);
-  if constexpr (DUAL) {
+  if constexpr (DUAL && DIRECT) {
     // 32-bit incremental builds: every entry's place in the merged, deduplicated order is
     // computed directly and written straight to the output -- old entries are always kept,
     // a new entry is dropped iff it equals the previous new one (src/routing_filter.c:465-494
@@ -939,7 +939,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     // (3) old entries: thread t owns B[t*cbn, t*cbn + cbn) (odd stride: distinct LDS banks);
     // merged position = own index + kept new entries before it -- one binary search of Ak,
     // then a walk. Values and positions stay in registers until every read of A and B is done.
-    const uint32_t cbn = ((nb + SORT_NT - 1) / SORT_NT) | 1u;  // <= PER
+    const uint32_t cbn = min((uint32_t)PER, ((nb + SORT_NT - 1) / SORT_NT) | 1u);  // PER * SORT_NT >= nb
     const uint32_t j0 = threadIdx.x * cbn;
     uint32_t ov[PER], opos[PER];
     {
@@ -3298,11 +3298,27 @@ static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const ui
   return 0;
 }
 
+// 32-bit incremental builds: K4 places every entry directly (RF_AMD_K4_DIRECT=1) or merges
+// the sorted new run with the old run through a merge path (default); read per launch, so one
+// process can compare them
+static bool k4_direct() {
+  const char* v = getenv("RF_AMD_K4_DIRECT");
+  return v && v[0] == '1';
+}
+
 template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* spill) {
-  hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
-                     a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start, a.outs, a.overflow,
-                     a.lis, a.first_old, a.has_old, spill, a.cb_outs);
+  bool direct = false;
+  if constexpr (DUAL) direct = k4_direct();
+  if (direct) {
+    hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
+                       a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start,
+                       a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
+  } else {
+    hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
+                       a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start,
+                       a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
+  }
   CHECK_LAUNCH();
   REC(EV_B_SORT);
   hipLaunchKernelGGL((k_cb_sort_big<EntT, FL, DUAL>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans,

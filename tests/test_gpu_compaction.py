@@ -30,13 +30,16 @@ def chain_ids(g, v, n):
 
 
 @pytest.mark.skipif(not R.available(), reason="reference library not built")
-@pytest.mark.parametrize("entries", ["flag32", "flag32_decode", "wide64"])
+@pytest.mark.parametrize("entries", ["flag32", "flag32_direct", "flag32_decode", "wide64"])
 def test_chain_rounds_match_reference(entries, monkeypatch):
     """both incremental pipelines: 32-bit flagged entries (fp_size + value_size <= 31, the
     default) and 64-bit entries (forced here). With 32-bit entries a round whose geometry is
     the previous round's (rounds 3 and 5: 40K -> 60K, 80K -> 100K fingerprints) reads the old
     entries in place from the previous batch; the others decode the old image
-    (flag32_decode forces the decode for every round)"""
+    (flag32_decode forces the decode for every round; flag32_direct takes K4's direct
+    placement of every entry instead of its merge path)"""
+    if entries == "flag32_direct":
+        monkeypatch.setenv("RF_AMD_K4_DIRECT", "1")
     if entries == "wide64":
         monkeypatch.setenv("RF_AMD_WIDE64", "1")
     if entries == "flag32_decode":

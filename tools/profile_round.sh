@@ -32,6 +32,9 @@ timeout -s KILL 180 rocprofv3 --pmc $TCC --output-format csv -d $O/tcc3 -o c3 --
 python3 tools/tcc_summary.py $O/tcc2/c2_counter_collection.csv $O/tcc3/c3_counter_collection.csv > $O/tcc_$TAG.txt || exit 1
 timeout -k 10 300 python3 bench.py --workload compaction --steps 5 --warmup 1 > $O/bench_compaction.json 2> $O/bench_compaction.err || { echo "bench compaction failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktc -o comp -- python3 bench.py --workload compaction --steps 2 --warmup 0 --no-cpu-baseline > $O/ktc.log 2>&1 || { echo "compaction kernel trace failed"; exit 1; }
+# k_probe against the software-pipelined persistent k_probe_pipe (7 workgroups per CU), C2 and C3
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktp -o pipe_c2 -- python3 tools/probe_pipe_ab.py c2 0 7 > $O/pipe_c2.txt 2>&1 || { echo "pipe c2 failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktp -o pipe_c3 -- python3 tools/probe_pipe_ab.py c3 0 7 > $O/pipe_c3.txt 2>&1 || { echo "pipe c3 failed"; exit 1; }
 # the drop-in's per-call costs beside the reference's routing_filter.c (tools/shim_latency.py)
 timeout -k 10 600 python3 tools/shim_latency.py > $O/shim_latency_$TAG.json 2> $O/shim_latency.err || { echo "shim latency failed"; exit 1; }
 cat $O/bench_c2.json
