@@ -135,7 +135,8 @@ int rf_amd_batch_probe_hashes_host(rf_amd_batch *b, const uint32_t *h_hashes, co
  * g = h_group[i] (NULL: 0); g >= num_groups finds nothing. The form of a flush of queued
  * routing_filter_lookup_async states (src/routing_filter.h:130-155) and of trunk_merge_lookup's
  * per-bundle routing_filter_lookup calls (src/trunk.c:6008-6075; routing_filter.h:87-92)
- * gathered together. All groups share fingerprint_size and log_index_size. */
+ * gathered together. Each group is probed with its own batch's routing config, so filters of
+ * differently configured kvstores may share a call. */
 int rf_amd_probe_filters_host(rf_amd_engine *e, rf_amd_batch *const *batches, const uint32_t *filter_index,
                               uint32_t num_groups, const uint32_t *h_hashes, const uint32_t *h_group,
                               uint64_t n, uint64_t *h_found);
@@ -192,21 +193,6 @@ uint32_t rf_amd_batch_num_filters(const rf_amd_batch *b);
  * reads back as -1): 2 event records per round instead of 10. */
 int rf_amd_batch_set_timing(rf_amd_batch *b, int enable);
 int rf_amd_batch_timings_back(rf_amd_batch *b, uint32_t back, float *ms, uint32_t n);
-/* diagnostics library only (librf_amd_stamps.so; the product library returns EINVAL for a
- * nonzero mode): truncate later probes after 1 = hashing, 2 = the probe-line load
- * (results are then NOT found_values); 0 restores normal probes. Bits 8-15: cap the probe
- * kernel at that many waves per SIMD; bits 16-23: probes per lane (experiments). */
-int rf_amd_debug_probe_ablate(uint32_t mode);
-/* diagnostics: the batch's device-only probe lines (64 B each). read_lines copies them to
- * host (h_lines == NULL: only *num_lines is set); rebuild_lines re-cuts them from the
- * filter images with the image-upload kernel (k_plines), so a test can check that the
- * build's lines and the image's lines are byte-identical. */
-/* diagnostics: a device buffer of 16 u64 per workgroup (NULL = off); the instrumented kernel
- * chosen by `kernel` (1 = bucket sort, 2 = fused partition) stamps the shader clock at each
- * of its phases into it (tools/phase_times.py). */
-int rf_amd_debug_phase_buffer(void *d_buf, uint32_t kernel);
-int rf_amd_debug_read_lines(rf_amd_batch *b, uint8_t *h_lines, uint64_t bytes, uint64_t *num_lines);
-int rf_amd_debug_rebuild_lines(rf_amd_batch *b);
 int rf_amd_batch_timings(rf_amd_batch *b, float *ms, uint32_t n);
 
 /* XXH32(key, cfg->seed) of n device-resident keys into d_hashes (data_key_hash as

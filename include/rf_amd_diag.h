@@ -1,0 +1,45 @@
+/*
+ * rf_amd_diag.h -- diagnostics of the MI355X routing-filter engine (librf_amd.so).
+ *
+ * Not part of the drop-in's product interface (include/rf_amd.h): hooks the parity tests and
+ * the measurement tools use to look inside the engine. None of these has a counterpart in
+ * the reference's src/routing_filter.h.
+ */
+#ifndef RF_AMD_DIAG_H
+#define RF_AMD_DIAG_H
+
+#include "rf_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* the batch's device-only probe lines (64 B each). read_lines copies them to host
+ * (h_lines == NULL: only *num_lines is set); rebuild_lines re-cuts them from the filter
+ * images with the image-upload kernel (k_plines), so a test can check that the build's
+ * lines and the image's lines are byte-identical. */
+int rf_amd_debug_read_lines(rf_amd_batch *b, uint8_t *h_lines, uint64_t bytes, uint64_t *num_lines);
+int rf_amd_debug_rebuild_lines(rf_amd_batch *b);
+
+/* diagnostics library only (librf_amd_stamps.so): a device buffer of 16 u64 per workgroup
+ * (NULL = off); the instrumented kernel chosen by `kernel` (1 = bucket sort, 2 = fused
+ * partition, 3 = page assembly, 4 = layout) stamps the shader clock at each of its phases
+ * into it (tools/phase_times.py). The product library accepts only NULL. */
+int rf_amd_debug_phase_buffer(void *d_buf, uint32_t kernel);
+
+/* where the host-buffer lookup round trips (rf_amd_probe_filters_host and the forms built on
+ * it) spent their time so far: out[0] calls, out[1] ns before the launch (lookup slot,
+ * buffers, ordering after builds, argument packing), out[2] ns in the launch call, out[3] ns
+ * waiting for the kernel's completion word and copying the results out. reset != 0 zeroes
+ * the counters after reading them. */
+int rf_amd_diag_lookup_stats(uint64_t *out, int reset);
+
+/* the source id the library was built from (16 hex digits of SHA-256 over the engine's
+ * sources and headers, splinterdb_amd/build.py source_id): the Python loader refuses a
+ * library whose id differs from the tree's (a stale prebuilt .so) */
+const char *rf_amd_build_id(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

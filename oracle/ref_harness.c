@@ -603,6 +603,25 @@ rfr_registry_set_limit(uint64 mib)
 
 __attribute__((weak)) uint64
 routing_filter_amd_async_probe_ns(void);
+__attribute__((weak)) void
+routing_filter_amd_async_breakdown(uint64 *out);
+int
+rf_amd_diag_lookup_stats(uint64_t *out, int reset) __attribute__((weak));
+
+/* out[0..5] = the shim's async batches, states, burst / gather / lookup / callback ns;
+ * out[6..9] = the engine's lookup round trips: calls, prep / launch / wait ns. 0 without a
+ * shim */
+int
+rfr_async_breakdown(uint64 *out)
+{
+   memset(out, 0, 10 * sizeof(uint64));
+   if (!routing_filter_amd_async_breakdown || !rf_amd_diag_lookup_stats) {
+      return 0;
+   }
+   routing_filter_amd_async_breakdown(out);
+   rf_amd_diag_lookup_stats((uint64_t *)&out[6], 0);
+   return 1;
+}
 
 /* out[0..5] = add batches, filters added, registry bytes, evictions, trims, ns spent probing
  * queued async states; 0 without a shim */
@@ -662,6 +681,41 @@ rfr_lookup_keys_async_flush(rfr_stack      *s,
       routing_filter_lookup_async_state_init(&st[i], (cache *)&s->cc, &s->rcfg,
                                              filters[filter_id ? filter_id[i] : 0], k, &found[i],
                                              count_callback, &cb);
+      routing_filter_lookup_async(&st[i]);
+   }
+   rfr_async_flush();
+   uint64 ret = 0;
+   for (uint64 i = 0; i < n; i++) {
+      if (routing_filter_lookup_async(&st[i]) != ASYNC_STATUS_DONE) {
+         ret = UINT64_MAX;
+      }
+   }
+   free(st);
+   return ret ? ret : __atomic_load_n(&cb, __ATOMIC_ACQUIRE);
+}
+
+/*
+ * The same over filters of SEVERAL stacks (each its own cache and routing config -- e.g. two
+ * kvstores with different filter_hash_size / filter_log_index_size): filter f belongs to
+ * stacks[filter_stack[f]]; every state is queued first, then ONE flush answers them all.
+ */
+uint64
+rfr_lookup_keys_async_flush_multi(rfr_stack     **stacks,
+                                  routing_filter *filters,
+                                  const uint32   *filter_stack,
+                                  const uint32   *filter_id,
+                                  const uint8    *keys,
+                                  uint32          key_len,
+                                  uint64          n,
+                                  uint64         *found)
+{
+   routing_filter_lookup_async_state *st = calloc(n ? n : 1, sizeof(*st));
+   uint64                             cb = 0;
+   for (uint64 i = 0; i < n; i++) {
+      rfr_stack *s = stacks[filter_stack[filter_id[i]]];
+      key        k = key_create(FALSE, key_len, keys + i * key_len);
+      routing_filter_lookup_async_state_init(&st[i], (cache *)&s->cc, &s->rcfg, filters[filter_id[i]], k,
+                                             &found[i], count_callback, &cb);
       routing_filter_lookup_async(&st[i]);
    }
    rfr_async_flush();

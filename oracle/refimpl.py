@@ -112,6 +112,10 @@ def lib(path=LIB_PATH):
         L.rfr_async_config.restype = i32
         L.rfr_lookup_keys_async_flush.argtypes = [vp, vp, vp, vp, u32, u64, vp]
         L.rfr_lookup_keys_async_flush.restype = u64
+        L.rfr_lookup_keys_async_flush_multi.argtypes = [vp, vp, vp, vp, vp, u32, u64, vp]
+        L.rfr_lookup_keys_async_flush_multi.restype = u64
+        L.rfr_async_breakdown.argtypes = [vp]
+        L.rfr_async_breakdown.restype = ctypes.c_int
         if hasattr(L, "rfr_filter_test_basic"):  # the filter_test libraries only
             L.rfr_filter_test_basic.argtypes = [vp, u64, u64, u64, ctypes.c_char_p]
             L.rfr_filter_test_basic.restype = i32
@@ -370,6 +374,20 @@ class Stack:
                                                 _p(k), key_len, n, _p(out))
         return out, (None if cb == (1 << 64) - 1 else int(cb))
 
+    def lookup_keys_async_flush_multi(self, stacks, descs, filter_stack, keys, filter_id, key_len=24):
+        """async states over filters of several stacks of this library (descs[f] belongs to
+        stacks[filter_stack[f]]), all queued, then ONE routing_filter_amd_flush()"""
+        k = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = k.size // key_len
+        arr = (RoutingFilter * max(1, len(descs)))(*descs)
+        hs = (ctypes.c_void_p * len(stacks))(*[st.h for st in stacks])
+        fs = np.ascontiguousarray(filter_stack, dtype=np.uint32)
+        fid = np.ascontiguousarray(filter_id, dtype=np.uint32)
+        out = np.zeros(n, dtype=np.uint64)
+        cb = self.L.rfr_lookup_keys_async_flush_multi(ctypes.addressof(hs), ctypes.addressof(arr), _p(fs), _p(fid),
+                                                      _p(k), key_len, n, _p(out))
+        return out, (None if cb == (1 << 64) - 1 else int(cb))
+
     def mt_chains(self, keys, threads, rounds, n, probe, nprobe, key_len=24):
         """threads x rounds incremental chains built by `threads` concurrent threads
         (oracle/ref_harness.c rfr_mt_chains), then each thread's nprobe lookups of its probe
@@ -395,6 +413,17 @@ class Stack:
             return None
         return dict(zip(("add_batches", "add_filters", "registry_bytes", "evictions", "trims", "async_probe_ns"),
                         (int(x) for x in out)))
+
+    def async_breakdown(self):
+        """the shim's async completion path so far: batches, states, ns in the burst wait /
+        batch gathering / lookup_many / callbacks, and the engine's lookup round trips (calls,
+        prep / launch / wait ns); None for the reference's library"""
+        out = np.zeros(10, dtype=np.uint64)
+        if not self.L.rfr_async_breakdown(_p(out)):
+            return None
+        keys = ("batches", "states", "burst_ns", "gather_ns", "lookup_ns", "callback_ns",
+                "rt_calls", "rt_prep_ns", "rt_launch_ns", "rt_wait_ns")
+        return dict(zip(keys, (int(x) for x in out)))
 
     def async_many_phases(self):
         """(start, poll) nanoseconds of the last lookup_keys_async_many call"""

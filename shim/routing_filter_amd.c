@@ -939,11 +939,14 @@ group_map_deinit(group_map *m)
    free(m->gid);
 }
 
-/* the group of (cc, addr); *is_new when this call created it as group `next` */
+/* the group of (cc, addr); *is_new when this call created it as group `next`. The start slot
+ * takes all 64 bits of the mix (registry_bucket keeps only 12: tables over 4,096 slots would
+ * cluster in their first 4,096) */
 static uint32
 group_map_get(group_map *m, const cache *cc, uint64 addr, uint32 next, int *is_new)
 {
-   uint64 s = registry_bucket(cc, addr) & m->mask;
+   uint64 x = ((addr >> 12) ^ (uint64)(uintptr_t)cc) * 0x9E3779B97F4A7C15ull;
+   uint64 s = (x ^ (x >> 29)) & m->mask;
    for (;; s = (s + 1) & m->mask) {
       if (m->gid[s] == UINT32_MAX) {
          m->key_addr[s] = addr;
@@ -1044,6 +1047,10 @@ static pthread_mutex_t g_aq_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t  g_aq_cv;
 static pthread_once_t  g_aq_once = PTHREAD_ONCE_INIT;
 static uint64          g_async_batches, g_async_probes, g_async_probe_ns;
+/* per-phase totals of the completion path (routing_filter_amd_async_breakdown): ns spent
+ * waiting for a burst to settle, gathering a batch (before lookup_many), in lookup_many (its
+ * host work plus the GPU round trip), firing callbacks */
+static uint64          g_async_burst_ns, g_async_gather_ns, g_async_cb_ns;
 static uint64          g_async_limit, g_async_window_ns, g_async_threads;
 
 #define AQ_NEXT(st) (*(rf_state **)&(st)->index_page)
@@ -1056,6 +1063,7 @@ complete_states(rf_state *list, uint64 n)
    if (n == 0) {
       return;
    }
+   const uint64          tg   = now_ns();
    rf_state             **q    = malloc(sizeof(*q) * n);
    cache               **ccs   = malloc(sizeof(*ccs) * n);
    const routing_config **cfgs = malloc(sizeof(*cfgs) * n);
@@ -1075,7 +1083,9 @@ complete_states(rf_state *list, uint64 n)
    }
    const uint64 t0 = now_ns();
    lookup_many(ccs, cfgs, fl, h, m, found, rc);
-   __atomic_fetch_add(&g_async_probe_ns, now_ns() - t0, __ATOMIC_RELAXED);
+   const uint64 t1 = now_ns();
+   __atomic_fetch_add(&g_async_gather_ns, t0 - tg, __ATOMIC_RELAXED);
+   __atomic_fetch_add(&g_async_probe_ns, t1 - t0, __ATOMIC_RELAXED);
    for (uint64 i = 0; i < m; i++) {
       rf_state         *st  = q[i];
       async_callback_fn cb  = st->callback;
@@ -1088,6 +1098,7 @@ complete_states(rf_state *list, uint64 n)
          cb(arg);
       }
    }
+   __atomic_fetch_add(&g_async_cb_ns, now_ns() - t1, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_batches, 1, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_probes, m, __ATOMIC_RELAXED);
    free(q);
@@ -1149,6 +1160,7 @@ completion_main(void *arg)
                tc = t;
             }
          }
+         __atomic_fetch_add(&g_async_burst_ns, t - t0, __ATOMIC_RELAXED);
       }
       const uint64 window = __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED);
       if (window) { /* optional coalescing window after the first arrival */
@@ -1231,6 +1243,19 @@ routing_filter_amd_async_stats(uint64 *batches, uint64 *probes)
 {
    *batches = __atomic_load_n(&g_async_batches, __ATOMIC_RELAXED);
    *probes  = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED);
+}
+
+/* out[0..5]: batches, states, then ns totals of the completion path's phases: burst wait,
+ * batch gathering, lookup_many (host work + GPU round trip), callbacks */
+void
+routing_filter_amd_async_breakdown(uint64 *out)
+{
+   out[0] = __atomic_load_n(&g_async_batches, __ATOMIC_RELAXED);
+   out[1] = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED);
+   out[2] = __atomic_load_n(&g_async_burst_ns, __ATOMIC_RELAXED);
+   out[3] = __atomic_load_n(&g_async_gather_ns, __ATOMIC_RELAXED);
+   out[4] = __atomic_load_n(&g_async_probe_ns, __ATOMIC_RELAXED);
+   out[5] = __atomic_load_n(&g_async_cb_ns, __ATOMIC_RELAXED);
 }
 
 uint64

@@ -27,6 +27,10 @@ routing_filter_amd_async_stats(uint64 *batches, uint64 *probes);
 /* nanoseconds spent so far probing queued states (grouping, residency, the GPU round trip) */
 uint64
 routing_filter_amd_async_probe_ns(void);
+/* out[0..5]: async batches, states, ns of the burst wait, batch gathering, lookup_many and
+ * callbacks (diagnostics) */
+void
+routing_filter_amd_async_breakdown(uint64 *out);
 
 /* routing_filter_add calls coalesced: GPU batches built and filters they held */
 void

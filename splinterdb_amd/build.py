@@ -11,9 +11,20 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "librf_amd.so")
 LIB_STAMPS = os.path.join(HERE, "librf_amd_stamps.so")  # diagnostics: per-phase clock stamps
 SOURCES = ["rf_kernels.hip", "rf_engine.cpp"]
-HEADERS = ["rf_device.h", "rf_plan.h", "../../include/rf_amd.h"]
+HEADERS = ["rf_device.h", "rf_plan.h", "../../include/rf_amd.h", "../../include/rf_amd_diag.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+
+
+def source_id():
+    """16 hex digits of SHA-256 over the engine's sources and headers: compiled into the
+    library (rf_amd_build_id), so a loaded library can be checked against the tree"""
+    import hashlib
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 
 def _stale(lib=LIB):
@@ -34,7 +45,8 @@ def build(force=False, verbose=False, stamps=False):
     for src in SOURCES:
         obj = os.path.join(CSRC, os.path.splitext(src)[0] + ("_stamps.o" if stamps else ".o"))
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-               "-Wall", "-Wno-unused-function", "-c", os.path.join(CSRC, src), "-o", obj]
+               "-Wall", "-Wno-unused-function", f'-DRF_AMD_SRC_ID="{source_id()}"',
+               "-c", os.path.join(CSRC, src), "-o", obj]
         if stamps:
             cmd.insert(1, "-DRF_PHASE_STAMPS")
         if src.endswith(".cpp"):

@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <map>
 #include <atomic>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "../../include/rf_amd.h"
+#include "../../include/rf_amd_diag.h"
 #include "rf_plan.h"
 
 using namespace rf;
@@ -36,9 +38,6 @@ extern "C" int rf_launch_probe(const LaunchArgs* a, int kind, const void* in0, c
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found);
 
 static thread_local std::string g_err;
-#ifdef RF_PHASE_STAMPS
-static uint32_t g_probe_ablate = 0;  // diagnostics library only (rf_amd_debug_probe_ablate)
-#endif
 static int fail(int rc, const std::string& msg) {
   g_err = msg;
   return rc;
@@ -236,7 +235,9 @@ struct rf_amd_batch {
       d_old_idx_filter, d_old32, d_old_tot, d_ob_lo, d_ob_n, d_pg_noline, d_cb_out;
   bool built = false;
   bool has_entries = false;  // built here: its sorted entries (d_part / d_sorted) are current
-  std::vector<uint32_t> err_host;  // per-filter build error bits once read back (empty: not yet)
+  std::vector<uint32_t> err_host;  // per-filter build error bits once read back (err_ready)
+  std::atomic<bool> err_ready{false};
+  std::mutex err_mu;
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
   uint32_t ev_mask = EV_MASK_ALL;     // EV_MASK_PROBE: the probe's two events only
@@ -827,8 +828,11 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
     int rc = rf_launch_old_decode(&a);
     if (rc) return fail(RF_AMD_EINVAL, std::string("old decode launch: ") + hipGetErrorString((hipError_t)rc));
   }
-  if (st == b->eng->stream) b->eng->builds_issued.fetch_add(1, std::memory_order_acq_rel);
+  b->err_ready.store(false, std::memory_order_release);  // a rebuild: read the new bits back
   int rc = rf_launch_build(&a);
+  // counted once every kernel of the build is queued: a lookup that finds the stream idle
+  // after reading this count cannot miss a build it covers
+  if (st == b->eng->stream) b->eng->builds_issued.fetch_add(1, std::memory_order_acq_rel);
   if (rc) return fail(RF_AMD_EINVAL, std::string("build launch: ") + hipGetErrorString((hipError_t)rc));
   b->built = true;
   b->has_entries = true;
@@ -932,8 +936,8 @@ extern "C" int rf_amd_batch_build_hashes_host(rf_amd_batch* b, const uint32_t* h
 
 // ---- host-buffer lookups over the engine's lookup slots (ProbeSlot) -----------------------
 extern "C" int rf_launch_probe_groups(void* stream, const uint32_t* in, const ProbeGroup* groups, uint32_t ng,
-                                      uint64_t n, uint64_t* found, uint32_t fp_size, uint32_t lis,
-                                      uint32_t* counter, uint32_t* done_flag, uint32_t seq);
+                                      uint64_t n, uint64_t* found, uint32_t* counter, uint32_t* done_flag,
+                                      uint32_t seq);
 extern "C" int rf_launch_probe_small(void* stream, const SmallProbe* a);
 
 static ProbeSlot* slot_take(rf_amd_engine* e) {
@@ -999,12 +1003,18 @@ static int slot_reserve(ProbeSlot* s, size_t hbytes, size_t dbytes) {
 // per-filter build error bits of a built batch, read back once (a batch is immutable once
 // built; a filter whose build failed finds nothing, as k_probe does through pplans.w)
 static int batch_errors(rf_amd_batch* b) {
-  if (!b->err_host.empty()) return 0;
+  // concurrent lookups of one batch may both get here first (rf_amd.h: host lookups are
+  // thread-safe): the read-back happens once, under the batch's lock, and err_host is
+  // published (err_ready) only once filled
+  if (b->err_ready.load(std::memory_order_acquire)) return 0;
+  std::lock_guard<std::mutex> lk(b->err_mu);
+  if (b->err_ready.load(std::memory_order_relaxed)) return 0;
   std::vector<FilterOut> o(b->F);
   HIPCHK(hipMemcpyAsync(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost, b->eng->stream));
   HIPCHK(hipStreamSynchronize(b->eng->stream));
   b->err_host.resize(b->F);
   for (uint32_t f = 0; f < b->F; f++) b->err_host[f] = o[f].error;
+  b->err_ready.store(true, std::memory_order_release);
   return 0;
 }
 
@@ -1013,6 +1023,8 @@ static ProbeGroup probe_group_of(const rf_amd_batch* b, uint32_t f) {
   ProbeGroup g;
   g.x = p.vs | (p.rem << 8) | (p.rvs << 16) | (p.lg_line << 24);
   g.err = b->err_host[f];
+  g.fpl = b->cfg.fingerprint_size | (b->cfg.log_index_size << 8);
+  g.pad = 0;
   g.lines = b->d_lines.as<uint4>() + 4ull * p.line_base;
   g.pages = b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size;
   g.slots = b->d_slots.as<uint64_t>() + p.idx_base;
@@ -1055,9 +1067,44 @@ static int slot_wait(ProbeSlot* s, uint32_t seq, bool sync) {
   }
 }
 
-static int probe_groups_host(rf_amd_engine* e, const rf_amd_config& cfg, const std::vector<ProbeGroup>& groups,
+// where a host-buffer lookup round trip spends its time (rf_amd_diag_lookup_stats): calls,
+// ns before the launch (slot, buffers, build ordering, argument packing), ns in the launch
+// call, ns waiting for the completion word (and copying the results out)
+static std::atomic<uint64_t> g_lk_calls{0}, g_lk_prep_ns{0}, g_lk_launch_ns{0}, g_lk_wait_ns{0};
+static inline uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+struct LookupClock {
+  uint64_t t0 = mono_ns(), t1 = 0, t2 = 0;
+  void launching() { t1 = mono_ns(); }
+  void launched() { t2 = mono_ns(); }
+  ~LookupClock() {
+    if (!t2) return;  // failed before the launch
+    const uint64_t t3 = mono_ns();
+    g_lk_calls.fetch_add(1, std::memory_order_relaxed);
+    g_lk_prep_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
+    g_lk_launch_ns.fetch_add(t2 - t1, std::memory_order_relaxed);
+    g_lk_wait_ns.fetch_add(t3 - t2, std::memory_order_relaxed);
+  }
+};
+#ifndef RF_AMD_SRC_ID
+#define RF_AMD_SRC_ID "unknown"
+#endif
+extern "C" const char* rf_amd_build_id(void) { return RF_AMD_SRC_ID; }
+
+extern "C" int rf_amd_diag_lookup_stats(uint64_t* out, int reset) {
+  if (!out) return fail(RF_AMD_EINVAL, "null output");
+  std::atomic<uint64_t>* c[4] = {&g_lk_calls, &g_lk_prep_ns, &g_lk_launch_ns, &g_lk_wait_ns};
+  for (int k = 0; k < 4; k++) out[k] = reset ? c[k]->exchange(0) : c[k]->load();
+  return 0;
+}
+
+static int probe_groups_host(rf_amd_engine* e, const std::vector<ProbeGroup>& groups,
                              const uint32_t* h_hashes, const uint32_t* h_group, uint64_t n, uint64_t* h_found) {
   if (n == 0) return 0;
+  LookupClock clk;
   static const int mode = env_mode("RF_AMD_PROBE_MODE", "mapped", "copy");
   static const int wait = env_mode("RF_AMD_PROBE_WAIT", "flag", "sync");
   static const bool small_ok = !getenv("RF_AMD_PROBE_SMALL") || atoi(getenv("RF_AMD_PROBE_SMALL")) != 0;
@@ -1092,8 +1139,6 @@ static int probe_groups_host(rf_amd_engine* e, const rf_amd_config& cfg, const s
     memset(&sp, 0, sizeof(sp));
     sp.n = (uint32_t)n;
     sp.ng = ng;
-    sp.fp_size = cfg.fingerprint_size;
-    sp.lis = cfg.log_index_size;
     sp.seq = seq;
     for (uint64_t i = 0; i < n; i++) {
       sp.h[i] = h_hashes[i];
@@ -1103,8 +1148,10 @@ static int probe_groups_host(rf_amd_engine* e, const rf_amd_config& cfg, const s
     for (uint32_t g = 0; g < ng; g++) sp.groups[g] = groups[g];
     sp.found = reinterpret_cast<uint64_t*>(s->h);
     sp.done_flag = s->flag;
+    clk.launching();
     if (int rc = rf_launch_probe_small(s->st, &sp))
       return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
+    clk.launched();
     if (int rc = slot_wait(s, seq, false)) return rc;
     memcpy(h_found, s->h, 8 * n);
     return 0;
@@ -1120,11 +1167,12 @@ static int probe_groups_host(rf_amd_engine* e, const rf_amd_config& cfg, const s
     in = s->d;
   }
   uint64_t* found = reinterpret_cast<uint64_t*>(s->h + o_f);
+  clk.launching();
   if (int rc = rf_launch_probe_groups(s->st, reinterpret_cast<const uint32_t*>(in),
                                       reinterpret_cast<const ProbeGroup*>(in + o_g), ng, n, found,
-                                      cfg.fingerprint_size, cfg.log_index_size, s->d_counter,
-                                      wait == 2 ? nullptr : s->flag, seq))
+                                      s->d_counter, wait == 2 ? nullptr : s->flag, seq))
     return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
+  clk.launched();
   if (int rc = slot_wait(s, seq, wait == 2)) return rc;
   memcpy(h_found, found, 8 * n);
   return 0;
@@ -1140,7 +1188,7 @@ extern "C" int rf_amd_batch_probe_hashes_host(rf_amd_batch* b, const uint32_t* h
   if (int rc = batch_errors(b)) return rc;
   std::vector<ProbeGroup> groups(h_filter_id ? b->F : 1);  // group = filter id (ids >= F find nothing)
   for (uint32_t f = 0; f < groups.size(); f++) groups[f] = probe_group_of(b, f);
-  return probe_groups_host(e, b->cfg, groups, h_hashes, h_filter_id, n, h_found);
+  return probe_groups_host(e, groups, h_hashes, h_filter_id, n, h_found);
 }
 
 extern "C" int rf_amd_probe_filters_host(rf_amd_engine* e, rf_amd_batch* const* batches, const uint32_t* filter_index,
@@ -1151,24 +1199,22 @@ extern "C" int rf_amd_probe_filters_host(rf_amd_engine* e, rf_amd_batch* const* 
   if (n == 0) return 0;
   if (!h_hashes || !h_found) return fail(RF_AMD_EINVAL, "null probe buffer");
   HIPCHK(hipSetDevice(e->device));
+  // each group carries its own batch's routing config: filters of kvstores with different
+  // fingerprint or index sizes go out in the same launch
   std::vector<ProbeGroup> groups(num_groups);
-  const rf_amd_config* cfg = nullptr;
   for (uint32_t g = 0; g < num_groups; g++) {
     rf_amd_batch* b = batches[g];
     const uint32_t f = filter_index ? filter_index[g] : 0u;
     if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "group on an unbuilt or foreign batch");
     if (f >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
-    if (!cfg) cfg = &b->cfg;
-    else if (b->cfg.fingerprint_size != cfg->fingerprint_size || b->cfg.log_index_size != cfg->log_index_size)
-      return fail(RF_AMD_EINVAL, "groups of one lookup call must share fingerprint_size and log_index_size");
     if (int rc = batch_errors(b)) return rc;
     groups[g] = probe_group_of(b, f);
   }
-  if (!cfg) {  // no filters: nothing found
+  if (!num_groups) {  // no filters: nothing found
     memset(h_found, 0, 8 * n);
     return 0;
   }
-  return probe_groups_host(e, *cfg, groups, h_hashes, h_group, n, h_found);
+  return probe_groups_host(e, groups, h_hashes, h_group, n, h_found);
 }
 
 // Lookups against many resident filters in ONE launch: group g probes counts[g] hashes
@@ -1200,11 +1246,6 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   LaunchArgs a = make_args(b, st);
   a.probe_runs = d_runs;
   a.wave_tab = d_runs ? b->d_wave_tab.as<uint32_t>() : nullptr;
-#ifdef RF_PHASE_STAMPS
-  a.ablate = g_probe_ablate & 0xff;
-  a.occ = (g_probe_ablate >> 8) & 0xff;
-  a.ppl = (g_probe_ablate >> 16) & 0xff;
-#endif
   int rc = rf_launch_probe(&a, kind, in0, offs, key_len, fid, n, found);
   if (rc) return fail(RF_AMD_EINVAL, std::string("probe launch: ") + hipGetErrorString((hipError_t)rc));
   return 0;
@@ -1264,18 +1305,15 @@ extern "C" int rf_amd_batch_probe_hashes_runs(rf_amd_batch* b, const uint32_t* d
 // Diagnostic (diagnostics library only; EINVAL in the product): low byte 1 = hash only,
 // 2 = + probe line load; 0 = normal probe. Bits 8-15: cap the probe kernel at that many
 // waves per SIMD via LDS padding; bits 16-23: probes per lane.
-extern "C" int rf_amd_debug_probe_ablate(uint32_t mode) {
-#ifdef RF_PHASE_STAMPS
-  g_probe_ablate = mode;
-  return 0;
-#else
-  return mode ? fail(RF_AMD_EINVAL, "probe ablation exists only in the diagnostics library") : 0;
-#endif
-}
 
 extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid);
 extern "C" int rf_amd_debug_phase_buffer(void* d_buf, uint32_t kernel) {
+#ifdef RF_PHASE_STAMPS
   return rf_debug_set_phase_buffer(static_cast<uint64_t*>(d_buf), kernel) ? fail(RF_AMD_EINVAL, "phase buffer") : 0;
+#else
+  (void)kernel;
+  return d_buf ? fail(RF_AMD_EINVAL, "phase stamps exist only in the diagnostics library") : 0;
+#endif
 }
 
 extern "C" int rf_amd_debug_read_lines(rf_amd_batch* b, uint8_t* h_lines, uint64_t bytes, uint64_t* num_lines) {
@@ -1369,8 +1407,12 @@ extern "C" int rf_amd_batch_infos(rf_amd_batch* b, rf_amd_filter_info* out, void
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost));
   }
-  b->err_host.resize(b->F);
-  for (uint32_t f = 0; f < b->F; f++) b->err_host[f] = o[f].error;
+  {
+    std::lock_guard<std::mutex> lk(b->err_mu);
+    b->err_host.resize(b->F);
+    for (uint32_t f = 0; f < b->F; f++) b->err_host[f] = o[f].error;
+    b->err_ready.store(true, std::memory_order_release);
+  }
   for (uint32_t f = 0; f < b->F; f++) {
     const FilterPlan& p = b->plans[f];
     out[f].num_fingerprints = p.num_fp;
@@ -1518,6 +1560,7 @@ static int batch_import(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t F, 
   }
   HIPCHK(hipStreamSynchronize(st));  // host vectors above are released on return
   b->err_host.assign(F, 0u);  // imports carry no error bits (checked above)
+  b->err_ready.store(true, std::memory_order_release);
   b->built = true;
   *out = b;
   return 0;

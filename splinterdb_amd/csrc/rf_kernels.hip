@@ -307,13 +307,6 @@ __device__ uint32_t g_dbg_kid = 0;
 // Compiled in only for the diagnostics library (RF_PHASE_STAMPS, build.py stamps=True):
 // reading the stamp buffer pointer is a vector load whose wait (vmcnt(0)) would also wait
 // for every load or atomic the kernel has in flight at that point.
-// Probe ablation / occupancy experiments (rf_amd_debug_probe_ablate) exist only in the
-// diagnostics library as well; the product's k_probe has no such branches.
-#ifdef RF_PHASE_STAMPS
-#define RF_DIAG 1
-#else
-#define RF_DIAG 0
-#endif
 #ifdef RF_PHASE_STAMPS
 #define DBG_PHASE_K(kid, k)                                                  \
   do {                                                                       \
@@ -2778,33 +2771,17 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
 #ifndef RF_PROBE_NT
 #define RF_PROBE_NT 1024
 #endif
+// quad-cooperative probe-line gather (k_probe); 0 = one lane loads its own line
+#ifndef RF_PROBE_QUAD
+#define RF_PROBE_QUAD 1
+#endif
 constexpr int PROBE_NT = RF_PROBE_NT;
 constexpr int PROBE_NT_VAR = 256;
 __host__ __device__ constexpr int probe_nt(int kind) { return kind == IN_VAR ? PROBE_NT_VAR : PROBE_NT; }
-constexpr int PROBE_LDS_PAD = 0;
-constexpr int PROBE_PPL = 1;  // probes per lane (production)
 
-// One lane per probe. (A cooperative variant that staged 128-byte block heads through LDS,
-// 8 lanes per block, measured slower on MI355X -- 3.09 vs 2.34 ms at C2 -- the kernel is
-// bound by random L2 line fetches, not load-instruction issue; it was removed.)
-// OCC_LDS > 0 pads LDS to cap workgroups per CU (occupancy experiments; 0 = none).
-// A lane handles PPL probes (i, i + PROBE_NT, ...): all their key loads, then all their
-// line loads, then the decodes -- PPL independent random line fetches in flight per lane.
-// filter of probe i when the probes come as per-filter runs: runs[f] <= i < runs[f + 1].
-// The search runs once per wave on its first probe (wave-uniform: scalar loads); lanes past
-// a run boundary step forward.
-__device__ __forceinline__ uint32_t run_filter(const uint64_t* __restrict__ runs, uint32_t nf, uint64_t i) {
-  const uint64_t wf = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(i >> 32)) << 32) |
-                      __builtin_amdgcn_readfirstlane((uint32_t)i);
-  uint32_t lo = 0, hi = nf;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (runs[mid] <= wf) lo = mid; else hi = mid;
-  }
-  while (lo + 1 < nf && runs[lo + 1] <= i) lo++;
-  return lo;
-}
-
+// One lane per probe for hashing and decoding. (A cooperative variant that staged 128-byte
+// block heads through LDS, 8 lanes per block, measured slower on MI355X -- 3.09 vs 2.34 ms at
+// C2; the quad gather below keeps the decode per lane and moves only the line through LDS.)
 // Wave table of per-filter probe runs: entry w = (filter of probe 64 w) << 7 | the number of
 // the wave's leading probes in that filter's run (64: the whole wave). Built by k_wave_tab
 // whenever the run bounds change, so a probe wave finds its filter with ONE scalar load
@@ -2891,7 +2868,7 @@ __device__ __forceinline__ uint64_t probe_walk(const uint4 P, uint32_t h, uint32
   return probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, pg, hdr, lis);
 }
 
-template <int KIND, int OCC_LDS = 0, int PPL = 1>
+template <int KIND>
 __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restrict__ pplans,
                                                     const FilterPlan* __restrict__ plans,
                                                     const uint8_t* __restrict__ pages,
@@ -2904,35 +2881,31 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
                                                     const uint32_t* __restrict__ wave_tab, uint64_t n,
                                                     uint64_t* __restrict__ found, uint32_t fp_size,
                                                     uint32_t seed, uint32_t lis, uint32_t page_size,
-                                                    uint32_t num_filters, uint32_t ablate) {
-#if RF_DIAG
-  if constexpr (OCC_LDS > 0) {
-    __shared__ uint32_t s_pad[OCC_LDS / 4];
-    if (ablate == 0xdead) s_pad[threadIdx.x] = 0;  // keeps the pad allocated
-  }
-#else
-  (void)ablate;
-#endif
+                                                    uint32_t num_filters) {
   constexpr int NT = probe_nt(KIND);
-  const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (NT * PPL) + threadIdx.x;
-  uint32_t h[PPL], fid[PPL];
-  uint4 pp[PPL];
-  constexpr bool WAVE_KEYS = KIND == IN_KEYS24 && PPL == 1 && OCC_LDS == 0;
+  const uint64_t i0 = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * NT + threadIdx.x;
+  uint32_t h = 0, fid = 0xffffffffu;
+  uint4 pp = make_uint4(0, 0, 0, 1);
+  constexpr bool WAVE_KEYS = KIND == IN_KEYS24;
+  constexpr bool WAVE_VAR = KIND == IN_VAR;
+  // per wave: the 24-byte keys' staging (96 x 16 B), then the quad-gathered probe lines
+  // (64 x 64 B); variable-length keys stage their window in s_vk and reuse it for the lines
+  constexpr bool QUAD = RF_PROBE_QUAD;
+  constexpr int WBUF = (QUAD && !WAVE_VAR) ? 256 : (WAVE_KEYS ? 96 : 1);
+  __shared__ v4u s_wbuf[NT / WAVE][WBUF];
+  constexpr uint32_t VCAP = 4096;
+  __shared__ __attribute__((aligned(16))) uint32_t s_vk[WAVE_VAR ? NT / WAVE : 1][WAVE_VAR ? VCAP / 4 + 4 : 1];
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t wf = i0 - lane;  // the wave's first probe
   if constexpr (WAVE_KEYS) {
     // 24-byte keys: the wave's 64 keys (1,536 contiguous bytes) are read with 16-byte
     // coalesced loads -- 12 cache lines per wave, where three strided 8-byte loads per lane
     // touch 36 -- and handed to their lanes through LDS
-    __shared__ v4u s_keys[NT / WAVE][96];
-    const uint32_t lane = threadIdx.x & (WAVE - 1);
-    const uint64_t wf = i0 - lane;
-    fid[0] = 0xffffffffu;
-    h[0] = 0;
-    pp[0] = make_uint4(0, 0, 0, 1);
     if (wf < n) {  // uniform per wave
-      if (i0 < n) fid[0] = runs ? tab_filter(wave_tab, runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
-      pp[0] = load_pplan(pplans, fid[0], num_filters);  // in flight with the key loads
+      if (i0 < n) fid = runs ? tab_filter(wave_tab, runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
+      pp = load_pplan(pplans, fid, num_filters);  // in flight with the key loads
       if (((uintptr_t)in0 & 15) == 0) {
-        v4u* sw = s_keys[threadIdx.x / WAVE];
+        v4u* sw = s_wbuf[threadIdx.x / WAVE];
         const uint32_t bytes = (uint32_t)min<uint64_t>(WAVE, n - wf) * 24;
         const v4u* src = reinterpret_cast<const v4u*>(static_cast<const uint8_t*>(in0) + wf * 24);
         if (bytes == WAVE * 24) {  // full wave: LDS-DMA, no VGPR round trip
@@ -2961,197 +2934,121 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
           const uint2* k2 = reinterpret_cast<const uint2*>(sw) + 3 * lane;
           const uint2 a = k2[0], b = k2[1], c = k2[2];
           uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-          h[0] = xxh32_24(w, seed);
+          h = xxh32_24(w, seed);
         }
       } else if (i0 < n) {
-        h[0] = hash_key<KIND, true>(in0, offs, key_len, seed, i0);
+        h = hash_key<KIND, true>(in0, offs, key_len, seed, i0);
       }
     }
-  }
-  constexpr bool WAVE_VAR = KIND == IN_VAR && PPL == 1 && OCC_LDS == 0;
-  if constexpr (WAVE_VAR) {
+  } else if constexpr (WAVE_VAR) {
     // variable-length keys: the wave's 64 keys are one contiguous byte range, read into a
     // 4 KiB LDS window with coalesced 16-byte loads and hashed from there (wave_hash_var)
-    constexpr uint32_t VCAP = 4096;
-    __shared__ __attribute__((aligned(16))) uint32_t s_vk[NT / WAVE][VCAP / 4 + 4];
-    fid[0] = 0xffffffffu;
-    h[0] = 0;
     uint64_t o0 = 0, o1 = 0;
     if (i0 < n) {
-      fid[0] = runs ? tab_filter(wave_tab, runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
+      fid = runs ? tab_filter(wave_tab, runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
       o0 = offs[i0];
       o1 = offs[i0 + 1];
     }
-    pp[0] = load_pplan(pplans, fid[0], num_filters);
+    pp = load_pplan(pplans, fid, num_filters);
     uint64_t w0 = 0, w1 = 0;
-    h[0] = wave_hash_var<VCAP, true>(static_cast<const uint8_t*>(in0), o0, o1, i0 < n,
-                                     s_vk[threadIdx.x / WAVE], seed, &w0, &w1);
-  }
-  // the keys (or hashes) and filter ids are independent loads: issue them all together
-#pragma unroll
-  for (int q = 0; q < PPL; q++) {
-    if constexpr (WAVE_KEYS || WAVE_VAR) break;
-    const uint64_t i = i0 + (uint64_t)q * NT;
-    fid[q] = 0xffffffffu;
-    h[q] = 0;
-    if (i < n) {
+    h = wave_hash_var<VCAP, true>(static_cast<const uint8_t*>(in0), o0, o1, i0 < n, s_vk[threadIdx.x / WAVE], seed,
+                                  &w0, &w1);
+  } else {
+    // the key (or hash) and filter id are independent loads: issued together
+    if (i0 < n) {
       if constexpr (KIND == IN_PAIR) {  // routed probes: (local filter id << 32 | hash)
-        const uint64_t pr = __builtin_nontemporal_load(static_cast<const uint64_t*>(in0) + i);
-        fid[q] = (uint32_t)(pr >> 32);
-        h[q] = (uint32_t)pr;
+        const uint64_t pr = __builtin_nontemporal_load(static_cast<const uint64_t*>(in0) + i0);
+        fid = (uint32_t)(pr >> 32);
+        h = (uint32_t)pr;
       } else {
-        fid[q] = runs ? (PPL == 1 ? tab_filter(wave_tab, runs, num_filters, i) : run_filter(runs, num_filters, i))
-                      : __builtin_nontemporal_load(filter_id + i);
-        h[q] = hash_key<KIND, true>(in0, offs, key_len, seed, i);
+        fid = runs ? tab_filter(wave_tab, runs, num_filters, i0) : __builtin_nontemporal_load(filter_id + i0);
+        h = hash_key<KIND, true>(in0, offs, key_len, seed, i0);
       }
     }
-    pp[q] = load_pplan(pplans, fid[q], num_filters);
+    pp = load_pplan(pplans, fid, num_filters);
   }
-#if !RF_DIAG
-  if constexpr (PPL == 1) {
-    if (i0 >= n) return;
-    const uint32_t fs = __builtin_amdgcn_readfirstlane(fid[0]);
-    uint64_t r;
-    bool ok;
-    if (__builtin_amdgcn_ballot_w64(fid[0] != fs) == 0) {
-      const uint4 U = make_uint4(__builtin_amdgcn_readfirstlane(pp[0].x), __builtin_amdgcn_readfirstlane(pp[0].y),
-                                 __builtin_amdgcn_readfirstlane(pp[0].z), __builtin_amdgcn_readfirstlane(pp[0].w));
-      ok = probe_line(U, h[0], lines, fp_size, r);
-    } else {
-      ok = probe_line(pp[0], h[0], lines, fp_size, r);
-    }
-    if (!ok) r = probe_walk(pp[0], h[0], fid[0], plans, pages, slots, fp_size, lis, page_size);
-    __builtin_nontemporal_store(r, found + i0);
-    return;
-  }
-#endif
-  uint32_t bucket[PPL], remainder[PPL];
-  v4u Q[PPL][4];
-#pragma unroll
-  for (int q = 0; q < PPL; q++) {
-    // unknown filter, or one whose build failed (k_layout sets pp.w): nothing found
-    const uint32_t rem = (pp[q].x >> 8) & 0xff, lgl = pp[q].x >> 24;
-    const uint32_t fp = h[q] >> (32 - fp_size);
-    bucket[q] = rem >= 32 ? 0u : fp >> rem;  // index << lis | bucket in index
-    remainder[q] = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-#if RF_DIAG
-    const bool load_line = !pp[q].w && lgl && ablate != 1;
-#else
-    const bool load_line = !pp[q].w && lgl;
-#endif
-    if (load_line) {
-      const v4u* lp = reinterpret_cast<const v4u*>(lines + ((uint64_t)pp[q].y + (bucket[q] >> (lgl - 1))) * 4);
-#pragma unroll
-      for (int k = 0; k < 4; k++) Q[q][k] = lp[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; k++) Q[q][k] = v4u{~0u, ~0u, ~0u, ~0u};  // "overflowed": image path
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < PPL; q++) {
-    const uint64_t i = i0 + (uint64_t)q * NT;
-    if (i >= n) continue;
-    uint64_t r = 0;
-    if (pp[q].w) {
-      r = 0;
-#if RF_DIAG
-    } else if (ablate == 1) {  // diagnostic: key stream + hash only
-      r = h[q];
-    } else if (ablate == 2) {  // diagnostic: + the line load
-      r = (uint64_t)Q[q][0].x ^ Q[q][3].w ^ h[q];
-#endif
-    } else {
-      const uint32_t vs = pp[q].x & 0xff, rvs = (pp[q].x >> 16) & 0xff, lgl = pp[q].x >> 24;
-      const uint32_t G = lgl ? 1u << (lgl - 1) : 1u;
-      if (!lgl || !line_decode(Q[q], bucket[q] & (G - 1), remainder[q], vs, rvs, r)) {
-        // overflowed line (or no lines): walk the image from the index slot
-        const uint64_t hdr = slots[pp[q].z + (bucket[q] >> lis)];
-        const uint8_t* pg = pages + (uint64_t)plans[fid[q]].page_base * page_size;
-        r = probe_stream(bucket[q] & ((1u << lis) - 1), remainder[q], vs, rvs, pg, hdr, lis);
-      }
-    }
-    __builtin_nontemporal_store(r, found + i);
-  }
-}
-
-// ---- persistent, software-pipelined probe (24-byte keys, probes in per-filter runs) -----
-// The same lookups as k_probe's WAVE_KEYS path, but each wave loops over its XCD's 64-probe
-// tiles and fetches tile k+1's keys (LDS-DMA into the other half of a two-tile buffer) while
-// tile k's hashes are computed and its probe lines are in flight: per wave one key fetch and
-// 64 line fetches overlap, where k_probe's one-tile waves wait for them one after the other
-// and rely on other waves for overlap. Full tiles only; the kernel's last wave takes a
-// partial final tile the simple way. Grid: a multiple of 8 workgroups, each XCD (blockIdx % 8,
-// the observed round-robin placement -- speed only) owns a contiguous eighth of the tiles,
-// as k_probe's xcd_chunk does.
-constexpr int PIPE_NT = 256;
-__global__ __launch_bounds__(PIPE_NT) void k_probe_pipe(const uint4* __restrict__ pplans,
-                                                        const FilterPlan* __restrict__ plans,
-                                                        const uint8_t* __restrict__ pages,
-                                                        const uint64_t* __restrict__ slots,
-                                                        const uint4* __restrict__ lines,
-                                                        const void* __restrict__ in0,
-                                                        const uint64_t* __restrict__ runs,
-                                                        const uint32_t* __restrict__ wave_tab, uint64_t n,
-                                                        uint64_t* __restrict__ found, uint32_t fp_size,
-                                                        uint32_t seed, uint32_t lis, uint32_t page_size,
-                                                        uint32_t num_filters) {
-  __shared__ v4u s_k[PIPE_NT / WAVE][2][96];
-  const uint32_t wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
-  const uint64_t T = n / WAVE;  // full tiles
-  const uint32_t nxb = gridDim.x / 8, x = blockIdx.x % 8, lb = blockIdx.x / 8;
-  const uint64_t t_begin = T * x / 8, t_end = T * (x + 1) / 8;
-  const uint64_t W = (uint64_t)nxb * (PIPE_NT / WAVE), w = (uint64_t)lb * (PIPE_NT / WAVE) + wv;
-  const uint64_t nt = t_begin + w < t_end ? (t_end - t_begin - w + W - 1) / W : 0;
-  auto issue = [&](uint64_t t, uint32_t buf) {
-    const v4u* src = reinterpret_cast<const v4u*>(static_cast<const uint8_t*>(in0) + t * (WAVE * 24));
-#pragma unroll
-    for (uint32_t it = 0; it < 2; it++) {
-      const uint32_t j = lane + it * WAVE;
-      if (j < 96)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j),
-                                         (__attribute__((address_space(3))) void*)(&s_k[wv][buf][it * WAVE]), 16, 0, 2);
-    }
-  };
-  // one probe given its key words: filter, plan, line, decode (image walk if the line overflowed)
-  auto finish = [&](uint64_t i, uint32_t h) {
-    const uint32_t fid = tab_filter(wave_tab, runs, num_filters, i);
-    const uint4 pp = load_pplan(pplans, fid, num_filters);
-    const uint32_t fs = __builtin_amdgcn_readfirstlane(fid);
-    uint64_t r;
-    bool ok;
-    if (__builtin_amdgcn_ballot_w64(fid != fs) == 0) {
+  const uint32_t fs = __builtin_amdgcn_readfirstlane(fid);
+  const bool uniform = __builtin_amdgcn_ballot_w64(fid != fs) == 0;
+  if constexpr (QUAD) {
+    // Quad-cooperative line gather (full waves probing one filter -- the usual case with
+    // per-filter runs; the conditions are wave-uniform, so every lane takes part in the
+    // lane exchanges). One 64-B line per probe, but each wave instruction fetches 16 whole
+    // lines (quad g = lanes 4g..4g+3 reads one line, 16 B per lane) instead of a 16-B piece
+    // of 64 different lines: 64 line requests per wave instead of 256. Instruction k gathers
+    // the lines of probes 4g + k (their line index comes from lane 4g + k by a DPP quad
+    // broadcast) straight into LDS (LDS-DMA, lane L -> byte 16 L of the k-th KiB); lane q of
+    // the quad loads quarter (q + k) & 3, so probe p finds quarter j of its line at
+    // KiB p & 3, line slot p >> 2, 16-B slot (j - p) & 3 -- the 16 lanes of each ds_read_b128
+    // lane group then hit 16 distinct 4-bank groups (no conflicts). C2 probe 0.842 -> 0.821
+    // ms, C3 2.577 -> 2.537 ms per 256M (profiles/r04_quad_ab.json).
+    if (wf + WAVE <= n && uniform) {
       const uint4 U = make_uint4(__builtin_amdgcn_readfirstlane(pp.x), __builtin_amdgcn_readfirstlane(pp.y),
                                  __builtin_amdgcn_readfirstlane(pp.z), __builtin_amdgcn_readfirstlane(pp.w));
-      ok = probe_line(U, h, lines, fp_size, r);
-    } else {
-      ok = probe_line(pp, h, lines, fp_size, r);
+      const uint32_t vs = U.x & 0xff, rem = (U.x >> 8) & 0xff, rvs = (U.x >> 16) & 0xff, lgl = U.x >> 24;
+      if (!U.w && lgl) {
+        const uint32_t q = lane & 3;
+        const uint32_t fp = h >> (32 - fp_size);
+        const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
+        const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+        const uint32_t li = U.y + (bucket >> (lgl - 1));
+        v4u* sw;
+        if constexpr (WAVE_VAR) sw = reinterpret_cast<v4u*>(s_vk[threadIdx.x / WAVE]);
+        else sw = s_wbuf[threadIdx.x / WAVE];
+        const v4u* lv = reinterpret_cast<const v4u*>(lines);
+#define RF_QUAD_LOAD(k)                                                                                      \
+  {                                                                                                          \
+    const uint32_t lk = (uint32_t)__builtin_amdgcn_mov_dpp((int)li, (k) * 0x55, 0xf, 0xf, false);            \
+    __builtin_amdgcn_global_load_lds(                                                                        \
+        (const __attribute__((address_space(1))) void*)(lv + (uint64_t)lk * 4 + ((q + (k)) & 3)),          \
+        (__attribute__((address_space(3))) void*)(sw + (k) * WAVE), 16, 0, 0);                             \
+  }
+        RF_QUAD_LOAD(0) RF_QUAD_LOAD(1) RF_QUAD_LOAD(2) RF_QUAD_LOAD(3)
+#undef RF_QUAD_LOAD
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const v4u* mine = sw + (lane & 3) * WAVE + (lane >> 2) * 4;
+        v4u Q[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) Q[j] = mine[(j - lane) & 3];
+        uint64_t r;
+        if (!line_decode(Q, bucket & ((1u << (lgl - 1)) - 1), remainder, vs, rvs, r))
+          r = probe_walk(U, h, fs, plans, pages, slots, fp_size, lis, page_size);
+        __builtin_nontemporal_store(r, found + i0);
+        return;
+      }
     }
-    if (!ok) r = probe_walk(pp, h, fid, plans, pages, slots, fp_size, lis, page_size);
-    __builtin_nontemporal_store(r, found + i);
-  };
-  if (nt) issue(t_begin + w, 0);
-  for (uint64_t k = 0; k < nt; k++) {
-    const uint64_t t = t_begin + w + k * W;
-    const uint32_t buf = (uint32_t)(k & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k's keys have landed
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint2* k2 = reinterpret_cast<const uint2*>(s_k[wv][buf]) + 3 * lane;
-    const uint2 a = k2[0], b = k2[1], c = k2[2];
-    // every lane has its words before the next fetch may land in the other half... which no
-    // lane reads in this iteration; the half read here is refilled two iterations later
-    if (k + 1 < nt) issue(t + W, buf ^ 1u);
-    uint32_t kw[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
-    finish(t * WAVE + lane, xxh32_24(kw, seed));
-    __builtin_amdgcn_wave_barrier();  // all lanes' LDS reads of this half precede its refill
   }
-  // a partial final tile: the last wave of XCD 7's range takes it, loading keys per lane
-  if (n % WAVE && x == 7 && lb == nxb - 1 && wv == PIPE_NT / WAVE - 1) {
-    const uint64_t i = T * WAVE + lane;
-    if (i < n) finish(i, hash_key<IN_KEYS24, true>(in0, nullptr, 24, seed, i));
+  // one lane per probe: partial waves, waves across filters, filters without lines
+  if (i0 >= n) return;
+  uint64_t r;
+  bool ok;
+  if (uniform) {  // plan fields in scalar registers: the decode's masks are computed once per wave
+    const uint4 U = make_uint4(__builtin_amdgcn_readfirstlane(pp.x), __builtin_amdgcn_readfirstlane(pp.y),
+                               __builtin_amdgcn_readfirstlane(pp.z), __builtin_amdgcn_readfirstlane(pp.w));
+    ok = probe_line(U, h, lines, fp_size, r);
+  } else {
+    ok = probe_line(pp, h, lines, fp_size, r);
   }
+  if (!ok) r = probe_walk(pp, h, fid, plans, pages, slots, fp_size, lis, page_size);
+  __builtin_nontemporal_store(r, found + i0);
+}
+
+// one lookup of hash h in a resident filter given by its group descriptor (its own routing
+// config: one launch may answer filters of differently configured kvstores)
+__device__ __forceinline__ uint64_t probe_group(const ProbeGroup& G, uint32_t h) {
+  const uint32_t fp_size = G.fpl & 0xff, lis = (G.fpl >> 8) & 0xff;
+  const uint4 P = make_uint4(G.x, 0u, 0u, G.err);
+  uint64_t r = 0;
+  if (!probe_line(P, h, G.lines, fp_size, r)) {  // overflowed line / no lines: walk the image
+    const uint32_t vs = G.x & 0xff, rem = (G.x >> 8) & 0xff, rvs = (G.x >> 16) & 0xff;
+    const uint32_t fp = h >> (32 - fp_size);
+    const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
+    const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
+    r = probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, G.pages, G.slots[bucket >> lis], lis);
+  }
+  return r;
 }
 
 // ---- lookups against many resident filters in one launch ------------------------------
@@ -3165,24 +3062,14 @@ __global__ __launch_bounds__(PIPE_NT) void k_probe_pipe(const uint4* __restrict_
 // of synchronising the stream (one HIP call fewer per round trip).
 __global__ __launch_bounds__(256) void k_probe_groups(const uint32_t* __restrict__ in,
                                                       const ProbeGroup* __restrict__ groups, uint32_t ng,
-                                                      uint64_t n, uint64_t* __restrict__ found, uint32_t fp_size,
-                                                      uint32_t lis, uint32_t* __restrict__ counter,
+                                                      uint64_t n, uint64_t* __restrict__ found,
+                                                      uint32_t* __restrict__ counter,
                                                       uint32_t* __restrict__ done_flag, uint32_t seq) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) {
     const uint32_t h = in[i], g = in[n + i];
     uint64_t r = 0;
-    if (g < ng) {
-      const ProbeGroup G = groups[g];
-      const uint4 P = make_uint4(G.x, 0u, 0u, G.err);
-      if (!probe_line(P, h, G.lines, fp_size, r)) {  // overflowed line / no lines: walk the image
-        const uint32_t vs = G.x & 0xff, rem = (G.x >> 8) & 0xff, rvs = (G.x >> 16) & 0xff;
-        const uint32_t fp = h >> (32 - fp_size);
-        const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
-        const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-        r = probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, G.pages, G.slots[bucket >> lis], lis);
-      }
-    }
+    if (g < ng) r = probe_group(groups[g], h);
     found[i] = r;
   }
   if (done_flag) {
@@ -3194,7 +3081,9 @@ __global__ __launch_bounds__(256) void k_probe_groups(const uint32_t* __restrict
       __threadfence_system();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t last = gridDim.x - 1;
-      if (last == 0 || atomicAdd(counter, 1u) == last) {
+      // acq_rel at agent scope: the last workgroup's RMW acquires every earlier workgroup's
+      // released results before it publishes the flag
+      if (last == 0 || __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == last) {
         if (last) atomicExch(counter, 0u);  // ready for the slot's next launch (stream-ordered)
         __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
@@ -3211,17 +3100,7 @@ __global__ __launch_bounds__(WAVE) void k_probe_small(SmallProbe a) {
   if (lane < a.n) {
     const uint32_t h = a.h[lane], g = a.g[lane];
     uint64_t r = 0;
-    if (g < a.ng) {
-      const ProbeGroup G = a.groups[g];
-      const uint4 P = make_uint4(G.x, 0u, 0u, G.err);
-      if (!probe_line(P, h, G.lines, a.fp_size, r)) {
-        const uint32_t vs = G.x & 0xff, rem = (G.x >> 8) & 0xff, rvs = (G.x >> 16) & 0xff;
-        const uint32_t fp = h >> (32 - a.fp_size);
-        const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
-        const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-        r = probe_stream(bucket & ((1u << a.lis) - 1), remainder, vs, rvs, G.pages, G.slots[bucket >> a.lis], a.lis);
-      }
-    }
+    if (g < a.ng) r = probe_group(a.groups[g], h);
     a.found[lane] = r;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3240,11 +3119,11 @@ extern "C" int rf_launch_probe_small(void* stream, const SmallProbe* a) {
 }
 
 extern "C" int rf_launch_probe_groups(void* stream, const uint32_t* in, const ProbeGroup* groups, uint32_t ng,
-                                      uint64_t n, uint64_t* found, uint32_t fp_size, uint32_t lis,
-                                      uint32_t* counter, uint32_t* done_flag, uint32_t seq) {
+                                      uint64_t n, uint64_t* found, uint32_t* counter, uint32_t* done_flag,
+                                      uint32_t seq) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_probe_groups, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, in, groups,
-                     ng, n, found, fp_size, lis, counter, done_flag, seq);
+                     ng, n, found, counter, done_flag, seq);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
@@ -3503,58 +3382,19 @@ extern "C" int rf_launch_probe(const LaunchArgs* pa, int kind, const void* in0, 
                                uint32_t key_len, const uint32_t* filter_id, uint64_t n, uint64_t* found) {
   const LaunchArgs& a = *pa;
   if (n == 0) return 0;
-#if RF_DIAG
-  const int ppl = a.ppl ? (int)a.ppl : PROBE_PPL;
-#else
-  const int ppl = PROBE_PPL;
-#endif
   const int nt = probe_nt(kind);
-  dim3 g((uint32_t)((n + (uint64_t)nt * ppl - 1) / ((uint64_t)nt * ppl))), b(nt);
+  dim3 g((uint32_t)((n + nt - 1) / nt)), b(nt);
   REC(EV_P_START);
-  // RF_AMD_PROBE_PIPE=1: the persistent, software-pipelined variant (k_probe_pipe) for the
-  // probe-run path of 24-byte keys (bench.py's C2-C4); grid = 8 workgroups per CU
-  // (read per launch, so an A/B in one process can flip it); value > 1: workgroups per CU
-  const char* pipe_env = getenv("RF_AMD_PROBE_PIPE");
-  const int pipe = pipe_env ? atoi(pipe_env) : 0;
-  if (pipe && kind == IN_KEYS24 && a.probe_runs && a.wave_tab && ((uintptr_t)in0 & 15) == 0 && n >= WAVE) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t grid = (uint32_t)((cus * (pipe > 1 ? pipe : 7) + 7) / 8 * 8);  // 91 SGPRs: 7 per CU
-    hipLaunchKernelGGL(k_probe_pipe, dim3(grid), dim3(PIPE_NT), 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages,
-                       a.slots, a.lines, in0, a.probe_runs, a.wave_tab, n, found, a.fp_size, a.seed, a.lis,
-                       a.page_size, a.num_filters);
-    CHECK_LAUNCH();
-    REC(EV_P_END);
-    return 0;
-  }
-#define PK(K, L, PP) hipLaunchKernelGGL((k_probe<K, L, PP>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, a.wave_tab, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters, a.ablate)
-#if RF_DIAG
-  if (kind == IN_KEYS24 && (a.occ || a.ppl)) {  // experiment variants: waves/SIMD cap, probes per lane
-    const int o = a.occ ? (int)a.occ : 8;
-    if (ppl == 2) {
-      if (o == 8) PK(IN_KEYS24, 0, 2); else if (o == 6) PK(IN_KEYS24, 24 * 1024, 2); else PK(IN_KEYS24, 30 * 1024, 2);
-    } else if (ppl == 3) {
-      PK(IN_KEYS24, 0, 3);
-    } else {
-      if (o == 8) PK(IN_KEYS24, 0, 1); else if (o == 6) PK(IN_KEYS24, 24 * 1024, 1); else if (o == 5) PK(IN_KEYS24, 30 * 1024, 1);
-      else if (o == 4) PK(IN_KEYS24, 38 * 1024, 1); else if (o == 3) PK(IN_KEYS24, 50 * 1024, 1);
-      else PK(IN_KEYS24, 70 * 1024, 1);
-    }
-  } else
-#endif
-  {
-    // production: no LDS pad (8 waves/SIMD). The line probe is bound by outstanding random
-    // line fetches (latency x concurrency): 8 waves 1.14 ms, 6 waves 1.20, 5 1.27, 4 1.41
-    // at C2 (tools/line_sigma.py). The record-era probe preferred 6 (L2 thrash).
-    switch (kind) {
-      case IN_KEYS24: PK(IN_KEYS24, PROBE_LDS_PAD, PROBE_PPL); break;
-      case IN_KEYS_W: PK(IN_KEYS_W, PROBE_LDS_PAD, PROBE_PPL); break;
-      case IN_KEYS_B: PK(IN_KEYS_B, PROBE_LDS_PAD, PROBE_PPL); break;
-      case IN_VAR: PK(IN_VAR, PROBE_LDS_PAD, PROBE_PPL); break;
-      case IN_PAIR: PK(IN_PAIR, PROBE_LDS_PAD, PROBE_PPL); break;
-      default: PK(IN_HASH, PROBE_LDS_PAD, PROBE_PPL); break;
-    }
+#define PK(K) hipLaunchKernelGGL((k_probe<K>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.plans, a.pages, a.slots, a.lines, in0, offs, key_len, filter_id, a.probe_runs, a.wave_tab, n, found, a.fp_size, a.seed, a.lis, a.page_size, a.num_filters)
+  // 8 waves/SIMD: the line probe is bound by outstanding random line fetches (latency x
+  // concurrency): 8 waves 1.14 ms, 6 waves 1.20, 5 1.27, 4 1.41 at C2 (round-1 occupancy sweep)
+  switch (kind) {
+    case IN_KEYS24: PK(IN_KEYS24); break;
+    case IN_KEYS_W: PK(IN_KEYS_W); break;
+    case IN_KEYS_B: PK(IN_KEYS_B); break;
+    case IN_VAR: PK(IN_VAR); break;
+    case IN_PAIR: PK(IN_PAIR); break;
+    default: PK(IN_HASH); break;
   }
 #undef PK
   CHECK_LAUNCH();

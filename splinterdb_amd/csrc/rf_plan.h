@@ -90,6 +90,8 @@ struct EstFilter {
 struct ProbeGroup {
   uint32_t x;             // vs | rem << 8 | rvs << 16 | lg_line << 24 (the filter's pplans[f].x)
   uint32_t err;           // nonzero: the filter's build failed, nothing is found
+  uint32_t fpl;           // fingerprint_size | log_index_size << 8 (its batch's routing config)
+  uint32_t pad;
   const uint4* lines;     // the filter's first probe line (lg_line != 0)
   const uint8_t* pages;   // the filter's data pages
   const uint64_t* slots;  // the filter's (relocatable) index slots
@@ -98,7 +100,7 @@ struct ProbeGroup {
 // a lookup call small enough to travel in the kernel arguments (k_probe_small)
 constexpr uint32_t SMALL_PROBES = 64, SMALL_GROUPS = 8;
 struct SmallProbe {
-  uint32_t n, ng, fp_size, lis, seq;
+  uint32_t n, ng, seq;
   uint32_t h[SMALL_PROBES];
   uint8_t g[SMALL_PROBES];
   ProbeGroup groups[SMALL_GROUPS];
@@ -167,9 +169,6 @@ struct LaunchArgs {
   uint32_t num_page_slots;
   uint8_t* pages;
   FilterOut* outs;
-  uint32_t ablate;  // probe diagnostics (0 = normal)
-  uint32_t occ;     // probe occupancy experiment (0 = normal)
-  uint32_t ppl;     // probe probes-per-lane experiment (0 = production)
   const uint64_t* probe_runs;  // probes grouped by filter: runs[f] <= i < runs[f+1] (nullptr: per-probe ids)
   const uint32_t* wave_tab;    // with probe_runs: per 64-probe wave, filter << 7 | leading probes in it
   void** events;  // optional hipEvent_t[NUM_EVENTS] for per-stage timing (nullptr = off)

@@ -34,8 +34,9 @@ EXPORTED = [
     "rf_amd_batch_probe_var_keys", "rf_amd_batch_probe_hashes", "rf_amd_batch_info",
     "rf_amd_batch_probe_keys_runs", "rf_amd_batch_probe_hashes_runs",
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
-    "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_batch_timings_back", "rf_amd_debug_probe_ablate",
-    "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer",
+    "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_batch_timings_back", 
+    "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer", "rf_amd_diag_lookup_stats",
+    "rf_amd_build_id",
     "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",
     "rf_amd_image_free",
     "rf_amd_max_fingerprints", "rf_amd_estimate_unique_keys_from_count",
@@ -83,6 +84,21 @@ class RfImage(ctypes.Structure):
 _lib = None
 
 
+def check_build_id(L, path):
+    """a library built from other sources than the tree's (a stale prebuilt .so, e.g. the
+    diagnostics build left behind by an earlier round) fails loudly instead of running"""
+    from . import build as _b
+    L.rf_amd_build_id.restype = ctypes.c_char_p
+    got = L.rf_amd_build_id().decode()
+    try:
+        want = _b.source_id()
+    except OSError:  # sources absent: nothing to compare with
+        return
+    if got != want:
+        raise RuntimeError(f"{path} was built from other sources (build id {got}, tree {want}): "
+                           "rebuild it (python -c 'import __graft_entry__ as g; g.build()')")
+
+
 def load_library(build_if_missing=True):
     """Load librf_amd.so (building it in-tree with hipcc if absent)."""
     global _lib
@@ -95,6 +111,7 @@ def load_library(build_if_missing=True):
         from . import build as _b
         _b.build()
     L = ctypes.CDLL(path)
+    check_build_id(L, path)
     vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     L.rf_amd_last_error.restype = ctypes.c_char_p
     L.rf_amd_engine_create.argtypes = [i32, ctypes.POINTER(vp)]
@@ -119,10 +136,10 @@ def load_library(build_if_missing=True):
     L.rf_amd_batch_set_timing.argtypes = [vp, i32]
     L.rf_amd_batch_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), u32]
     L.rf_amd_batch_timings_back.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_float), u32]
-    L.rf_amd_debug_probe_ablate.argtypes = [u32]
     L.rf_amd_debug_read_lines.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
     L.rf_amd_debug_rebuild_lines.argtypes = [vp]
     L.rf_amd_debug_phase_buffer.argtypes = [vp, u32]
+    L.rf_amd_diag_lookup_stats.argtypes = [vp, ctypes.c_int]
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
     L.rf_amd_filter_add.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),

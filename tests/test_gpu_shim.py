@@ -245,6 +245,54 @@ def test_one_launch_per_flush_over_512_filters(pair):
     assert (got == want).all()
 
 
+def test_async_states_of_two_routing_configs_in_one_flush():
+    """Two kvstores with different filter_hash_size / filter_log_index_size
+    (splinterdb.c:147-152) share the drop-in: async states of both are queued together and
+    answered by ONE flush (one GPU launch, each filter probed with its own routing config);
+    every result equals the reference's (the launch used to reject mixed configs)"""
+    cfgs = ((26, 8), (20, 6))
+    refs = [R.Stack(fingerprint_size=a, log_index_size=b, cache_mib=512, disk_mib=4096) for a, b in cfgs]
+    shims = [R.Stack(fingerprint_size=a, log_index_size=b, cache_mib=512, disk_mib=4096, path=R.SHIM_PATH)
+             for a, b in cfgs]
+    try:
+        descs_r, descs_s, owner, allkeys = [], [], [], []
+        for f, n in enumerate((40_000, 9_000, 25_000, 3)):
+            st = f % 2
+            keys = K.random_keys(n, seed=700 + f)
+            h = refs[st].hash_keys(keys)
+            descs_r.append(refs[st].add(h, value=f + 1))
+            descs_s.append(shims[st].add(h, value=f + 1))
+            owner.append(st)
+            allkeys.append(keys)
+        rng = np.random.default_rng(21)
+        P = 12_000
+        fid = rng.integers(0, len(descs_s), size=P).astype(np.uint32)
+        probe = K.random_keys(P, seed=0x2CF)
+        for i in np.nonzero(rng.random(P) < 0.6)[0]:
+            src = allkeys[fid[i]]
+            probe[i] = src[rng.integers(0, src.shape[0])]
+        want = np.zeros(P, dtype=np.uint64)
+        for f, d in enumerate(descs_r):
+            m = fid == f
+            want[m] = refs[owner[f]].lookup_keys(d, probe[m])
+        sh = shims[0]
+        assert sh.async_config(1 << 40, 60_000_000)  # the completion thread stays out of it
+        try:
+            b0, p0 = sh.async_stats()
+            got, cb = sh.lookup_keys_async_flush_multi(shims, descs_s, owner, probe, fid)
+            b1, p1 = sh.async_stats()
+        finally:
+            sh.async_config(1024, 0)
+        assert cb == P
+        assert (b1 - b0, p1 - p0) == (1, P)
+        assert (got == want).all()
+        for st in refs + shims:
+            assert st.device_writes() == 0
+    finally:
+        for st in refs + shims:
+            st.close()
+
+
 def test_concurrent_adds_and_lookups_from_8_threads(pair):
     """8 registered threads at once, each growing its own filter by 3 incremental
     routing_filter_add calls (2^17 keys each) and then looking up 4,000 keys synchronously
