@@ -144,6 +144,21 @@ int rf_amd_probe_filters_host(rf_amd_engine *e, rf_amd_batch *const *batches, co
 int rf_amd_probe_many_hashes_host(rf_amd_engine *e, rf_amd_batch *const *batches,
                                   const uint32_t *filter_index, const uint64_t *counts,
                                   uint32_t num_groups, const uint32_t *h_hashes, uint64_t *h_found);
+/* The engine's lookup server: single lookups -- routing_filter_lookup (src/routing_filter.h:
+ * 87-92) and routing_filter_lookup_async states (:130-155) -- without a kernel launch per
+ * call. A persistent wave (started on demand on a queue of its own, exiting after 1 ms
+ * without requests, RF_AMD_SERVER_IDLE_US) polls a ring of requests in pinned host memory and
+ * answers each with filter filter_index of batch b, in submission order. submit queues the
+ * lookup of `hash` and returns its ticket; the batch must stay alive until the result is
+ * taken. A NULL tag: the caller takes the result with rf_amd_lookup_wait (blocking). A
+ * non-NULL tag: the result is delivered by rf_amd_lookup_reap, which returns up to max
+ * answered tagged lookups in ticket order (tags[i], found_values[i]) without blocking (0 if
+ * none is ready or another thread is reaping). Thread-safe. */
+#define RF_AMD_SERVER_RING 4096 /* requests in flight at most (a submit beyond waits for a slot) */
+int rf_amd_lookup_submit(rf_amd_engine *e, rf_amd_batch *b, uint32_t filter_index, uint32_t hash,
+                         void *tag, uint64_t *ticket);
+int rf_amd_lookup_wait(rf_amd_engine *e, uint64_t ticket, uint64_t *found_values);
+uint64_t rf_amd_lookup_reap(rf_amd_engine *e, void **tags, uint64_t *found_values, uint64_t max);
 /* device-allocation pool of the engine (batch work buffers are recycled across batches; up
  * to RF_AMD_POOL_MIB MiB stay pooled, by default a quarter of the device memory free at
  * engine creation and at most 16 GiB); trim hands pooled blocks back to the device until at

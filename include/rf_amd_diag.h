@@ -34,6 +34,10 @@ int rf_amd_debug_phase_buffer(void *d_buf, uint32_t kernel);
  * the counters after reading them. */
 int rf_amd_diag_lookup_stats(uint64_t *out, int reset);
 
+/* the lookup server so far: out[0] tickets issued, out[1] server launches, out[2] the first
+ * ticket the last exited server did not serve */
+int rf_amd_lookup_server_stats(rf_amd_engine *e, uint64_t *out);
+
 /* the source id the library was built from (16 hex digits of SHA-256 over the engine's
  * sources and headers, splinterdb_amd/build.py source_id): the Python loader refuses a
  * library whose id differs from the tree's (a stale prebuilt .so) */

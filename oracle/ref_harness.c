@@ -245,6 +245,41 @@ io_read_bootstrap(const char *filename, void *buf, uint64 bytes, uint64 addr)
    return STATUS_NOTSUP; /* only used to mount an existing disk, never here */
 }
 
+/* the in-memory device as a standalone io handle: platform_io.c's io_handle_create /
+ * io_handle_destroy for the kvstore harness (ref_kvs.c), sized by g_rfr_kvs_disk_bytes */
+uint64 g_rfr_kvs_disk_bytes = 16ull << 30;
+
+io_handle *
+rfr_mem_io_create(io_config *cfg, uint64 bytes)
+{
+   mem_io *io = calloc(1, sizeof(*io));
+   if (!io) {
+      return NULL;
+   }
+   io->super.ops = &mem_io_ops;
+   pthread_mutex_init(&io->lock, NULL);
+   io->cfg  = cfg;
+   io->size = bytes;
+   io->disk = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+   if (io->disk == MAP_FAILED) {
+      free(io);
+      return NULL;
+   }
+   return &io->super;
+}
+
+void
+rfr_mem_io_destroy(io_handle *ioh)
+{
+   mem_io *io = (mem_io *)ioh;
+   if (!io) {
+      return;
+   }
+   mem_cleanup(ioh, 0);
+   munmap(io->disk, io->size);
+   free(io);
+}
+
 /* ---- one reference filter stack: heap, device, allocator, clockcache, configs --------- */
 typedef struct rfr_stack {
    platform_heap_id  hid;
@@ -584,8 +619,7 @@ __attribute__((weak)) void
 routing_filter_amd_add_stats(uint64 *batches, uint64 *filters);
 __attribute__((weak)) void
 routing_filter_amd_registry_stats(uint64 *bytes, uint64 *evictions, uint64 *trims);
-__attribute__((weak)) void
-routing_filter_amd_async_config(uint64 batch, uint64 window_us);
+
 __attribute__((weak)) void
 routing_filter_amd_flush(void);
 __attribute__((weak)) void
@@ -635,16 +669,6 @@ rfr_shim_stats(uint64 *out)
    routing_filter_amd_add_stats(&out[0], &out[1]);
    routing_filter_amd_registry_stats(&out[2], &out[3], &out[4]);
    out[5] = routing_filter_amd_async_probe_ns();
-   return 1;
-}
-
-int
-rfr_async_config(uint64 batch, uint64 window_us)
-{
-   if (!routing_filter_amd_async_config) {
-      return 0;
-   }
-   routing_filter_amd_async_config(batch, window_us);
    return 1;
 }
 

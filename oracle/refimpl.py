@@ -108,8 +108,6 @@ def lib(path=LIB_PATH):
         L.rfr_shim_stats.restype = i32
         L.rfr_registry_set_limit.argtypes = [u64]
         L.rfr_registry_set_limit.restype = i32
-        L.rfr_async_config.argtypes = [u64, u64]
-        L.rfr_async_config.restype = i32
         L.rfr_lookup_keys_async_flush.argtypes = [vp, vp, vp, vp, u32, u64, vp]
         L.rfr_lookup_keys_async_flush.restype = u64
         L.rfr_lookup_keys_async_flush_multi.argtypes = [vp, vp, vp, vp, vp, u32, u64, vp]
@@ -415,13 +413,13 @@ class Stack:
                         (int(x) for x in out)))
 
     def async_breakdown(self):
-        """the shim's async completion path so far: batches, states, ns in the burst wait /
-        batch gathering / lookup_many / callbacks, and the engine's lookup round trips (calls,
-        prep / launch / wait ns); None for the reference's library"""
+        """the shim's async path so far: reaps that completed states, states, ns submitting
+        (hash, pin, ring) / reaping / in callbacks, and the engine's launch-based lookup round
+        trips (calls, prep / launch / wait ns); None for the reference's library"""
         out = np.zeros(10, dtype=np.uint64)
         if not self.L.rfr_async_breakdown(_p(out)):
             return None
-        keys = ("batches", "states", "burst_ns", "gather_ns", "lookup_ns", "callback_ns",
+        keys = ("batches", "states", "submit_ns", "unused_ns", "reap_ns", "callback_ns",
                 "rt_calls", "rt_prep_ns", "rt_launch_ns", "rt_wait_ns")
         return dict(zip(keys, (int(x) for x in out)))
 
@@ -433,9 +431,6 @@ class Stack:
 
     def registry_set_limit(self, mib):
         return bool(self.L.rfr_registry_set_limit(mib))
-
-    def async_config(self, batch, window_us):
-        return bool(self.L.rfr_async_config(batch, window_us))
 
     def filter_test_basic(self, num_fingerprints, num_values, key_size=24):
         """the reference's test_filter_basic (tests/functional/filter_test.c:22-148) on this

@@ -54,19 +54,19 @@
  * never released under it. dec_ref drops the device copy when the reference's refcount
  * reaches zero.
  *
- * async. routing_filter_lookup_async's first call on a state hashes the key, queues the
- * state and returns ASYNC_STATUS_RUNNING without touching the state again (async.h:115-125:
- * it may be completed on another thread at once). A completion thread (two by default) probes
- * the queued states -- ONE GPU launch for every filter they name -- as soon as it is free:
- * whatever arrived during the previous GPU round trip, batches size themselves
- * (RF_SHIM_ASYNC_WINDOW_US, default 0, adds a wait for up to RF_SHIM_ASYNC_BATCH states,
- * default 1024) -- so every state
- * completes without being called again. Completion stores found_values and
- * the result, marks the state done, then calls its callback(callback_arg) -- from the
- * completion thread, registered with the platform like any SplinterDB thread -- and the
- * state's next call returns ASYNC_STATUS_DONE. A state called again while still queued (a
- * polling owner) probes the queue in its own thread and returns ASYNC_STATUS_RUNNING: a call
- * never both fires its state's callback and returns DONE.
+ * Lookups. routing_filter_lookup and routing_filter_lookup_async go to the engine's lookup
+ * server (rf_amd_lookup_submit): a ring of requests in pinned host memory that a persistent
+ * GPU wave polls, so a single lookup costs no kernel launch and needs no batching.
+ * routing_filter_lookup waits for its answer. routing_filter_lookup_async's first call on a
+ * state hashes the key, submits it and returns ASYNC_STATUS_RUNNING without touching the
+ * state again (async.h:115-125: it may be completed on another thread at once). A completion
+ * thread reaps the answers in submission order, stores found_values and the result, marks
+ * the state done, then calls its callback(callback_arg) -- from that thread, registered with
+ * the platform like any SplinterDB thread -- and the state's next call returns
+ * ASYNC_STATUS_DONE. A state called again while still running (a polling owner) reaps in its
+ * own thread and returns ASYNC_STATUS_RUNNING: a call never both fires its state's callback
+ * and returns DONE. routing_filter_amd_lookup_batch (many keys at once) stays one launch over
+ * every filter they name.
  */
 #include "routing_filter.h"
 #include "mini_allocator.h"
@@ -79,7 +79,6 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <sys/prctl.h>
 #include <time.h>
 
 #include "rf_amd.h"
@@ -903,7 +902,13 @@ routing_filter_lookup(cache                *cc,
    if (!SUCCESS(rc)) {
       return rc;
    }
-   rc = status_of(rf_amd_probe_filters_host(engine(), &sb->b, &f, 1, &h, NULL, 1, found_values));
+   /* one request to the engine's lookup server: no kernel launch (a launch round trip is
+      ~6.5 us, the server's ~3.8 us, profiles/r04_pingpong.txt) */
+   uint64 ticket;
+   rc = status_of(rf_amd_lookup_submit(engine(), sb->b, f, h, NULL, &ticket));
+   if (SUCCESS(rc)) {
+      rc = status_of(rf_amd_lookup_wait(engine(), ticket, found_values));
+   }
    registry_unpin(sb);
    return rc;
 }
@@ -1024,104 +1029,66 @@ lookup_many(cache *const          *ccs,
    free(grc);
 }
 
-/* ---- async: queued states, completed by a completion thread ------------------------------ */
+/* ---- async: states answered by the engine's lookup server ---------------------------------- */
 /*
- * Queued states form a lock-free stack (one compare-and-swap per enqueue, the link kept in
- * the state's index_page local, which the shim's coroutine never uses otherwise). A
- * completion thread takes the whole stack at once and answers it with one launch: batches
- * size themselves -- what arrives during one GPU round trip goes out in the next. There are
- * RF_SHIM_ASYNC_THREADS of them (default 2), each on its own lookup slot, so a batch that
- * arrives while another is on the GPU does not wait for it (callers that re-submit from
- * callbacks keep two launches in flight). After a batch a thread spins briefly for more
- * before sleeping on a condition variable; an enqueue onto an empty stack wakes one. RF_SHIM_ASYNC_WINDOW_US (default 0) makes it wait that long after
- * the first arrival for up to RF_SHIM_ASYNC_BATCH states (default 1024) before taking them.
+ * routing_filter_lookup_async hashes the key, pins the filter's device batch and submits ONE
+ * request to the engine's lookup server (rf_amd_lookup_submit: a ring in pinned host memory
+ * that a persistent GPU wave polls -- no kernel launch, no batching delay), then returns
+ * ASYNC_STATUS_RUNNING without touching the state again (async.h:115-125). A completion
+ * thread registered with the platform reaps answered requests in submission order
+ * (rf_amd_lookup_reap) and, for each state, stores the result, marks it done and fires its
+ * callback; the next call returns DONE. A polling owner's re-call reaps in its own thread.
+ * The state's pin (its batch stays resident until answered) is kept in its filter_page
+ * local, which the shim's coroutine never uses otherwise.
  */
 static char g_queued_marker;
 #define ASYNC_STATE_QUEUED ((async_state)&g_queued_marker)
 typedef routing_filter_lookup_async_state rf_state;
 
-static rf_state      *g_aq_head;     /* the stack of queued states (atomic) */
-static uint64         g_aq_count;    /* states on it (atomic) */
-static int            g_aq_sleeping; /* completion threads waiting on g_aq_cv (atomic) */
+static uint64          g_aq_outstanding; /* submitted, not yet completed (atomic) */
+static int             g_aq_sleeping;    /* the completion thread waits on g_aq_cv (atomic) */
 static pthread_mutex_t g_aq_mu = PTHREAD_MUTEX_INITIALIZER;
-static pthread_cond_t  g_aq_cv;
+static pthread_cond_t  g_aq_cv = PTHREAD_COND_INITIALIZER;
 static pthread_once_t  g_aq_once = PTHREAD_ONCE_INIT;
-static uint64          g_async_batches, g_async_probes, g_async_probe_ns;
-/* per-phase totals of the completion path (routing_filter_amd_async_breakdown): ns spent
- * waiting for a burst to settle, gathering a batch (before lookup_many), in lookup_many (its
- * host work plus the GPU round trip), firing callbacks */
-static uint64          g_async_burst_ns, g_async_gather_ns, g_async_cb_ns;
-static uint64          g_async_limit, g_async_window_ns, g_async_threads;
+/* reaps that returned states, states completed, and ns spent submitting (hash, pin, ring),
+ * reaping and firing callbacks (routing_filter_amd_async_breakdown) */
+static uint64          g_async_batches, g_async_probes, g_async_submit_ns, g_async_reap_ns, g_async_cb_ns;
 
-#define AQ_NEXT(st) (*(rf_state **)&(st)->index_page)
+#define AQ_PIN(st) (*(shim_batch **)&(st)->filter_page)
 
-/* probe and complete the n states of a taken stack (their filters in one launch); each
- * state's callback fires after it is marked done */
-static void
-complete_states(rf_state *list, uint64 n)
+/* take what the server has answered and complete those states; returns how many */
+static uint64
+async_reap_complete(void)
 {
-   if (n == 0) {
-      return;
-   }
-   const uint64          tg   = now_ns();
-   rf_state             **q    = malloc(sizeof(*q) * n);
-   cache               **ccs   = malloc(sizeof(*ccs) * n);
-   const routing_config **cfgs = malloc(sizeof(*cfgs) * n);
-   const routing_filter **fl   = malloc(sizeof(*fl) * n);
-   uint32               *h     = malloc(sizeof(uint32) * n);
-   uint64               *found = malloc(sizeof(uint64) * n);
-   platform_status      *rc    = malloc(sizeof(*rc) * n);
-   platform_assert(q && ccs && cfgs && fl && h && found && rc);
-   uint64 m = 0;
-   for (rf_state *st = list; st && m < n; st = AQ_NEXT(st)) {
-      q[m]   = st;
-      ccs[m] = st->cc;
-      cfgs[m] = st->cfg;
-      fl[m]  = &st->filter;
-      h[m]   = st->fp; /* the full 32-bit hash, stored when queued */
-      m++;
-   }
+   enum { REAP = 256 };
+   void  *tags[REAP];
+   uint64 found[REAP];
    const uint64 t0 = now_ns();
-   lookup_many(ccs, cfgs, fl, h, m, found, rc);
+   uint64       n  = rf_amd_lookup_reap(engine(), tags, found, REAP);
+   if (n == 0) {
+      return 0;
+   }
    const uint64 t1 = now_ns();
-   __atomic_fetch_add(&g_async_gather_ns, t0 - tg, __ATOMIC_RELAXED);
-   __atomic_fetch_add(&g_async_probe_ns, t1 - t0, __ATOMIC_RELAXED);
-   for (uint64 i = 0; i < m; i++) {
-      rf_state         *st  = q[i];
+   for (uint64 i = 0; i < n; i++) {
+      rf_state         *st  = tags[i];
       async_callback_fn cb  = st->callback;
       void             *arg = st->callback_arg;
+      shim_batch       *sb  = AQ_PIN(st);
       *st->found_values     = found[i];
-      st->__async_result    = rc[i];
+      st->__async_result    = STATUS_OK;
       /* from here the owner may resume (and reuse) the state: it is not touched again */
       __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
+      registry_unpin(sb);
+      __atomic_sub_fetch(&g_aq_outstanding, 1, __ATOMIC_RELAXED);
       if (cb) {
          cb(arg);
       }
    }
+   __atomic_fetch_add(&g_async_reap_ns, t1 - t0, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_cb_ns, now_ns() - t1, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_batches, 1, __ATOMIC_RELAXED);
-   __atomic_fetch_add(&g_async_probes, m, __ATOMIC_RELAXED);
-   free(q);
-   free(ccs);
-   free(cfgs);
-   free(fl);
-   free(h);
-   free(found);
-   free(rc);
-}
-
-/* takes every queued state: the stack's head and how many states it holds */
-static rf_state *
-aq_take(uint64 *n)
-{
-   rf_state *list = __atomic_exchange_n(&g_aq_head, NULL, __ATOMIC_ACQUIRE);
-   uint64    c    = 0;
-   for (rf_state *st = list; st; st = AQ_NEXT(st)) {
-      c++;
-   }
-   __atomic_fetch_sub(&g_aq_count, c, __ATOMIC_RELAXED);
-   *n = c;
-   return list;
+   __atomic_fetch_add(&g_async_probes, n, __ATOMIC_RELAXED);
+   return n;
 }
 
 static void *
@@ -1129,55 +1096,21 @@ completion_main(void *arg)
 {
    (void)arg;
    platform_ensure_thread_registered(); /* callbacks and cache_get (imports) run here */
-   prctl(PR_SET_TIMERSLACK, 1UL, 0UL, 0UL, 0UL); /* microsecond waits, not the 50 us default slack */
    for (;;) {
-      if (!__atomic_load_n(&g_aq_head, __ATOMIC_ACQUIRE)) {
-         /* a GPU round trip is ~10-20 us: spin that long for the next arrivals, then sleep */
-         const uint64 t0 = now_ns();
-         while (!__atomic_load_n(&g_aq_head, __ATOMIC_ACQUIRE) && now_ns() - t0 < 30000) {
-            __builtin_ia32_pause();
-         }
-         pthread_mutex_lock(&g_aq_mu);
-         __atomic_add_fetch(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
-         while (!__atomic_load_n(&g_aq_head, __ATOMIC_SEQ_CST)) {
-            pthread_cond_wait(&g_aq_cv, &g_aq_mu);
-         }
-         __atomic_sub_fetch(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
-         pthread_mutex_unlock(&g_aq_mu);
+      if (async_reap_complete()) {
+         continue;
       }
-      /* a burst of submissions (a caller starting its in-flight states) goes out as one launch:
-         wait until no state has arrived for a microsecond, at most 4 */
-      {
-         uint64 c0 = __atomic_load_n(&g_aq_count, __ATOMIC_RELAXED);
-         const uint64 t0 = now_ns();
-         uint64       tc = t0, t = t0;
-         while (t - t0 < 4000 && t - tc < 1000) {
-            __builtin_ia32_pause();
-            t = now_ns();
-            const uint64 c1 = __atomic_load_n(&g_aq_count, __ATOMIC_RELAXED);
-            if (c1 != c0) {
-               c0 = c1;
-               tc = t;
-            }
-         }
-         __atomic_fetch_add(&g_async_burst_ns, t - t0, __ATOMIC_RELAXED);
+      if (__atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE)) {
+         __builtin_ia32_pause(); /* answers arrive within microseconds */
+         continue;
       }
-      const uint64 window = __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED);
-      if (window) { /* optional coalescing window after the first arrival */
-         const uint64 deadline = now_ns() + window;
-         pthread_mutex_lock(&g_aq_mu);
-         while (__atomic_load_n(&g_aq_count, __ATOMIC_RELAXED) < __atomic_load_n(&g_async_limit, __ATOMIC_RELAXED)
-                && __atomic_load_n(&g_aq_head, __ATOMIC_ACQUIRE) && now_ns() < deadline
-                && __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED) == window)
-         {
-            struct timespec ts = {.tv_sec = deadline / 1000000000ull, .tv_nsec = deadline % 1000000000ull};
-            pthread_cond_timedwait(&g_aq_cv, &g_aq_mu, &ts);
-         }
-         pthread_mutex_unlock(&g_aq_mu);
+      pthread_mutex_lock(&g_aq_mu);
+      __atomic_store_n(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
+      while (!__atomic_load_n(&g_aq_outstanding, __ATOMIC_SEQ_CST)) {
+         pthread_cond_wait(&g_aq_cv, &g_aq_mu);
       }
-      uint64    n;
-      rf_state *list = aq_take(&n);
-      complete_states(list, n);
+      __atomic_store_n(&g_aq_sleeping, 0, __ATOMIC_SEQ_CST);
+      pthread_mutex_unlock(&g_aq_mu);
    }
    return NULL;
 }
@@ -1185,57 +1118,25 @@ completion_main(void *arg)
 static void
 aq_init(void)
 {
-   g_async_limit     = env_u64("RF_SHIM_ASYNC_BATCH", 1024);
-   g_async_window_ns = env_u64("RF_SHIM_ASYNC_WINDOW_US", 0) * 1000;
-   g_async_threads   = env_u64("RF_SHIM_ASYNC_THREADS", 2);
-   if (g_async_threads == 0 || g_async_threads > 16) {
-      g_async_threads = 2;
-   }
-   if (g_async_limit == 0) {
-      g_async_limit = 1;
-   }
-   pthread_condattr_t ca;
-   pthread_condattr_init(&ca);
-   pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
-   pthread_cond_init(&g_aq_cv, &ca);
-   pthread_condattr_destroy(&ca);
    pthread_attr_t at;
    pthread_attr_init(&at);
    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
-   for (uint64 k = 0; k < g_async_threads; k++) {
-      pthread_t t;
-      platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
-   }
+   pthread_t t;
+   platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
    pthread_attr_destroy(&at);
 }
 
-static void
-aq_wake(void)
-{
-   pthread_mutex_lock(&g_aq_mu);
-   pthread_cond_signal(&g_aq_cv);
-   pthread_mutex_unlock(&g_aq_mu);
-}
-
-/* probe every state queued so far, in the caller's thread */
+/* complete every state submitted so far, in the caller's thread (reaping with the
+   completion thread) */
 void
 routing_filter_amd_flush(void)
 {
    pthread_once(&g_aq_once, aq_init);
-   uint64    n;
-   rf_state *list = aq_take(&n);
-   complete_states(list, n);
-}
-
-void
-routing_filter_amd_async_config(uint64 batch, uint64 window_us)
-{
-   pthread_once(&g_aq_once, aq_init);
-   __atomic_store_n(&g_async_limit, batch ? batch : 1, __ATOMIC_RELAXED);
-   __atomic_store_n(&g_async_window_ns, window_us * 1000, __ATOMIC_RELAXED);
-   pthread_mutex_lock(&g_aq_mu); /* waiting completion threads re-read them */
-   pthread_cond_broadcast(&g_aq_cv);
-   pthread_mutex_unlock(&g_aq_mu);
+   while (__atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE)) {
+      if (!async_reap_complete()) {
+         __builtin_ia32_pause();
+      }
+   }
 }
 
 void
@@ -1245,23 +1146,23 @@ routing_filter_amd_async_stats(uint64 *batches, uint64 *probes)
    *probes  = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED);
 }
 
-/* out[0..5]: batches, states, then ns totals of the completion path's phases: burst wait,
- * batch gathering, lookup_many (host work + GPU round trip), callbacks */
+/* out[0..5]: reaps that completed states, states completed, then ns totals: submitting
+ * (hash, pin, ring write), -, reaping, callbacks */
 void
 routing_filter_amd_async_breakdown(uint64 *out)
 {
    out[0] = __atomic_load_n(&g_async_batches, __ATOMIC_RELAXED);
    out[1] = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED);
-   out[2] = __atomic_load_n(&g_async_burst_ns, __ATOMIC_RELAXED);
-   out[3] = __atomic_load_n(&g_async_gather_ns, __ATOMIC_RELAXED);
-   out[4] = __atomic_load_n(&g_async_probe_ns, __ATOMIC_RELAXED);
+   out[2] = __atomic_load_n(&g_async_submit_ns, __ATOMIC_RELAXED);
+   out[3] = 0;
+   out[4] = __atomic_load_n(&g_async_reap_ns, __ATOMIC_RELAXED);
    out[5] = __atomic_load_n(&g_async_cb_ns, __ATOMIC_RELAXED);
 }
 
 uint64
 routing_filter_amd_async_probe_ns(void)
 {
-   return __atomic_load_n(&g_async_probe_ns, __ATOMIC_RELAXED);
+   return __atomic_load_n(&g_async_reap_ns, __ATOMIC_RELAXED);
 }
 
 async_status
@@ -1272,12 +1173,10 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
       return ASYNC_STATUS_DONE;
    }
    if (at == ASYNC_STATE_QUEUED) {
-      /* a polling owner: probe what is queued now, in this thread (this state among them,
-         unless the completion thread already holds it). RUNNING either way -- the state's
-         callback may have fired; the next call returns DONE */
-      if (__atomic_load_n(&g_aq_head, __ATOMIC_RELAXED)) {
-         routing_filter_amd_flush();
-      }
+      /* a polling owner: reap in this thread (this state among them, unless the completion
+         thread already holds it). RUNNING either way -- the state's callback may have
+         fired; the next call returns DONE */
+      async_reap_complete();
       return ASYNC_STATUS_RUNNING;
    }
    /* ASYNC_STATE_INIT (:898-905) */
@@ -1288,18 +1187,43 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
       return ASYNC_STATUS_DONE;
    }
    pthread_once(&g_aq_once, aq_init);
-   state->fp                     = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
+   const uint64 t0 = now_ns();
+   state->fp       = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
+   shim_batch     *sb;
+   uint32          fi;
+   platform_status rc = resident_pin(state->cc, state->cfg, &state->filter, &sb, &fi);
+   if (!SUCCESS(rc)) {
+      *state->found_values          = 0;
+      state->__async_result         = rc;
+      state->__async_state_stack[0] = ASYNC_STATE_DONE;
+      return ASYNC_STATUS_DONE;
+   }
+   /* a nearly full ring: reap here first (a callback that submits from the completion thread
+      must not wait for a slot only that thread would free) */
+   while (__atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE) >= RF_AMD_SERVER_RING - 64) {
+      if (!async_reap_complete()) {
+         __builtin_ia32_pause();
+      }
+   }
+   AQ_PIN(state)                 = sb;
    state->__async_state_stack[0] = ASYNC_STATE_QUEUED;
-   rf_state *old = __atomic_load_n(&g_aq_head, __ATOMIC_RELAXED);
-   do {
-      AQ_NEXT(state) = old;
-   } while (!__atomic_compare_exchange_n(&g_aq_head, &old, state, 1, __ATOMIC_SEQ_CST, __ATOMIC_RELAXED));
+   __atomic_add_fetch(&g_aq_outstanding, 1, __ATOMIC_SEQ_CST);
+   uint64 ticket;
+   int    r = rf_amd_lookup_submit(engine(), sb->b, fi, state->fp, state, &ticket);
+   if (r) { /* not queued: nobody else saw the state */
+      __atomic_sub_fetch(&g_aq_outstanding, 1, __ATOMIC_SEQ_CST);
+      registry_unpin(sb);
+      *state->found_values          = 0;
+      state->__async_result         = status_of(r);
+      state->__async_state_stack[0] = ASYNC_STATE_DONE;
+      return ASYNC_STATUS_DONE;
+   }
    /* the state may already be complete (another thread): it is not read again here */
-   const uint64 c = __atomic_add_fetch(&g_aq_count, 1, __ATOMIC_RELAXED);
-   if ((old == NULL && __atomic_load_n(&g_aq_sleeping, __ATOMIC_SEQ_CST))
-       || (c == __atomic_load_n(&g_async_limit, __ATOMIC_RELAXED) && __atomic_load_n(&g_async_window_ns, __ATOMIC_RELAXED)))
-   {
-      aq_wake();
+   __atomic_fetch_add(&g_async_submit_ns, now_ns() - t0, __ATOMIC_RELAXED);
+   if (__atomic_load_n(&g_aq_sleeping, __ATOMIC_SEQ_CST)) {
+      pthread_mutex_lock(&g_aq_mu);
+      pthread_cond_signal(&g_aq_cv);
+      pthread_mutex_unlock(&g_aq_mu);
    }
    return ASYNC_STATUS_RUNNING;
 }

@@ -7,28 +7,21 @@
 #include "platform.h"
 #include "routing_filter.h"
 
-/* probe every routing_filter_lookup_async state queued so far in the caller's thread (one
- * GPU launch over every filter they name), complete them and fire their callbacks. Queued
- * states also complete on their own: the shim's completion thread takes the whole queue
- * whenever it is free (what arrived during its previous GPU round trip), waiting up to
- * RF_SHIM_ASYNC_WINDOW_US (default 0) microseconds for RF_SHIM_ASYNC_BATCH states */
+/* complete every routing_filter_lookup_async state submitted so far in the caller's thread
+ * (their answers reaped from the engine's lookup server, callbacks fired). States also
+ * complete on their own: the shim's completion thread reaps answers as they arrive */
 void
 routing_filter_amd_flush(void);
 
-/* the completion thread's batch size and window (RF_SHIM_ASYNC_BATCH and
- * RF_SHIM_ASYNC_WINDOW_US at start-up) */
-void
-routing_filter_amd_async_config(uint64 batch, uint64 window_us);
-
-/* flushes so far (GPU launches) and states completed */
+/* reaps that completed states so far, and states completed */
 void
 routing_filter_amd_async_stats(uint64 *batches, uint64 *probes);
 
-/* nanoseconds spent so far probing queued states (grouping, residency, the GPU round trip) */
+/* nanoseconds spent so far reaping answered states */
 uint64
 routing_filter_amd_async_probe_ns(void);
-/* out[0..5]: async batches, states, ns of the burst wait, batch gathering, lookup_many and
- * callbacks (diagnostics) */
+/* out[0..5]: reaps, states, ns submitting (hash, pin, ring), -, reaping, callbacks
+ * (diagnostics) */
 void
 routing_filter_amd_async_breakdown(uint64 *out);
 

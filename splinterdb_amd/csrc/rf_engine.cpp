@@ -6,6 +6,7 @@
 // the host: there is no CPU fallback, and every entry point fails with ENODEV when no HIP
 // device is present.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <math.h>
 #include <algorithm>
 #include <stdio.h>
@@ -163,8 +164,28 @@ struct ProbeSlot {
   uint32_t seq = 0;
 };
 
+// The engine's lookup server (k_lookup_server): rings in pinned coherent host memory, the
+// persistent kernel's generation and state, and the host-side bookkeeping of tickets.
+struct LookupServer {
+  std::once_flag once;
+  int init_rc = 0;
+  SrvReq* ring = nullptr;  // pinned coherent host memory
+  SrvRes* res = nullptr;
+  SrvCtl* ctl = nullptr;
+  hipStream_t st = nullptr;             // its own HSA queue (CU-masked), so it never blocks other work
+  void* tags[SRV_RING] = {};            // per slot: the submitter's tag (NULL: a waiter's ticket)
+  std::atomic<uint64_t> consumed[SRV_RING];  // per slot: 1 + the last ticket whose result was taken
+  std::atomic<uint64_t> tail{0};        // the next ticket
+  std::atomic<uint64_t> state{0};       // generation << 1 | running
+  std::mutex reap_mu;
+  uint64_t reap_next = 0;               // the next ticket reap() looks at (under reap_mu)
+  std::atomic<uint64_t> launches{0};
+  uint64_t idle_ticks = 0, life_ticks = 0;
+};
+
 struct rf_amd_engine {
   int device;
+  LookupServer srv;
   hipStream_t stream;
   DevPool pool;
   HostStage stage;
@@ -282,9 +303,11 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
   return 0;
 }
 
+static void srv_stop(rf_amd_engine* e);
 extern "C" void rf_amd_engine_destroy(rf_amd_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  srv_stop(e);
   (void)hipDeviceSynchronize();
   (void)hipStreamDestroy(e->stream);
   for (ProbeSlot* s : e->slots_all) {
@@ -1065,6 +1088,182 @@ static int slot_wait(ProbeSlot* s, uint32_t seq, bool sync) {
       return 0;
     }
   }
+}
+
+// ---- the lookup server (host side) --------------------------------------------------------
+extern "C" int rf_launch_lookup_server(void* stream, const SrvReq* ring, SrvRes* res, SrvCtl* ctl, uint64_t head,
+                                       uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks);
+static const uint64_t SRV_UNPUBLISHED = ~0ull, SRV_BUSY = ~0ull - 1;
+static_assert(SRV_RING == RF_AMD_SERVER_RING, "rf_amd.h and the kernels agree on the ring size");
+
+static int srv_init(rf_amd_engine* e) {
+  LookupServer& v = e->srv;
+  std::call_once(v.once, [&] {
+    if (hipSetDevice(e->device) != hipSuccess ||
+        hipHostMalloc((void**)&v.ring, sizeof(SrvReq) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc((void**)&v.res, sizeof(SrvRes) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc((void**)&v.ctl, sizeof(SrvCtl), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+      v.init_rc = RF_AMD_ENOMEM;
+      return;
+    }
+    for (uint32_t s = 0; s < SRV_RING; s++) {
+      v.ring[s].ticket = SRV_UNPUBLISHED;
+      v.res[s].ticket = SRV_UNPUBLISHED;
+      v.consumed[s].store(0, std::memory_order_relaxed);
+    }
+    memset(v.ctl, 0, sizeof(SrvCtl));
+    // a CU-masked stream is a queue of its own: the persistent wave never sits in front of
+    // another stream's work (one CU is enough for one wave); without it, a plain stream
+    // and a short lifetime bound the wait of whatever shares its queue
+    uint32_t mask[8] = {1u, 0, 0, 0, 0, 0, 0, 0};
+    const bool masked = hipExtStreamCreateWithCUMask(&v.st, 8, mask) == hipSuccess;
+    if (!masked && hipStreamCreateWithFlags(&v.st, hipStreamNonBlocking) != hipSuccess) {
+      v.init_rc = RF_AMD_EINVAL;
+      return;
+    }
+    // s_memrealtime runs at 100 MHz: idle 1 ms, lifetime 1 s (2 ms without a queue of its own)
+    const char* idle = getenv("RF_AMD_SERVER_IDLE_US");
+    v.idle_ticks = (idle ? strtoull(idle, nullptr, 10) : 1000) * 100;
+    v.life_ticks = masked ? 100000000ull : 200000ull;
+  });
+  return v.init_rc ? fail(v.init_rc, "lookup server allocation failed") : 0;
+}
+
+// make sure a server wave is running (or queued): the first submit launches one; a server that
+// exited (idle, lifetime, stop) while tickets wait is relaunched from the first ticket it did
+// not serve. The generation CAS makes exactly one caller launch.
+static int srv_ensure(rf_amd_engine* e) {
+  LookupServer& v = e->srv;
+  uint64_t s = v.state.load(std::memory_order_acquire);
+  const uint64_t gen = s >> 1;
+  if (s & 1) {
+    if (__atomic_load_n(&v.ctl->exit_gen, __ATOMIC_ACQUIRE) != gen) return 0;  // running
+  }
+  const uint64_t next = ((gen + 1) << 1) | 1;
+  if (!v.state.compare_exchange_strong(s, next, std::memory_order_acq_rel)) return 0;  // another launched
+  const uint64_t head = __atomic_load_n(&v.ctl->exit_head, __ATOMIC_ACQUIRE);
+  (void)hipSetDevice(e->device);
+  if (int rc = rf_launch_lookup_server(v.st, v.ring, v.res, v.ctl, head, gen + 1, v.idle_ticks, v.life_ticks))
+    return fail(RF_AMD_EINVAL, std::string("lookup server launch: ") + hipGetErrorString((hipError_t)rc));
+  v.launches.fetch_add(1, std::memory_order_relaxed);
+  return 0;
+}
+
+static void srv_stop(rf_amd_engine* e) {
+  LookupServer& v = e->srv;
+  if (!v.ctl || !v.st) return;
+  __atomic_store_n(&v.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(v.st);
+  (void)hipStreamDestroy(v.st);
+  (void)hipHostFree(v.ring);
+  (void)hipHostFree(v.res);
+  (void)hipHostFree(v.ctl);
+  v.st = nullptr;
+  v.ctl = nullptr;
+}
+
+// the server stream's error, if its kernel faulted (checked while waiting)
+static int srv_check(rf_amd_engine* e) {
+  const hipError_t q = hipStreamQuery(e->srv.st);
+  if (q == hipSuccess || q == hipErrorNotReady) return 0;
+  return fail(RF_AMD_EINVAL, std::string("lookup server: ") + hipGetErrorString(q));
+}
+
+static ProbeGroup probe_group_of(const rf_amd_batch* b, uint32_t f);
+static int batch_errors(rf_amd_batch* b);
+
+extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t filter_index, uint32_t hash,
+                                    void* tag, uint64_t* ticket) {
+  if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "lookup on an unbuilt or foreign batch");
+  if (filter_index >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
+  if (!ticket) return fail(RF_AMD_EINVAL, "null ticket");
+  if (int rc = srv_init(e)) return rc;
+  if (int rc = batch_errors(b)) return rc;
+  LookupServer& v = e->srv;
+  const uint64_t t = v.tail.fetch_add(1, std::memory_order_acq_rel);
+  const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
+  if (t >= SRV_RING) {  // the slot's previous ticket must have been taken
+    for (uint32_t spin = 1; v.consumed[slot].load(std::memory_order_acquire) != t - SRV_RING + 1; spin++) {
+      __builtin_ia32_pause();
+      if ((spin & 1023) == 0) {
+        if (int rc = srv_ensure(e)) return rc;
+        if (int rc = srv_check(e)) return rc;
+      }
+    }
+    // the slot is being rewritten: readers that see this do not trust its payload or tag
+    __atomic_store_n(&v.ring[slot].ticket, SRV_BUSY, __ATOMIC_RELEASE);
+  }
+  SrvReq& q = v.ring[slot];
+  q.g = probe_group_of(b, filter_index);
+  q.h = hash;
+  q.pad = tag ? 0u : 1u;  // 1: a waiter's ticket (rf_amd_lookup_wait takes its result)
+  v.tags[slot] = tag;
+  __atomic_store_n(&q.ticket, t, __ATOMIC_RELEASE);
+  *ticket = t;
+  return srv_ensure(e);
+}
+
+extern "C" int rf_amd_lookup_wait(rf_amd_engine* e, uint64_t ticket, uint64_t* found_values) {
+  if (!e || !e->srv.ring) return fail(RF_AMD_EINVAL, "no lookup server");
+  LookupServer& v = e->srv;
+  const uint32_t slot = (uint32_t)(ticket & (SRV_RING - 1));
+  for (uint32_t spin = 1;; spin++) {
+    if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) == ticket) {
+      if (found_values) *found_values = __atomic_load_n(&v.res[slot].found, __ATOMIC_RELAXED);
+      v.consumed[slot].store(ticket + 1, std::memory_order_release);
+      return 0;
+    }
+    __builtin_ia32_pause();
+    if ((spin & 255) == 0) {
+      if (int rc = srv_ensure(e)) return rc;
+      if ((spin & 65535) == 0)
+        if (int rc = srv_check(e)) return rc;
+    }
+  }
+}
+
+extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* found_values, uint64_t max) {
+  if (!e || !e->srv.ring || !tags || !found_values) return 0;
+  LookupServer& v = e->srv;
+  std::unique_lock<std::mutex> lk(v.reap_mu, std::try_to_lock);
+  if (!lk.owns_lock()) return 0;  // another thread is reaping
+  uint64_t n = 0, t = v.reap_next;
+  const uint64_t tail = v.tail.load(std::memory_order_acquire);
+  while (n < max && t < tail) {
+    const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
+    const uint64_t tk = __atomic_load_n(&v.ring[slot].ticket, __ATOMIC_ACQUIRE);
+    if (tk == SRV_UNPUBLISHED || tk == SRV_BUSY || tk < t) break;  // not yet published
+    if (tk > t) {  // a waiter already took ticket t and its slot was reused
+      t++;
+      continue;
+    }
+    const uint32_t waiter = v.ring[slot].pad;
+    void* tag = v.tags[slot];
+    if (__atomic_load_n(&v.ring[slot].ticket, __ATOMIC_ACQUIRE) != t) continue;  // rewritten meanwhile: re-read
+    if (waiter) {  // its waiter takes the result
+      t++;
+      continue;
+    }
+    if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) != t) break;  // not answered yet
+    tags[n] = tag;
+    found_values[n] = __atomic_load_n(&v.res[slot].found, __ATOMIC_RELAXED);
+    v.consumed[slot].store(t + 1, std::memory_order_release);
+    n++;
+    t++;
+  }
+  v.reap_next = t;
+  lk.unlock();
+  if (n == 0 && t < tail) (void)srv_ensure(e);
+  return n;
+}
+
+extern "C" int rf_amd_lookup_server_stats(rf_amd_engine* e, uint64_t* out) {
+  if (!e || !out) return fail(RF_AMD_EINVAL, "null argument");
+  out[0] = e->srv.tail.load();
+  out[1] = e->srv.launches.load();
+  out[2] = e->srv.ctl ? __atomic_load_n(&e->srv.ctl->exit_head, __ATOMIC_ACQUIRE) : 0;
+  return 0;
 }
 
 // where a host-buffer lookup round trip spends its time (rf_amd_diag_lookup_stats): calls,

@@ -3112,6 +3112,90 @@ __global__ __launch_bounds__(WAVE) void k_probe_small(SmallProbe a) {
   }
 }
 
+// ---- the lookup server ---------------------------------------------------------------------
+// One persistent wave answers single lookups (routing_filter_lookup, routing_filter_lookup_async
+// states) that the host writes into a ring of SrvReq in pinned coherent host memory: no
+// kernel launch per call (a launch round trip is ~6.5 us on MI355X, a round trip through the
+// ring ~3.8 us, profiles/r04_pingpong.txt). Each pass reads the ticket words of the next 64
+// slots; when some are ready, a system-scope acquire orders the payload reads after them (the
+// host stores the payload before the ticket) and drops stale cached device data (batches are
+// built by other kernels into pooled memory while this one runs); the lanes of the ready prefix
+// probe their filter
+// (probe_group, as k_probe_groups does) and answer in the result ring, found first, then the
+// ticket (system-scope release). When nothing is ready, lane 0 polls the next ticket with
+// s_sleep between polls. The wave exits after `idle_ticks` without requests, after
+// `life_ticks` in total (s_memrealtime, 100 MHz) or when the host sets ctl->stop -- every
+// loop iteration checks the clock, so the kernel always ends -- and reports the first ticket
+// it did not serve; the host relaunches it from there when more requests come.
+__global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict__ ring, SrvRes* __restrict__ res,
+                                                        SrvCtl* __restrict__ ctl, uint64_t head, uint64_t gen,
+                                                        uint64_t idle_ticks, uint64_t life_ticks) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_busy = t0, served = 0;
+  for (;;) {
+    const uint32_t slot = (uint32_t)((head + lane) & (SRV_RING - 1));
+    const uint64_t tk = __hip_atomic_load(&ring[slot].ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t ready = __builtin_amdgcn_ballot_w64(tk == head + lane);
+    const uint32_t k = ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);  // the ready prefix
+    if (k) {
+      // acquire (system scope) once per served pass, not per poll: the payloads after the
+      // tickets, and no stale cached device data (it invalidates this CU's L1 and the L2)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (lane < k) {
+        const SrvReq& q = ring[slot];
+        const ProbeGroup G = q.g;
+        const uint32_t h = q.h;
+        __hip_atomic_store(&res[slot].found, probe_group(G, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      // the found words (system-coherent stores to host memory, no cached copy to write back)
+      // have completed before any ticket is stored
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < k) __hip_atomic_store(&res[slot].ticket, head + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      head += k;
+      served += k;
+      t_busy = __builtin_amdgcn_s_memrealtime();
+      continue;
+    }
+    // idle: poll the next ticket alone (one 8-byte PCIe read per poll), bounded by the clock
+    bool stop = false;
+    for (;;) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (now - t_busy > idle_ticks || now - t0 > life_ticks) {
+        stop = true;
+        break;
+      }
+      uint64_t t1 = 0, st = 0;
+      if (lane == 0) {
+        t1 = __hip_atomic_load(&ring[head & (SRV_RING - 1)].ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st = __hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      t1 = __shfl(t1, 0);
+      st = __shfl(st, 0);
+      if (st) {
+        stop = true;
+        break;
+      }
+      if (t1 == head) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (stop) break;
+  }
+  if (lane == 0) {
+    __hip_atomic_store(&ctl->exit_head, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&ctl->served, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&ctl->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+extern "C" int rf_launch_lookup_server(void* stream, const SrvReq* ring, SrvRes* res, SrvCtl* ctl, uint64_t head,
+                                       uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks) {
+  hipLaunchKernelGGL(k_lookup_server, dim3(1), dim3(WAVE), 0, (hipStream_t)stream, ring, res, ctl, head, gen,
+                     idle_ticks, life_ticks);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
 extern "C" int rf_launch_probe_small(void* stream, const SmallProbe* a) {
   hipLaunchKernelGGL(k_probe_small, dim3(1), dim3(WAVE), 0, (hipStream_t)stream, *a);
   const hipError_t e = hipGetLastError();

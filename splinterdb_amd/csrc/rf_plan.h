@@ -97,6 +97,32 @@ struct ProbeGroup {
   const uint64_t* slots;  // the filter's (relocatable) index slots
 };
 
+// The lookup server (k_lookup_server): single lookups travel through a ring of requests in
+// pinned coherent host memory that a persistent wave polls, instead of one kernel launch per
+// call. Request t sits in slot t % SRV_RING; the host writes the payload, then `ticket` = t
+// (release); the server answers in slot t of the result ring (found, then ticket = t).
+constexpr uint32_t SRV_RING = 4096;
+struct SrvReq {
+  ProbeGroup g;     // the filter (its own routing config)
+  uint32_t h;       // the key's 32-bit hash
+  uint32_t pad;
+  uint64_t pad2;
+  uint64_t ticket;  // written last
+};
+static_assert(sizeof(SrvReq) == 64, "one request per 64-byte line");
+struct SrvRes {
+  uint64_t found;
+  uint64_t ticket;  // written last
+};
+// control block (pinned coherent host memory): stop is set by the host; the server writes the
+// first ticket it did not serve, then its generation, when it exits
+struct SrvCtl {
+  uint64_t stop;
+  uint64_t exit_head;
+  uint64_t exit_gen;
+  uint64_t served;
+};
+
 // a lookup call small enough to travel in the kernel arguments (k_probe_small)
 constexpr uint32_t SMALL_PROBES = 64, SMALL_GROUPS = 8;
 struct SmallProbe {

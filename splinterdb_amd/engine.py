@@ -36,6 +36,7 @@ EXPORTED = [
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
     "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_batch_timings_back", 
     "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer", "rf_amd_diag_lookup_stats",
+    "rf_amd_lookup_submit", "rf_amd_lookup_wait", "rf_amd_lookup_reap", "rf_amd_lookup_server_stats",
     "rf_amd_build_id",
     "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",
     "rf_amd_image_free",
@@ -140,6 +141,11 @@ def load_library(build_if_missing=True):
     L.rf_amd_debug_rebuild_lines.argtypes = [vp]
     L.rf_amd_debug_phase_buffer.argtypes = [vp, u32]
     L.rf_amd_diag_lookup_stats.argtypes = [vp, ctypes.c_int]
+    L.rf_amd_lookup_submit.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64)]
+    L.rf_amd_lookup_wait.argtypes = [vp, u64, ctypes.POINTER(u64)]
+    L.rf_amd_lookup_reap.argtypes = [vp, vp, vp, u64]
+    L.rf_amd_lookup_reap.restype = u64
+    L.rf_amd_lookup_server_stats.argtypes = [vp, vp]
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
     L.rf_amd_filter_add.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),

@@ -1,0 +1,176 @@
+"""The engine's lookup server (rf_amd_lookup_submit / _wait / _reap, k_lookup_server): single
+lookups answered by a persistent wave that polls a ring in pinned host memory. Every answer
+must equal the batch probe's (k_probe) for the same filter and hash, through the waiting and
+the reaping forms, from several threads at once, across the wave's idle exit and relaunch,
+and after the batch's device memory was reused by another build while the wave kept running
+(the wave must not answer from stale cached lines)."""
+import ctypes
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from splinterdb_amd import engine as E
+from splinterdb_amd import keys as K
+
+pytestmark = pytest.mark.gpu
+
+L = None
+
+
+def lib():
+    global L
+    if L is None:
+        L = E.load_library()
+    return L
+
+
+def build(cfg, sizes, values, seed):
+    """a batch of len(sizes) filters from random hashes; returns (batch, hashes, per-probe
+    filter ids)"""
+    rng = np.random.default_rng(seed)
+    h = rng.integers(0, 1 << 32, size=sum(sizes), dtype=np.uint64).astype(np.uint32)
+    b = E.FilterBatch(cfg, sizes, values)
+    b.build_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"))
+    torch.cuda.synchronize()
+    return b, h
+
+
+def batch_probe(b, h, fid):
+    """the reference answer: the batch probe kernel over the same (filter, hash) pairs"""
+    found = torch.zeros(h.size, dtype=torch.int64, device="cuda:0")
+    b.probe_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"),
+                   torch.from_numpy(fid.astype(np.int32)).to("cuda:0"), h.size, found)
+    torch.cuda.synchronize()
+    return found.cpu().numpy().view(np.uint64)
+
+
+def submit(b, f, hash_, tag):
+    t = ctypes.c_uint64()
+    E._check(lib().rf_amd_lookup_submit(b.engine.h, b.h, int(f), int(hash_), tag, ctypes.byref(t)))
+    return t.value
+
+
+def wait(b, ticket):
+    out = ctypes.c_uint64()
+    E._check(lib().rf_amd_lookup_wait(b.engine.h, ticket, ctypes.byref(out)))
+    return out.value
+
+
+def reap_all(e, n, timeout_s=30.0):
+    """reap n tagged answers: {tag: found}"""
+    tags = (ctypes.c_void_p * 256)()
+    found = (ctypes.c_uint64 * 256)()
+    got = {}
+    t0 = time.time()
+    while len(got) < n:
+        k = lib().rf_amd_lookup_reap(e.h, ctypes.addressof(tags), ctypes.addressof(found), 256)
+        for i in range(k):
+            got[tags[i]] = found[i]
+        assert time.time() - t0 < timeout_s, f"reaped {len(got)} of {n}"
+    return got
+
+
+def probes(h, sizes, n, seed):
+    """n (filter, hash) pairs: half inserted hashes, half random"""
+    rng = np.random.default_rng(seed)
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    fid = rng.integers(0, len(sizes), size=n).astype(np.uint32)
+    ph = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    hit = rng.random(n) < 0.5
+    for i in np.nonzero(hit)[0]:
+        ph[i] = h[starts[fid[i]] + rng.integers(0, sizes[fid[i]])]
+    return fid, ph
+
+
+def test_wait_and_reap_equal_batch_probe():
+    cfg = E.routing_config_init(log_index_size=8)
+    sizes, values = [200_000, 70_000, 3], [0, 9, 31]
+    b, h = build(cfg, sizes, values, seed=1)
+    fid, ph = probes(h, sizes, 6000, seed=2)
+    want = batch_probe(b, ph, fid)
+    # waiting form, one at a time
+    got = np.array([wait(b, submit(b, fid[i], ph[i], None)) for i in range(1500)], dtype=np.uint64)
+    assert (got == want[:1500]).all()
+    # reaping form: 4,500 in flight at once (the 4,096-slot ring wraps while answers are reaped)
+    e = b.engine
+    res = {}
+    done = threading.Event()
+
+    def reaper():
+        res.update(reap_all(e, 4500))
+        done.set()
+
+    th = threading.Thread(target=reaper)
+    th.start()
+    for i in range(1500, 6000):
+        submit(b, fid[i], ph[i], i + 1)  # tag = index + 1 (never NULL)
+    th.join(60)
+    assert done.is_set()
+    got = np.array([res[i + 1] for i in range(1500, 6000)], dtype=np.uint64)
+    assert (got == want[1500:]).all()
+    b.close()
+
+
+def test_threads_idle_relaunch_and_reused_memory():
+    cfg = E.routing_config_init(log_index_size=8)
+    sizes = [100_000] * 4
+    b, h = build(cfg, sizes, [1, 2, 3, 4], seed=3)
+    fid, ph = probes(h, sizes, 8000, seed=4)
+    want = batch_probe(b, ph, fid)
+    # 8 threads waiting on their own lookups at once
+    out = np.zeros(8000, dtype=np.uint64)
+
+    def worker(t):
+        for i in range(t, 8000, 8):
+            out[i] = wait(b, submit(b, fid[i], ph[i], None))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(60)
+    assert (out == want).all()
+    # the wave exits after 1 ms without requests; the next lookup relaunches it and is answered
+    st = (ctypes.c_uint64 * 3)()
+    E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
+    launches0 = st[1]
+    time.sleep(0.05)
+    assert wait(b, submit(b, fid[0], ph[0], None)) == want[0]
+    E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
+    assert st[1] > launches0
+    # a keeper thread's lookups keep the wave busy (no idle exit) while the batch is replaced
+    # by other builds in the same (pooled) device memory: the new batches' answers must not
+    # come from lines the running wave cached before
+    bk, hk = build(cfg, [5000], [0], seed=99)
+    stop = threading.Event()
+    kept = []
+
+    def keeper():
+        while not stop.is_set():
+            kept.append(wait(bk, submit(bk, 0, hk[len(kept) % 5000], None)))
+
+    kt = threading.Thread(target=keeper)
+    kt.start()
+    try:
+        E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
+        launches1 = st[1]
+        b.close()
+        torch.cuda.synchronize()
+        for rnd in range(3):
+            b2, h2 = build(cfg, sizes, [5, 6, 7, 8], seed=10 + rnd)
+            fid2, ph2 = probes(h2, sizes, 3000, seed=20 + rnd)
+            want2 = batch_probe(b2, ph2, fid2)
+            got2 = np.array([wait(b2, submit(b2, fid2[i], ph2[i], None)) for i in range(3000)], dtype=np.uint64)
+            assert (got2 == want2).all(), rnd
+            b2.close()
+            torch.cuda.synchronize()
+        E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
+    finally:
+        stop.set()
+        kt.join(30)
+    assert st[1] == launches1  # the same wave served the rebuilt batches
+    assert len(kept) > 100 and all(v & 1 for v in kept)  # every kept hash was inserted, value 0
+    bk.close()

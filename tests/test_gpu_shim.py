@@ -90,9 +90,10 @@ def test_incremental_chain_identical_to_reference(pair):
 
 def test_lookup_async_coalesced_equals_reference(pair):
     """20,000 routing_filter_lookup_async states over three filters, each started once and
-    then polled: the shim queues them (every first call returns ASYNC_STATUS_RUNNING) and its
-    completion thread answers them in a few GPU launches; every found_values equals the
-    reference coroutine's, every callback fires once"""
+    then polled: the shim submits them to the engine's lookup server (every first call returns
+    ASYNC_STATUS_RUNNING; 20,000 states wrap its 4,096-slot ring several times) and its
+    completion thread reaps the answers; every found_values equals the reference coroutine's,
+    every callback fires once"""
     ref, shim = pair
     descs_r, descs_s, allkeys = [], [], []
     for f, n in enumerate((50_000, 200_000, 7)):
@@ -117,7 +118,7 @@ def test_lookup_async_coalesced_equals_reference(pair):
     # every state was queued (its first call returned RUNNING, never DONE) and completed by
     # a flush with its callback fired exactly once
     assert cb_s == P and run_s == P
-    assert p1 - p0 == P and 0 < b1 - b0 <= P  # one GPU launch per flush
+    assert p1 - p0 == P and 0 < b1 - b0 <= P  # reaped in batches
     assert run_r == 0  # the reference's coroutine finds every page in the cache
     # and the synchronous form agrees with both
     for f in range(3):
@@ -213,10 +214,10 @@ def test_lookup_async_callback_driven(pair, inflight):
     assert st_s == {"running": P, "callbacks": P, "done": P, "violations": 0}, st_s
 
 
-def test_one_launch_per_flush_over_512_filters(pair):
-    """8,192 async states over 512 distinct filters, answered by ONE routing_filter_amd_flush:
-    one GPU launch (the engine's multi-filter probe, k_probe_groups) covers every filter,
-    and every result equals the reference's lookups"""
+def test_async_states_over_512_filters_then_flush(pair):
+    """8,192 async states over 512 distinct filters, all submitted to the engine's lookup
+    server, then routing_filter_amd_flush(): every state is done once the flush returns, each
+    callback fired once, and every result equals the reference's lookups"""
     ref, shim = pair
     descs_r, descs_s, allkeys = [], [], []
     for f in range(512):
@@ -233,23 +234,20 @@ def test_one_launch_per_flush_over_512_filters(pair):
         src = allkeys[fid[i]]
         probe[i] = src[rng.integers(0, src.shape[0])]
     want, _ = ref.lookup_batch(descs_r, probe, fid)
-    assert shim.async_config(1 << 40, 60_000_000)  # the completion thread stays out of it
-    try:
-        b0, p0 = shim.async_stats()
-        got, cb = shim.lookup_keys_async_flush(descs_s, probe, fid)
-        b1, p1 = shim.async_stats()
-    finally:
-        shim.async_config(1024, 0)
+    b0, p0 = shim.async_stats()
+    got, cb = shim.lookup_keys_async_flush(descs_s, probe, fid)
+    b1, p1 = shim.async_stats()
     assert cb == P
-    assert (b1 - b0, p1 - p0) == (1, P)
+    assert p1 - p0 == P and 0 < b1 - b0 <= P
     assert (got == want).all()
 
 
 def test_async_states_of_two_routing_configs_in_one_flush():
     """Two kvstores with different filter_hash_size / filter_log_index_size
-    (splinterdb.c:147-152) share the drop-in: async states of both are queued together and
-    answered by ONE flush (one GPU launch, each filter probed with its own routing config);
-    every result equals the reference's (the launch used to reject mixed configs)"""
+    (splinterdb.c:147-152) share the drop-in: async states of both go to the engine's lookup
+    server together (each filter probed with its own routing config) and one flush completes
+    them; every result equals the reference's (a launch used to reject mixed
+    configs)"""
     cfgs = ((26, 8), (20, 6))
     refs = [R.Stack(fingerprint_size=a, log_index_size=b, cache_mib=512, disk_mib=4096) for a, b in cfgs]
     shims = [R.Stack(fingerprint_size=a, log_index_size=b, cache_mib=512, disk_mib=4096, path=R.SHIM_PATH)
@@ -276,15 +274,11 @@ def test_async_states_of_two_routing_configs_in_one_flush():
             m = fid == f
             want[m] = refs[owner[f]].lookup_keys(d, probe[m])
         sh = shims[0]
-        assert sh.async_config(1 << 40, 60_000_000)  # the completion thread stays out of it
-        try:
-            b0, p0 = sh.async_stats()
-            got, cb = sh.lookup_keys_async_flush_multi(shims, descs_s, owner, probe, fid)
-            b1, p1 = sh.async_stats()
-        finally:
-            sh.async_config(1024, 0)
+        b0, p0 = sh.async_stats()
+        got, cb = sh.lookup_keys_async_flush_multi(shims, descs_s, owner, probe, fid)
+        b1, p1 = sh.async_stats()
         assert cb == P
-        assert (b1 - b0, p1 - p0) == (1, P)
+        assert p1 - p0 == P and 0 < b1 - b0 <= P
         assert (got == want).all()
         for st in refs + shims:
             assert st.device_writes() == 0

@@ -50,13 +50,8 @@ for name, path in (("shim", R.SHIM_PATH), ("reference", R.LIB_PATH)):
         probe = np.stack([keys[f][rng.integers(0, n)] for f in fid])
         # one routing_filter_lookup call: 2,000 calls in a C loop (oracle/ref_harness.c
         # rfr_lookup_keys), per call -- no Python in the timed path of each call
-        lb0 = s.async_breakdown()
         r["lookup_one_ms"] = round(med(lambda: s.lookup_keys(descs[0], probe[:2000]), reps=7) / 2000, 5)
-        lb1 = s.async_breakdown()
-        if lb0:
-            c = max(lb1["rt_calls"] - lb0["rt_calls"], 1)
-            r["lookup_one_breakdown_us"] = {k: round((lb1[f"rt_{k}_ns"] - lb0[f"rt_{k}_ns"]) / c / 1e3, 2)
-                                            for k in ("prep", "launch", "wait")}
+
         r["lookup_batch_8192_ms"] = med(lambda: s.lookup_batch(descs, probe, fid))
         st0 = s.shim_stats() or {}
         b0 = s.async_stats()
@@ -75,14 +70,12 @@ for name, path in (("shim", R.SHIM_PATH), ("reference", R.LIB_PATH)):
             # per completion batch (6 driven runs), in microseconds
             d = {k: ab1[k] - ab0[k] for k in ab0}
             nb = max(d["batches"], 1)
-            r["async_driven_breakdown_us_per_batch"] = {
-                "batches_per_run": round(d["batches"] / 6, 1), "states_per_batch": round(d["states"] / nb, 1),
-                "burst_wait": round(d["burst_ns"] / nb / 1e3, 2), "gather": round(d["gather_ns"] / nb / 1e3, 2),
-                "lookup_many": round(d["lookup_ns"] / nb / 1e3, 2), "callbacks": round(d["callback_ns"] / nb / 1e3, 2),
-                "rt_prep": round(d["rt_prep_ns"] / max(d["rt_calls"], 1) / 1e3, 2),
-                "rt_launch": round(d["rt_launch_ns"] / max(d["rt_calls"], 1) / 1e3, 2),
-                "rt_wait": round(d["rt_wait_ns"] / max(d["rt_calls"], 1) / 1e3, 2),
-                "run_us_per_batch": round(r["async_driven_8192_ms"] * 1e3 / max(d["batches"] / 6, 1), 2)}
+            r["async_driven_breakdown"] = {
+                "reaps_per_run": round(d["batches"] / 6, 1), "states_per_reap": round(d["states"] / nb, 1),
+                "submit_us_per_state": round(d["submit_ns"] / max(d["states"], 1) / 1e3, 3),
+                "reap_us_per_reap": round(d["reap_ns"] / nb / 1e3, 2),
+                "callbacks_us_per_reap": round(d["callback_ns"] / nb / 1e3, 2),
+                "run_us_per_reap": round(r["async_driven_8192_ms"] * 1e3 / max(d["batches"] / 6, 1), 2)}
         many = [s.add(s.hash_keys(K.ids_keys((np.uint64(100 + f) << np.uint64(32)) +
                                              np.arange(2000, dtype=np.uint64))), value=f % 30)
                 for f in range(512)]
