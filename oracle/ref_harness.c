@@ -639,6 +639,21 @@ __attribute__((weak)) uint64
 routing_filter_amd_async_probe_ns(void);
 __attribute__((weak)) void
 routing_filter_amd_async_breakdown(uint64 *out);
+__attribute__((weak)) void
+routing_filter_amd_add_breakdown(uint64 *out);
+
+/* out[0..8]: the shim's routing_filter_add breakdown (calls, batches, create / stage / build /
+ * infos / readback ns per batch, wait / place ns per add); 0 without a shim */
+int
+rfr_add_breakdown(uint64 *out)
+{
+   memset(out, 0, 9 * sizeof(uint64));
+   if (!routing_filter_amd_add_breakdown) {
+      return 0;
+   }
+   routing_filter_amd_add_breakdown(out);
+   return 1;
+}
 int
 rf_amd_diag_lookup_stats(uint64_t *out, int reset) __attribute__((weak));
 

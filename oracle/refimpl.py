@@ -112,6 +112,8 @@ def lib(path=LIB_PATH):
         L.rfr_lookup_keys_async_flush.restype = u64
         L.rfr_lookup_keys_async_flush_multi.argtypes = [vp, vp, vp, vp, vp, u32, u64, vp]
         L.rfr_lookup_keys_async_flush_multi.restype = u64
+        L.rfr_add_breakdown.argtypes = [vp]
+        L.rfr_add_breakdown.restype = ctypes.c_int
         L.rfr_async_breakdown.argtypes = [vp]
         L.rfr_async_breakdown.restype = ctypes.c_int
         if hasattr(L, "rfr_filter_test_basic"):  # the filter_test libraries only
@@ -411,6 +413,16 @@ class Stack:
             return None
         return dict(zip(("add_batches", "add_filters", "registry_bytes", "evictions", "trims", "async_probe_ns"),
                         (int(x) for x in out)))
+
+    def add_breakdown(self):
+        """the shim's routing_filter_add so far: calls, combiner batches, ns per phase (None
+        for the reference's library)"""
+        out = np.zeros(9, dtype=np.uint64)
+        if not self.L.rfr_add_breakdown(_p(out)):
+            return None
+        keys = ("calls", "batches", "create_ns", "stage_ns", "build_ns", "infos_ns", "readback_ns", "wait_ns",
+                "place_ns")
+        return dict(zip(keys, (int(x) for x in out)))
 
     def async_breakdown(self):
         """the shim's async path so far: reaps that completed states, states, ns submitting

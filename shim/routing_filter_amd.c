@@ -584,6 +584,20 @@ static pthread_cond_t  g_add_cv = PTHREAD_COND_INITIALIZER;
 static add_req        *g_add_head, *g_add_tail;
 static int             g_add_busy;
 static uint64          g_add_batches, g_add_filters;
+/* where routing_filter_add spends its time (routing_filter_amd_add_breakdown): per combiner
+ * batch -- batch creation, the staging copies, the build, the info read-back, the image
+ * read-back; per add -- the wait for its batch, the page allocation and fill */
+enum { AB_CALLS, AB_BATCHES, AB_CREATE, AB_STAGE, AB_BUILD, AB_INFOS, AB_READBACK, AB_WAIT, AB_PLACE, AB_N };
+static uint64 g_add_ns[AB_N];
+#define AB_ADD(k, v) __atomic_fetch_add(&g_add_ns[k], (v), __ATOMIC_RELAXED)
+
+void
+routing_filter_amd_add_breakdown(uint64 *out)
+{
+   for (int k = 0; k < AB_N; k++) {
+      out[k] = __atomic_load_n(&g_add_ns[k], __ATOMIC_RELAXED);
+   }
+}
 
 /* copies a request's fingerprints into its staging slot, unless another thread has claimed it */
 static void
@@ -615,7 +629,8 @@ run_adds(rf_amd_engine *e, add_req **rq, uint32 k)
       any_old |= old[i] != NULL;
       total += rq[i]->n;
    }
-   rf_amd_batch *b = NULL;
+   rf_amd_batch *b  = NULL;
+   uint64        tp = now_ns();
    int           r = rf_amd_batch_create(e, &rq[0]->c, k, num_new, value, any_old ? old : NULL,
                                any_old ? old_idx : NULL, &b);
    if (r == RF_AMD_ENOMEM) {
@@ -640,6 +655,9 @@ run_adds(rf_amd_engine *e, add_req **rq, uint32 k)
       copy made by its own waiting thread or by this one, whichever claims it first */
    uint32 *stage = NULL;
    r             = rf_amd_batch_stage_begin(b, &stage);
+   uint64 tn     = now_ns();
+   AB_ADD(AB_CREATE, tn - tp);
+   tp = tn;
    if (!r) {
       pthread_mutex_lock(&g_add_mu);
       uint64 at = 0;
@@ -657,13 +675,22 @@ run_adds(rf_amd_engine *e, add_req **rq, uint32 k)
             __builtin_ia32_pause();
          }
       }
+      tn = now_ns();
+      AB_ADD(AB_STAGE, tn - tp);
+      tp = tn;
       r = rf_amd_batch_stage_build(b);
+      tn = now_ns();
+      AB_ADD(AB_BUILD, tn - tp);
+      tp = tn;
    }
    (void)total;
    rf_amd_filter_info *infos = malloc(sizeof(*infos) * k);
    platform_assert(infos != NULL);
    if (!r) {
       r = rf_amd_batch_infos(b, infos, rf_amd_engine_stream(e));
+      tn = now_ns();
+      AB_ADD(AB_INFOS, tn - tp);
+      tp = tn;
    }
    const uint64 ps = rq[0]->c.page_size;
    for (uint32 i = 0; i < k && !r; i++) {
@@ -681,7 +708,9 @@ run_adds(rf_amd_engine *e, add_req **rq, uint32 k)
    }
    if (!r) {
       r = rf_amd_engine_sync(e);
+      AB_ADD(AB_READBACK, now_ns() - tp);
    }
+   AB_ADD(AB_BATCHES, 1);
    free(infos);
    if (r) {
       for (uint32 i = 0; i < k; i++) {
@@ -816,7 +845,11 @@ routing_filter_add(cache                *cc,
    }
 
    /* the image, on the GPU (coalesced with concurrent adds) */
+   const uint64 tw = now_ns();
    add_submit(e, &q);
+   const uint64 tpl = now_ns();
+   AB_ADD(AB_WAIT, tpl - tw);
+   AB_ADD(AB_CALLS, 1);
    registry_unpin(q.old_sb);
    if (q.rc) {
       free(q.pages);
@@ -878,6 +911,7 @@ routing_filter_add(cache                *cc,
    filter->num_unique       = info.num_unique;
    filter->value_size       = info.value_size;
 
+   AB_ADD(AB_PLACE, now_ns() - tpl);
    /* keep the filter on the device, its whole batch (the pin becomes the registry entry) */
    registry_insert(cc, filter->addr, q.sb, &q.f, 1, 0);
    return STATUS_OK;

@@ -25,6 +25,12 @@ routing_filter_amd_async_probe_ns(void);
 void
 routing_filter_amd_async_breakdown(uint64 *out);
 
+/* out[0..8]: routing_filter_add calls, combiner batches, then ns totals: batch creation,
+ * staging copies, build, info read-back, image read-back (per batch); the wait for the batch,
+ * page allocation and fill (per add) -- diagnostics */
+void
+routing_filter_amd_add_breakdown(uint64 *out);
+
 /* routing_filter_add calls coalesced: GPU batches built and filters they held */
 void
 routing_filter_amd_add_stats(uint64 *batches, uint64 *filters);

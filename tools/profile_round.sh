@@ -4,10 +4,11 @@
 #      summarised to per-launch HBM bytes per kernel;
 #   2. rocprofv3 --kernel-trace --stats of the default bench command;
 #   3. the bench lines (c2 with the CPU baseline, c3, c4, c5, routed, compaction) with roofline
-#      traffic from (1), the compaction chain's kernel trace and the shim's per-call costs.
+#      traffic from (1), the compaction chain's kernel trace, the shim's per-call costs and the
+#      reference's own kvstore driving the shim (tools/trunk_latency.py).
 # usage: bash tools/profile_round.sh <tag>      (outputs under gpurun_out/prof_<tag>/)
 set -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r04}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/prof_$TAG
@@ -32,9 +33,7 @@ timeout -s KILL 180 rocprofv3 --pmc $TCC --output-format csv -d $O/tcc3 -o c3 --
 python3 tools/tcc_summary.py $O/tcc2/c2_counter_collection.csv $O/tcc3/c3_counter_collection.csv > $O/tcc_$TAG.txt || exit 1
 timeout -k 10 300 python3 bench.py --workload compaction --steps 5 --warmup 1 > $O/bench_compaction.json 2> $O/bench_compaction.err || { echo "bench compaction failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktc -o comp -- python3 bench.py --workload compaction --steps 2 --warmup 0 --no-cpu-baseline > $O/ktc.log 2>&1 || { echo "compaction kernel trace failed"; exit 1; }
-# k_probe against the software-pipelined persistent k_probe_pipe (7 workgroups per CU), C2 and C3
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktp -o pipe_c2 -- python3 tools/probe_pipe_ab.py c2 0 7 > $O/pipe_c2.txt 2>&1 || { echo "pipe c2 failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktp -o pipe_c3 -- python3 tools/probe_pipe_ab.py c3 0 7 > $O/pipe_c3.txt 2>&1 || { echo "pipe c3 failed"; exit 1; }
 # the drop-in's per-call costs beside the reference's routing_filter.c (tools/shim_latency.py)
 timeout -k 10 600 python3 tools/shim_latency.py > $O/shim_latency_$TAG.json 2> $O/shim_latency.err || { echo "shim latency failed"; exit 1; }
+timeout -k 10 300 python3 tools/trunk_latency.py > $O/trunk_latency_$TAG.json 2> $O/trunk_latency.err || { echo "trunk latency failed"; exit 1; }
 cat $O/bench_c2.json

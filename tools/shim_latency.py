@@ -41,8 +41,23 @@ for name, path in (("shim", R.SHIM_PATH), ("reference", R.LIB_PATH)):
         keys = [K.ids_keys((np.uint64(f) << np.uint64(32)) + np.arange(n, dtype=np.uint64)) for f in range(8)]
         hs = [s.hash_keys(k) for k in keys]
         base = s.add(hs[0])
-        r = {"add_fresh_ms": med(lambda: s.add(hs[0])),
-             "add_incremental_ms": med(lambda: s.add(hs[1], value=1, old=base))}
+        def add_phases(fn):
+            """median ms of fn, and the shim's add breakdown over its runs (us per add / batch)"""
+            a0 = s.add_breakdown()
+            ms = med(fn)
+            a1 = s.add_breakdown()
+            if not a0:
+                return ms, None
+            d = {k: a1[k] - a0[k] for k in a0}
+            c, nb = max(d["calls"], 1), max(d["batches"], 1)
+            return ms, {"adds": d["calls"], "batches": d["batches"],
+                        **{f"{k}_us_per_batch": round(d[f"{k}_ns"] / nb / 1e3, 1)
+                           for k in ("create", "stage", "build", "infos", "readback")},
+                        **{f"{k}_us_per_add": round(d[f"{k}_ns"] / c / 1e3, 1) for k in ("wait", "place")}}
+
+        r = {}
+        r["add_fresh_ms"], r["add_fresh_breakdown"] = add_phases(lambda: s.add(hs[0]))
+        r["add_incremental_ms"], r["add_incremental_breakdown"] = add_phases(lambda: s.add(hs[1], value=1, old=base))
         descs = [s.add(h, value=i % 8) for i, h in enumerate(hs)]
         rng = np.random.default_rng(1)
         P = 8192
@@ -85,7 +100,17 @@ for name, path in (("shim", R.SHIM_PATH), ("reference", R.LIB_PATH)):
         mkeys = K.ids_keys(np.arange(T * n, dtype=np.uint64) + np.uint64(1 << 40))
         pr = K.random_keys(T * 16, seed=1)
         # the adds' wall time: the slowest thread's, hashing excluded (rfr_mt_chains)
+        a0 = s.add_breakdown()
         ts8 = [float(s.mt_chains(mkeys, T, 1, n, pr, 16)[3].max()) for _ in range(3)]
+        a1 = s.add_breakdown()
+        if a0:
+            d = {k: a1[k] - a0[k] for k in a0}
+            c, nb = max(d["calls"], 1), max(d["batches"], 1)
+            r["mt_adds_8x_breakdown"] = {"adds": d["calls"], "batches": d["batches"],
+                                         **{f"{k}_us_per_batch": round(d[f"{k}_ns"] / nb / 1e3, 1)
+                                            for k in ("create", "stage", "build", "infos", "readback")},
+                                         **{f"{k}_us_per_add": round(d[f"{k}_ns"] / c / 1e3, 1)
+                                            for k in ("wait", "place")}}
         ts1 = [float(s.mt_chains(mkeys[: n], 1, 1, n, pr[:16], 16)[3].max()) for _ in range(3)]
         r["mt_adds_8x_ms"] = round(float(np.median(ts8)) * 1e3, 3)
         r["mt_adds_1x_ms"] = round(float(np.median(ts1)) * 1e3, 3)
