@@ -169,6 +169,28 @@ int rf_amd_engine_pool_trim(rf_amd_engine *e, uint64_t keep_bytes);
  * its synchronisation (only that stream, not the device) */
 void *rf_amd_engine_stream(rf_amd_engine *e);
 int   rf_amd_engine_sync(rf_amd_engine *e);
+/* pinned host memory: a read-back target that the DMA engines write at full PCIe rate (a
+ * copy into pageable memory goes through the driver's staging buffers) */
+int  rf_amd_host_alloc(rf_amd_engine *e, uint64_t bytes, void **out);
+void rf_amd_host_free(rf_amd_engine *e, void *p);
+/* a completion point after the work queued on the engine stream so far (e.g. one filter's
+ * image read-back); fence_wait blocks until it has passed and releases it (once) */
+int rf_amd_engine_fence(rf_amd_engine *e, uint64_t *fence);
+/* host memory the kernels may write directly (e.g. a page cache's buffer, registered once):
+ * rf_amd_batch_place_image stores images there without a staging copy */
+int rf_amd_host_register(rf_amd_engine *e, void *p, uint64_t bytes);
+int rf_amd_host_unregister(rf_amd_engine *e, void *p);
+/* filter f's image straight into host pages (replaces the reference's page fill,
+ * src/routing_filter.c:603-633): `table` (rf_amd_host_alloc'd) holds the destination of each
+ * of the num_pages image pages (inside registered memory), then each page's disk address,
+ * then the destinations of the ceil(num_indices / addrs_per_page) index pages. One call writes
+ * pages [first_page, first_page + count) and, with_index, the absolute index slots; the
+ * destinations it uses are translated in place. Stream-ordered (NULL: the engine stream):
+ * wait with rf_amd_engine_fence before using the pages */
+int rf_amd_batch_place_image(rf_amd_batch *b, uint32_t f, uint64_t *table, uint32_t num_pages,
+                             uint32_t first_page, uint32_t count, int with_index, uint32_t addrs_per_page,
+                             void *stream);
+int rf_amd_engine_fence_wait(rf_amd_engine *e, uint64_t fence);
 /* Residency control for callers that keep many built batches (the shim's registry):
  * device_bytes = the device memory the batch holds; trim drops its build work buffers,
  * keeping pages, slots, probe lines and plans (lookups, image reads, estimates and use as an

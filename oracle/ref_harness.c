@@ -345,6 +345,11 @@ rfr_create(uint32 fingerprint_size, uint32 log_index_size, uint64 cache_mib, uin
    return s;
 }
 
+/* the shim's release of a cache whose page buffer took images directly (weak: absent from
+ * the reference's own library) */
+__attribute__((weak)) void
+routing_filter_amd_cache_release(cache *cc);
+
 void
 rfr_destroy(rfr_stack *s)
 {
@@ -352,6 +357,9 @@ rfr_destroy(rfr_stack *s)
       return;
    }
    mem_cleanup(&s->io.super, 0); /* complete every outstanding request first */
+   if (routing_filter_amd_cache_release) {
+      routing_filter_amd_cache_release((cache *)&s->cc);
+   }
    clockcache_deinit(&s->cc);
    rc_allocator_deinit(&s->al);
    munmap(s->io.disk, s->io.size);

@@ -209,10 +209,18 @@ rfk_open(uint64 cache_mib,
    return k;
 }
 
+/* the shim's release of a cache whose page buffer took images directly (weak: absent from
+ * the reference's own library) */
+__attribute__((weak)) void
+routing_filter_amd_cache_release(cache *cc);
+
 void
 rfk_close(rfk_kvs *k)
 {
    if (k) {
+      if (routing_filter_amd_cache_release) {
+         routing_filter_amd_cache_release((cache *)splinterdb_get_cache_handle(k->kvs));
+      }
       splinterdb_close(&k->kvs);
       free(k);
    }

@@ -69,6 +69,7 @@
  * every filter they name.
  */
 #include "routing_filter.h"
+#include "clockcache.h"
 #include "mini_allocator.h"
 #include "iterator.h"
 #include "platform_assert.h"
@@ -567,8 +568,11 @@ typedef struct add_req {
    /* results */
    int                rc;
    rf_amd_filter_info info;
-   uint8             *pages;
+   uint8             *pages; /* pinned read-back buffer: pages, then slots */
    uint64            *slots;
+   uint64             pin_cap; /* bytes of the pinned buffer (returned to the pool) */
+   uint64             fence;   /* the read-back's completion point on the engine stream */
+   int                direct;  /* no read-back: the adding thread places the image itself */
    shim_batch        *sb; /* the built batch, pinned once for this request */
    uint32             f;
    int                done;
@@ -607,6 +611,186 @@ add_copy(add_req *q)
       memcpy(q->stage_dst, q->hashes, sizeof(uint32) * q->n);
       __atomic_store_n(&q->copied, 1, __ATOMIC_RELEASE);
    }
+}
+
+/* pinned read-back buffers, recycled: an image is read straight into one by the DMA engine
+ * (a read-back into malloc'd memory goes through the driver's staging copies), then copied
+ * into the cache pages by its adding thread */
+#define PIN_POOL 16
+static struct {
+   void  *p;
+   uint64 cap;
+} g_pin_pool[PIN_POOL];
+static uint32          g_pin_n;
+static pthread_mutex_t g_pin_mu = PTHREAD_MUTEX_INITIALIZER;
+
+/* RF_SHIM_PINNED=0: read-backs into malloc'd memory after one engine-wide sync (A/B) */
+static int
+pin_enabled(void)
+{
+   static int v = -1;
+   if (v < 0) {
+      const char *s = getenv("RF_SHIM_PINNED");
+      v             = (s && s[0] == '0') ? 0 : 1;
+   }
+   return v;
+}
+
+static void *
+pin_take_any(rf_amd_engine *e, uint64 bytes, uint64 *cap, int force)
+{
+   if (!force && !pin_enabled()) {
+      *cap = bytes;
+      return malloc(bytes);
+   }
+   pthread_mutex_lock(&g_pin_mu);
+   for (uint32 i = 0; i < g_pin_n; i++) { /* the smallest that fits */
+      if (g_pin_pool[i].cap >= bytes) {
+         uint32 best = i;
+         for (uint32 j = i + 1; j < g_pin_n; j++) {
+            if (g_pin_pool[j].cap >= bytes && g_pin_pool[j].cap < g_pin_pool[best].cap) {
+               best = j;
+            }
+         }
+         void *p = g_pin_pool[best].p;
+         *cap    = g_pin_pool[best].cap;
+         g_pin_pool[best] = g_pin_pool[--g_pin_n];
+         pthread_mutex_unlock(&g_pin_mu);
+         return p;
+      }
+   }
+   pthread_mutex_unlock(&g_pin_mu);
+   const uint64 c = bytes < (1ull << 20) ? (1ull << 20) : bytes + bytes / 4;
+   void        *p = NULL;
+   if (rf_amd_host_alloc(e, c, &p)) {
+      return NULL;
+   }
+   *cap = c;
+   return p;
+}
+
+static void
+pin_give_any(rf_amd_engine *e, void *p, uint64 cap, int force)
+{
+   if (!p) {
+      return;
+   }
+   if (!force && !pin_enabled()) {
+      free(p);
+      return;
+   }
+   pthread_mutex_lock(&g_pin_mu);
+   if (g_pin_n < PIN_POOL) {
+      g_pin_pool[g_pin_n].p   = p;
+      g_pin_pool[g_pin_n].cap = cap;
+      g_pin_n++;
+      p = NULL;
+   }
+   pthread_mutex_unlock(&g_pin_mu);
+   if (p) {
+      rf_amd_host_free(e, p);
+   }
+}
+
+static void *
+pin_take(rf_amd_engine *e, uint64 bytes, uint64 *cap)
+{
+   return pin_take_any(e, bytes, cap, 0);
+}
+
+static void
+pin_give(rf_amd_engine *e, void *p, uint64 cap)
+{
+   pin_give_any(e, p, cap, 0);
+}
+
+/* ---- images placed straight into the cache's pages -----------------------------------------
+ * The cache's page buffer (clockcache.c:3426, one platform_buffer of cfg->capacity bytes) is
+ * registered with the engine once; an add then writes its image into the pages it allocated
+ * with one kernel (its stores cross PCIe), instead of a read-back into a bounce buffer and a
+ * memcpy per page (src/routing_filter.c:603-633 fills the pages in place too). The cache is a
+ * clockcache (SplinterDB's only cache); every destination is checked against the registered
+ * range by the engine before the launch. RF_SHIM_DIRECT=0 keeps the bounce-buffer path. */
+#define DIRECT_CACHES 16
+static struct {
+   const cache *cc;
+   char        *base;
+   uint64       bytes;
+   int          ok;
+} g_direct[DIRECT_CACHES];
+static uint32          g_direct_n;
+static pthread_mutex_t g_direct_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static int
+direct_enabled(void)
+{
+   static int v = -1;
+   if (v < 0) {
+      const char *s = getenv("RF_SHIM_DIRECT");
+      v             = (s && s[0] == '0') ? 0 : 1;
+   }
+   return v;
+}
+
+/* 1 when cc's page buffer is registered with the engine (registering it on first use) */
+static int
+cache_direct(rf_amd_engine *e, cache *cc)
+{
+   if (!direct_enabled()) {
+      return 0;
+   }
+   int         ok = 0, found = 0;
+   clockcache *ccc = (clockcache *)cc;
+   pthread_mutex_lock(&g_direct_mu);
+   for (uint32 i = 0; i < g_direct_n; i++) {
+      if (g_direct[i].cc == cc) {
+         if (g_direct[i].base != ccc->data || !ccc->cfg || g_direct[i].bytes != ccc->cfg->capacity) {
+            /* another cache at this address since: drop the old registration */
+            if (g_direct[i].ok) {
+               (void)rf_amd_host_unregister(e, g_direct[i].base);
+            }
+            g_direct[i] = g_direct[--g_direct_n];
+            break;
+         }
+         ok    = g_direct[i].ok;
+         found = 1;
+         break;
+      }
+   }
+   if (!found && g_direct_n < DIRECT_CACHES) {
+      char       *base  = ccc->data;
+      uint64      bytes = ccc->cfg ? ccc->cfg->capacity : 0;
+      ok = base && bytes && rf_amd_host_register(e, base, bytes) == 0;
+      g_direct[g_direct_n].cc    = cc;
+      g_direct[g_direct_n].base  = base;
+      g_direct[g_direct_n].bytes = bytes;
+      g_direct[g_direct_n].ok    = ok;
+      g_direct_n++;
+   }
+   pthread_mutex_unlock(&g_direct_mu);
+   return ok;
+}
+
+/* a cache is going away (its buffer may be reused): unregister it. The entry stays, marked
+ * released, so adds issued while the cache closes take the bounce-buffer path instead of
+ * registering it again; a later cache at this address with another buffer replaces it. */
+void
+routing_filter_amd_cache_release(cache *cc)
+{
+   pthread_mutex_lock(&g_direct_mu);
+   for (uint32 i = 0; i < g_direct_n; i++) {
+      if (g_direct[i].cc == cc) {
+         if (g_direct[i].ok) {
+            rf_amd_engine *e = engine();
+            if (e) {
+               (void)rf_amd_host_unregister(e, g_direct[i].base);
+            }
+         }
+         g_direct[i].ok = 0;
+         break;
+      }
+   }
+   pthread_mutex_unlock(&g_direct_mu);
 }
 
 /* builds k requests of one config as one batch; a batch that cannot be created (one
@@ -700,21 +884,41 @@ run_adds(rf_amd_engine *e, add_req **rq, uint32 k)
          q->rc = RF_AMD_EINVAL; /* a block over a page: undefined behaviour in the reference */
          continue;
       }
-      q->pages = malloc(ps * q->info.num_pages + 16);
-      q->slots = malloc(sizeof(uint64) * q->info.num_indices);
-      platform_assert(q->pages && q->slots);
-      r = rf_amd_batch_read_image_async(b, i, q->pages, ps * q->info.num_pages, q->slots,
+      if (q->direct) {
+         continue; /* its thread writes the image into its cache pages */
+      }
+      /* the image and its slots into a pinned buffer; each request gets its own completion
+         point, so its thread places its pages while the next images are still in flight */
+      const uint64 pb = (ps * q->info.num_pages + 15) & ~15ull;
+      q->pages        = pin_take(e, pb + sizeof(uint64) * q->info.num_indices, &q->pin_cap);
+      if (!q->pages) {
+         r = RF_AMD_ENOMEM;
+         break;
+      }
+      q->slots = (uint64 *)(q->pages + pb);
+      r        = rf_amd_batch_read_image_async(b, i, q->pages, ps * q->info.num_pages, q->slots,
                                         q->info.num_indices, NULL);
+      if (!r && pin_enabled()) {
+         r = rf_amd_engine_fence(e, &q->fence);
+      }
    }
-   if (!r) {
+   if (!r && !pin_enabled()) {
       r = rf_amd_engine_sync(e);
-      AB_ADD(AB_READBACK, now_ns() - tp);
    }
+   AB_ADD(AB_READBACK, now_ns() - tp);
    AB_ADD(AB_BATCHES, 1);
    free(infos);
    if (r) {
+      (void)rf_amd_engine_sync(e); /* read-backs already queued land before their buffers go */
       for (uint32 i = 0; i < k; i++) {
          rq[i]->rc = r;
+         if (rq[i]->fence) {
+            (void)rf_amd_engine_fence_wait(e, rq[i]->fence);
+            rq[i]->fence = 0;
+         }
+         pin_give(e, rq[i]->pages, rq[i]->pin_cap);
+         rq[i]->pages = NULL;
+         rq[i]->slots = NULL;
       }
       rf_amd_batch_destroy_on(b, NULL);
       return;
@@ -812,6 +1016,87 @@ routing_filter_amd_add_stats(uint64 *batches, uint64 *filters)
    *filters = __atomic_load_n(&g_add_filters, __ATOMIC_RELAXED);
 }
 
+/* pages held write-locked at once while their images land (the reference holds one) */
+#define PLACE_CHUNK 512
+
+/* Allocates q's data pages in the reference's order (mini_alloc + cache_alloc per page,
+ * :603-610) and has the engine write the image into them and the absolute index slots into
+ * the index pages (:612-633), PLACE_CHUNK pages per launch, each chunk unlocked once its
+ * images have landed. A launch the engine refuses (a page outside the registered buffer)
+ * falls back to a read-back of the image and a copy per page. */
+static void
+place_direct(rf_amd_engine  *e,
+             cache          *cc,
+             add_req        *q,
+             mini_allocator *mini,
+             page_handle   **index_page,
+             uint64          addrs_per_page,
+             uint64         *page_addr)
+{
+   const uint64 np  = q->info.num_pages, ni = q->info.num_indices;
+   const uint64 nip = (ni + addrs_per_page - 1) / addrs_per_page;
+   const uint64 ps  = q->c.page_size;
+   rf_amd_batch *b  = q->sb->b;
+   uint64        tcap = 0, bcap = 0;
+   uint64       *table = pin_take_any(e, sizeof(uint64) * (2 * np + nip + 1), &tcap, 1);
+   uint8        *bounce = NULL; /* the fallback's read-back: pages, then slots */
+   page_handle **ph     = malloc(sizeof(*ph) * (np ? np : 1));
+   platform_assert(table && ph);
+   for (uint64 i = 0; i < nip; i++) {
+      table[2 * np + i] = (uint64)(uintptr_t)index_page[i]->data;
+   }
+   for (uint64 k0 = 0; k0 < np || k0 == 0; k0 += PLACE_CHUNK) {
+      const uint64 cnt  = np - k0 < PLACE_CHUNK ? np - k0 : PLACE_CHUNK;
+      const int    last = k0 + cnt == np;
+      for (uint64 k = k0; k < k0 + cnt; k++) {
+         page_addr[k]     = mini_alloc(mini, 0, NULL);
+         ph[k]            = cache_alloc(cc, page_addr[k], PAGE_TYPE_FILTER);
+         table[k]         = (uint64)(uintptr_t)ph[k]->data;
+         table[np + k]    = page_addr[k];
+      }
+      int r = bounce ? 1
+                     : rf_amd_batch_place_image(b, q->f, table, (uint32)np, (uint32)k0, (uint32)cnt, last,
+                                                (uint32)addrs_per_page, NULL);
+      uint64 fence = 0;
+      if (!r) {
+         r = rf_amd_engine_fence(e, &fence);
+      }
+      if (!r) {
+         r = rf_amd_engine_fence_wait(e, fence);
+      }
+      if (r) {
+         if (!bounce) { /* one read-back of the whole image and its slots */
+            const uint64 pb = (ps * np + 15) & ~15ull;
+            bounce          = pin_take_any(e, pb + sizeof(uint64) * ni + 8, &bcap, 1);
+            platform_assert(bounce != NULL);
+            platform_assert(rf_amd_batch_read_image_async(b, q->f, bounce, ps * np, bounce + pb, (uint32)ni,
+                                                          NULL)
+                            == 0);
+            platform_assert(rf_amd_engine_sync(e) == 0);
+         }
+         for (uint64 k = k0; k < k0 + cnt; k++) {
+            memcpy(ph[k]->data, bounce + k * ps, ps);
+         }
+         if (last) {
+            const uint64 *slots = (const uint64 *)(bounce + ((ps * np + 15) & ~15ull));
+            for (uint64 i = 0; i < ni; i++) {
+               uint64 *cursor = (uint64 *)index_page[i / addrs_per_page]->data + i % addrs_per_page;
+               *cursor        = page_addr[slots[i] / ps] + slots[i] % ps;
+            }
+         }
+      }
+      for (uint64 k = k0; k < k0 + cnt; k++) {
+         unlock_and_unget_page(cc, ph[k]);
+      }
+      if (last) {
+         break;
+      }
+   }
+   free(ph);
+   pin_give_any(e, table, tcap, 1);
+   pin_give_any(e, bounce, bcap, 1);
+}
+
 platform_status
 routing_filter_add(cache                *cc,
                    const routing_config *cfg,
@@ -845,15 +1130,21 @@ routing_filter_add(cache                *cc,
    }
 
    /* the image, on the GPU (coalesced with concurrent adds) */
+   q.direct        = cache_direct(e, cc);
    const uint64 tw = now_ns();
    add_submit(e, &q);
+   if (q.fence) { /* this request's image has landed in its pinned buffer */
+      int fr = rf_amd_engine_fence_wait(e, q.fence);
+      if (fr && !q.rc) {
+         q.rc = fr;
+      }
+   }
    const uint64 tpl = now_ns();
    AB_ADD(AB_WAIT, tpl - tw);
    AB_ADD(AB_CALLS, 1);
    registry_unpin(q.old_sb);
    if (q.rc) {
-      free(q.pages);
-      free(q.slots);
+      pin_give(e, q.pages, q.pin_cap);
       registry_unpin(q.sb);
       return status_of(q.rc);
    }
@@ -888,24 +1179,27 @@ routing_filter_add(cache                *cc,
    /* data pages in placement order (:453-455, :603-610), each filled from the image */
    uint64 *page_addr = malloc(sizeof(uint64) * info.num_pages);
    platform_assert(page_addr != NULL);
-   for (uint32 k = 0; k < info.num_pages; k++) {
-      page_addr[k]        = mini_alloc(&mini, 0, NULL);
-      page_handle *page   = cache_alloc(cc, page_addr[k], PAGE_TYPE_FILTER);
-      memcpy(page->data, pages + k * ps, ps);
-      unlock_and_unget_page(cc, page);
-   }
-   /* absolute index slots (:612-620) */
-   for (uint32 i = 0; i < info.num_indices; i++) {
-      uint64 *cursor = (uint64 *)index_page[i / addrs_per_page]->data + i % addrs_per_page;
-      *cursor        = page_addr[slots[i] / ps] + slots[i] % ps;
+   if (q.direct) {
+      place_direct(e, cc, &q, &mini, index_page, addrs_per_page, page_addr);
+   } else {
+      for (uint32 k = 0; k < info.num_pages; k++) {
+         page_addr[k]      = mini_alloc(&mini, 0, NULL);
+         page_handle *page = cache_alloc(cc, page_addr[k], PAGE_TYPE_FILTER);
+         memcpy(page->data, pages + k * ps, ps);
+         unlock_and_unget_page(cc, page);
+      }
+      /* absolute index slots (:612-620) */
+      for (uint32 i = 0; i < info.num_indices; i++) {
+         uint64 *cursor = (uint64 *)index_page[i / addrs_per_page]->data + i % addrs_per_page;
+         *cursor        = page_addr[slots[i] / ps] + slots[i] % ps;
+      }
    }
    for (uint64 i = 0; i < pages_per_extent; i++) {
       unlock_and_unget_page(cc, index_page[i]);
    }
    mini_release(&mini);
    free(page_addr);
-   free(q.pages);
-   free(q.slots);
+   pin_give(e, q.pages, q.pin_cap);
 
    filter->num_fingerprints = (uint32)nfp;
    filter->num_unique       = info.num_unique;

@@ -54,3 +54,9 @@ routing_filter_amd_lookup_batch(cache                *cc,
                                 const key            *keys,
                                 uint64                n,
                                 uint64               *found);
+
+/* routing_filter_add writes its images straight into the cache's page buffer, which it
+ * registers with the GPU on the cache's first add (RF_SHIM_DIRECT=0: a bounce buffer and a
+ * copy per page instead). Before a cache is destroyed, this releases that registration. */
+void
+routing_filter_amd_cache_release(cache *cc);

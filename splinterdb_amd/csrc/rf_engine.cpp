@@ -27,6 +27,9 @@
 using namespace rf;
 
 extern "C" int rf_launch_build(const LaunchArgs* a);
+extern "C" int rf_launch_place(void* stream, const uint8_t* img, const uint64_t* slots, uint32_t first_page,
+                                uint32_t count, uint32_t num_pages, uint32_t num_indices, uint32_t page_size,
+                                const uint64_t* table, uint32_t addrs_per_page);
 extern "C" int rf_launch_old_decode(const LaunchArgs* a);
 extern "C" int rf_launch_wave_tab(void* stream, const uint64_t* runs, uint32_t nf, uint64_t n, uint32_t* tab);
 extern "C" int rf_launch_plines(const LaunchArgs* a);
@@ -186,6 +189,18 @@ struct LookupServer {
 struct rf_amd_engine {
   int device;
   LookupServer srv;
+  // completion points on the engine stream (rf_amd_engine_fence): recycled events
+  std::mutex fence_mu;
+  std::vector<hipEvent_t> fence_free;
+  // host ranges registered for direct image placement (rf_amd_host_register): host base,
+  // bytes, device address of the base
+  struct HostReg {
+    uintptr_t h;
+    uint64_t bytes;
+    uintptr_t d;
+  };
+  std::mutex reg_mu;
+  std::vector<HostReg> regs;
   hipStream_t stream;
   DevPool pool;
   HostStage stage;
@@ -319,6 +334,8 @@ extern "C" void rf_amd_engine_destroy(rf_amd_engine* e) {
     delete s;
   }
   e->pool.drain();
+  for (hipEvent_t ev : e->fence_free) (void)hipEventDestroy(ev);
+  for (const auto& r : e->regs) (void)hipHostUnregister((void*)r.h);
   if (e->stage.h) (void)hipHostFree(e->stage.h);
   if (e->stage.d) (void)hipFree(e->stage.d);
   delete e;
@@ -521,6 +538,10 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
           ob->cfg.fingerprint_size == fps && ob->cfg.log_index_size == lis) {
         const uint32_t* es = ob->wide ? ob->d_sorted.as<uint32_t>() : ob->d_part.as<uint32_t>();
         p.old_direct = 1;
+        // same geometry: one new index per old index, so K6 can merge the old entries in
+        // place (merge6); RF_AMD_K6_MERGE=0 keeps the merge in K4
+        const char* m6 = getenv("RF_AMD_K6_MERGE");
+        p.merge6 = (p.npo == 1 && !(m6 && m6[0] == '0')) ? 1u : 0u;
         p.old_entries = es + op->e_first;
         p.old_idx_start = ob->d_idx_start.as<uint32_t>() + op->idx_base;
         p.old_idx_cnt = ob->d_idx_cnt.as<uint32_t>() + op->idx_base;
@@ -736,6 +757,140 @@ extern "C" int rf_amd_engine_sync(rf_amd_engine* e) {
   return 0;
 }
 
+extern "C" int rf_amd_host_alloc(rf_amd_engine* e, uint64_t bytes, void** out) {
+  if (!e || !out) return fail(RF_AMD_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(e->device));
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) {
+    *out = nullptr;
+    return fail(RF_AMD_ENOMEM, "hipHostMalloc failed");
+  }
+  return 0;
+}
+
+extern "C" void rf_amd_host_free(rf_amd_engine* e, void* p) {
+  (void)e;
+  if (p) (void)hipHostFree(p);
+}
+
+// a fence is an event recorded on the engine stream; its handle travels as a uint64
+extern "C" int rf_amd_engine_fence(rf_amd_engine* e, uint64_t* fence) {
+  if (!e || !fence) return fail(RF_AMD_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(e->device));
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> g(e->fence_mu);
+    if (!e->fence_free.empty()) {
+      ev = e->fence_free.back();
+      e->fence_free.pop_back();
+    }
+  }
+  if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(ev, e->stream));
+  *fence = (uint64_t)(uintptr_t)ev;
+  return 0;
+}
+
+extern "C" int rf_amd_engine_fence_wait(rf_amd_engine* e, uint64_t fence) {
+  if (!e || !fence) return fail(RF_AMD_EINVAL, "null argument");
+  hipEvent_t ev = (hipEvent_t)(uintptr_t)fence;
+  const hipError_t r = hipEventSynchronize(ev);
+  {
+    std::lock_guard<std::mutex> g(e->fence_mu);
+    e->fence_free.push_back(ev);
+  }
+  if (r != hipSuccess) return fail(RF_AMD_EINVAL, std::string("fence: ") + hipGetErrorString(r));
+  return 0;
+}
+
+static int batch_errors(rf_amd_batch* b);
+
+extern "C" int rf_amd_host_register(rf_amd_engine* e, void* p, uint64_t bytes) {
+  if (!e || !p || !bytes) return fail(RF_AMD_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(e->device));
+  std::lock_guard<std::mutex> g(e->reg_mu);
+  const uintptr_t h = (uintptr_t)p;
+  for (const auto& r : e->regs)
+    if (h < r.h + r.bytes && r.h < h + bytes) return fail(RF_AMD_EINVAL, "range overlaps a registered one");
+  if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(RF_AMD_ENOMEM, "hipHostRegister failed");
+  }
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+    (void)hipHostUnregister(p);
+    return fail(RF_AMD_EINVAL, "no device address for the registered range");
+  }
+  e->regs.push_back({h, bytes, (uintptr_t)d});
+  return 0;
+}
+
+extern "C" int rf_amd_host_unregister(rf_amd_engine* e, void* p) {
+  if (!e || !p) return fail(RF_AMD_EINVAL, "null argument");
+  std::lock_guard<std::mutex> g(e->reg_mu);
+  for (size_t i = 0; i < e->regs.size(); i++) {
+    if (e->regs[i].h == (uintptr_t)p) {
+      HIPCHK(hipSetDevice(e->device));
+      (void)hipHostUnregister(p);
+      e->regs.erase(e->regs.begin() + i);
+      return 0;
+    }
+  }
+  return fail(RF_AMD_EINVAL, "not a registered range");
+}
+
+// Filter f's image pages [first_page, first_page + count) (and, with_index, its index slots)
+// written straight into host pages (D2H by the kernel's own stores, no staging copy): table (rf_amd_host_alloc'd, 2 * num_pages + ceil(num_indices /
+// addrs_per_page) words) = the destination of each image page (host addresses inside a
+// registered range), each page's disk address, and each index page's destination. The
+// destinations are checked against the registered ranges and replaced in place by their
+// device addresses; index slot i becomes disk_addr[slot / page_size] + slot % page_size,
+// written at word i % addrs_per_page of index page i / addrs_per_page (src/routing_filter.c
+// :612-620). Stream-ordered; the caller waits (rf_amd_engine_fence) before using the pages.
+extern "C" int rf_amd_batch_place_image(rf_amd_batch* b, uint32_t f, uint64_t* table, uint32_t num_pages,
+                                        uint32_t first_page, uint32_t count, int with_index,
+                                        uint32_t addrs_per_page, void* stream) {
+  if (!b || f >= b->F || !table || !addrs_per_page) return fail(RF_AMD_EINVAL, "bad argument");
+  if (int rc = batch_errors(b)) return rc;
+  if (b->err_host[f]) return fail(RF_AMD_EINVAL, "the filter's build failed");
+  const FilterPlan& p = b->plans[f];
+  const uint32_t P = b->cfg.page_size;
+  if (num_pages > p.page_cap || first_page > num_pages || count > num_pages - first_page)
+    return fail(RF_AMD_EINVAL, "pages outside the filter's reservation");
+  const uint32_t nidx = with_index ? p.num_indices : 0u, nip = (nidx + addrs_per_page - 1) / addrs_per_page;
+  if ((uint64_t)addrs_per_page * 8 > P) return fail(RF_AMD_EINVAL, "index page overflow");
+  rf_amd_engine* e = b->eng;
+  {
+    std::lock_guard<std::mutex> g(e->reg_mu);
+    size_t hint = 0;
+    auto xlate = [&](uint64_t& w, uint64_t len) -> bool {
+      const uintptr_t h = (uintptr_t)w;
+      for (size_t k = 0; k < e->regs.size(); k++) {
+        const auto& r = e->regs[(hint + k) % e->regs.size()];
+        if (h >= r.h && h + len <= r.h + r.bytes) {
+          hint = (hint + k) % e->regs.size();
+          w = r.d + (h - r.h);
+          return true;
+        }
+      }
+      return false;
+    };
+    for (uint32_t k = first_page; k < first_page + count; k++)
+      if (!xlate(table[k], P)) return fail(RF_AMD_EINVAL, "page destination outside the registered ranges");
+    for (uint32_t k = 0; k < nip; k++)
+      if (!xlate(table[2ull * num_pages + k], P)) return fail(RF_AMD_EINVAL, "index page outside the registered ranges");
+  }
+  void* dt = nullptr;
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipHostGetDevicePointer(&dt, table, 0));
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  const int rc = rf_launch_place(st, b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * P,
+                                 b->d_slots.as<uint64_t>() + p.idx_base, first_page, count, num_pages, nidx, P,
+                                 (const uint64_t*)dt, addrs_per_page);
+  if (rc) return fail(RF_AMD_EINVAL, std::string("place launch: ") + hipGetErrorString((hipError_t)rc));
+  return 0;
+}
+
 extern "C" int rf_amd_engine_pool_stats(rf_amd_engine* e, uint64_t* pooled_bytes, uint64_t* hits, uint64_t* misses) {
   if (!e) return fail(RF_AMD_EINVAL, "null engine");
   std::lock_guard<std::mutex> g(e->pool.mu);
@@ -801,6 +956,8 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.overflow = b->d_overflow.as<uint32_t>();
   a.spill = b->d_spill.p ? b->d_spill.as<uint32_t>() : nullptr;
   a.cb_outs = b->d_cb_out.p ? b->d_cb_out.as<uint32_t>() : nullptr;
+  a.any_merge6 = 0;
+  for (const auto& p : b->plans) a.any_merge6 |= p.merge6;
   a.idx_cnt = b->d_idx_cnt.as<uint32_t>();
   a.idx_start = b->d_idx_start.as<uint32_t>();
   a.first_old = b->d_first_old.as<uint32_t>();
@@ -1121,10 +1278,14 @@ static int srv_init(rf_amd_engine* e) {
       v.init_rc = RF_AMD_EINVAL;
       return;
     }
-    // s_memrealtime runs at 100 MHz: idle 1 ms, lifetime 1 s (2 ms without a queue of its own)
+    // s_memrealtime runs at 100 MHz: idle 1 ms; lifetime 20 ms on a queue of its own (a bound
+    // on every wave, relaunched if lookups continue), 2 ms when it shares a queue. The masked
+    // stream synchronises with the legacy null stream, so a device-wide synchronisation or
+    // null-stream work in the process waits at most one lifetime for a busy wave.
     const char* idle = getenv("RF_AMD_SERVER_IDLE_US");
+    const char* life = getenv("RF_AMD_SERVER_LIFE_US");
     v.idle_ticks = (idle ? strtoull(idle, nullptr, 10) : 1000) * 100;
-    v.life_ticks = masked ? 100000000ull : 200000ull;
+    v.life_ticks = masked ? (life ? strtoull(life, nullptr, 10) : 20000) * 100 : 200000ull;
   });
   return v.init_rc ? fail(v.init_rc, "lookup server allocation failed") : 0;
 }

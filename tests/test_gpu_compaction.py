@@ -30,16 +30,21 @@ def chain_ids(g, v, n):
 
 
 @pytest.mark.skipif(not R.available(), reason="reference library not built")
-@pytest.mark.parametrize("entries", ["flag32", "flag32_direct", "flag32_decode", "wide64"])
+@pytest.mark.parametrize("entries", ["flag32", "flag32_k4merge", "flag32_direct", "flag32_decode", "wide64"])
 def test_chain_rounds_match_reference(entries, monkeypatch):
     """both incremental pipelines: 32-bit flagged entries (fp_size + value_size <= 31, the
     default) and 64-bit entries (forced here). With 32-bit entries a round whose geometry is
     the previous round's (rounds 3 and 5: 40K -> 60K, 80K -> 100K fingerprints) reads the old
     entries in place from the previous batch; the others decode the old image
     (flag32_decode forces the decode for every round; flag32_direct takes K4's direct
-    placement of every entry instead of its merge path)"""
+    placement of every entry instead of its merge path). Rounds that read the old entries in
+    place merge them in K6 while encoding (merge6, the default); flag32_k4merge keeps that
+    merge in K4 (RF_AMD_K6_MERGE=0)"""
     if entries == "flag32_direct":
         monkeypatch.setenv("RF_AMD_K4_DIRECT", "1")
+        monkeypatch.setenv("RF_AMD_K6_MERGE", "0")
+    if entries == "flag32_k4merge":
+        monkeypatch.setenv("RF_AMD_K6_MERGE", "0")
     if entries == "wide64":
         monkeypatch.setenv("RF_AMD_WIDE64", "1")
     if entries == "flag32_decode":
@@ -119,3 +124,59 @@ def test_bench_compaction_full_chains_golden(gpus, filters):
     assert 0 in line["sha_checked_filters"]
     assert line["num_unique_filter0"] == 4254486
     assert len(line["round_wall_ms"]) == 8
+
+
+@pytest.mark.skipif(not R.available(), reason="reference library not built")
+@pytest.mark.parametrize("k6merge", ["1", "0"])
+def test_incremental_ties_and_duplicates(k6merge, monkeypatch):
+    """an incremental add onto a filter of the same geometry (old entries read in place and,
+    by default, merged in K6 while encoding) whose new keys repeat old keys under the SAME
+    value (equal old and new entries: the old one first, both kept, src/routing_filter.c
+    :563-566) and repeat each other (new duplicates dropped, :473-482), over two rounds --
+    byte-identical to the reference's chain, num_unique included"""
+    monkeypatch.setenv("RF_AMD_K6_MERGE", k6merge)
+    cfg = E.routing_config_init(fingerprint_size=26, log_index_size=8, seed=42)
+    eng = E.Engine(0)
+    rng = np.random.default_rng(7)
+    F = 2
+    r0 = [rng.integers(0, 1 << 62, size=40000, dtype=np.uint64) for _ in range(F)]
+    # round 1: 8,000 old keys again, 6,000 fresh keys each twice (20,000 keys, same value)
+    r1 = []
+    for f in range(F):
+        fresh = rng.integers(0, 1 << 62, size=6000, dtype=np.uint64)
+        r1.append(rng.permutation(np.concatenate([r0[f][:8000], fresh, fresh])))
+    # round 2: 10,000 keys of rounds 0 and 1 again under another value
+    r2 = [rng.permutation(np.concatenate([r0[f][8000:13000], r1[f][:5000]])) for f in range(F)]
+    rounds = [(r0, 3), (r1, 3), (r2, 5)]
+    with R.Stack() as ref:
+        rprev = [None] * F
+        prev = None
+        for ids, val in rounds:
+            n = ids[0].size
+            keys = np.concatenate([K.ids_keys(ids[f]) for f in range(F)])
+            dk = torch.from_numpy(keys.reshape(-1)).to("cuda:0")
+            b = E.FilterBatch(cfg, [n] * F, [val] * F, old=[(prev, f) for f in range(F)] if prev else None,
+                              engine=eng)
+            b.build_keys(dk, 24)
+            torch.cuda.synchronize()
+            for f in range(F):
+                rf = ref.add(ref.hash_keys(keys[f * n:(f + 1) * n]), value=val, old=rprev[f])
+                want = ref.image(rf)
+                img = b.image(f)
+                assert (img.num_unique, img.num_pages) == (rf.num_unique, want.pages.size // 4096), (val, f)
+                assert (img.pages == want.pages).all(), (val, f)
+                assert (img.slots == want.slots).all(), (val, f)
+                rprev[f] = rf
+            if prev is not None:
+                prev.close()
+            prev = b
+        for ids, _ in rounds:
+            n = ids[0].size
+            keys = np.concatenate([K.ids_keys(ids[f]) for f in range(F)])
+            found = torch.empty(F * n, dtype=torch.int64, device="cuda:0")
+            prev.probe_keys_runs(torch.from_numpy(keys.reshape(-1)).to("cuda:0"), 24, [n] * F, found)
+            got = found.cpu().numpy().view(np.uint64)
+            for f in range(F):
+                assert (got[f * n:(f + 1) * n] == ref.lookup_keys(rprev[f], keys[f * n:(f + 1) * n])).all()
+        prev.close()
+    eng.close()

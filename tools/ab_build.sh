@@ -5,7 +5,7 @@ set -e
 REV=$1; TAG=$2; DEFS=$3; D=$(mktemp -d)
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p $D/splinterdb_amd/csrc $D/include
-for f in splinterdb_amd/csrc/rf_kernels.hip splinterdb_amd/csrc/rf_engine.cpp splinterdb_amd/csrc/rf_device.h splinterdb_amd/csrc/rf_plan.h include/rf_amd.h; do
+for f in splinterdb_amd/csrc/rf_kernels.hip splinterdb_amd/csrc/rf_engine.cpp splinterdb_amd/csrc/rf_device.h splinterdb_amd/csrc/rf_plan.h include/rf_amd.h include/rf_amd_diag.h; do
   if [ "$REV" = WT ]; then cp $ROOT/$f $D/$f; else git -C $ROOT show $REV:$f > $D/$f; fi
 done
 H=/opt/rocm/bin/hipcc
