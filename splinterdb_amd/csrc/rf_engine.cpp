@@ -538,10 +538,6 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
           ob->cfg.fingerprint_size == fps && ob->cfg.log_index_size == lis) {
         const uint32_t* es = ob->wide ? ob->d_sorted.as<uint32_t>() : ob->d_part.as<uint32_t>();
         p.old_direct = 1;
-        // same geometry: one new index per old index, so K6 can merge the old entries in
-        // place (merge6); RF_AMD_K6_MERGE=0 keeps the merge in K4
-        const char* m6 = getenv("RF_AMD_K6_MERGE");
-        p.merge6 = (p.npo == 1 && !(m6 && m6[0] == '0')) ? 1u : 0u;
         p.old_entries = es + op->e_first;
         p.old_idx_start = ob->d_idx_start.as<uint32_t>() + op->idx_base;
         p.old_idx_cnt = ob->d_idx_cnt.as<uint32_t>() + op->idx_base;
@@ -956,8 +952,6 @@ static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {
   a.overflow = b->d_overflow.as<uint32_t>();
   a.spill = b->d_spill.p ? b->d_spill.as<uint32_t>() : nullptr;
   a.cb_outs = b->d_cb_out.p ? b->d_cb_out.as<uint32_t>() : nullptr;
-  a.any_merge6 = 0;
-  for (const auto& p : b->plans) a.any_merge6 |= p.merge6;
   a.idx_cnt = b->d_idx_cnt.as<uint32_t>();
   a.idx_start = b->d_idx_start.as<uint32_t>();
   a.first_old = b->d_first_old.as<uint32_t>();

@@ -659,16 +659,12 @@ __device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_
 // (s_b[nn, n)), and the dedupe pass reads the two sorted runs through a merge path. Old
 // flagged values are even and new ones odd, so no old value equals a new one and the merge
 // yields exactly the order a sort of all n would (old first on equal e).
-// merge6 index marker (first_old): its entries were merged by K4b, K6 copies them
-constexpr uint32_t PREMERGED = 0xffffffffu;
-static_assert(MAX_IPC <= SORT_NT, "K4's merge6 pass takes one index per thread");
-
 template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false, bool DIRECT = false>
 __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ cb_filter,
                                                      const uint32_t* __restrict__ cb_count,
                                                      const uint32_t* __restrict__ cb_start,
-                                                     EntT* __restrict__ part,
+                                                     const EntT* __restrict__ part,
                                                      const uint32_t* __restrict__ old32,
                                                      const uint32_t* __restrict__ ob_lo,
                                                      const uint32_t* __restrict__ ob_n,
@@ -699,10 +695,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   const uint32_t cb = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's buckets share an XCD (its partition's L2)
   const uint32_t f = cb_filter[cb];
   const FilterPlan& P = plans[f];
-  // DUAL: the coarse bucket's old run is merged here -- unless the filter merges in K6
-  // (merge6): then only its new entries are sorted here
-  const uint32_t obn = (DUAL && !P.merge6) ? ob_n[cb] : 0u;
-  const uint32_t n = (DUAL && P.merge6) ? cb_count[cb] - ob_n[cb] : cb_count[cb];
+  const uint32_t n = cb_count[cb];
   const uint32_t cbl = cb - P.cb_base;
   // fused build without spill: fixed SORT_CAP regions; otherwise the scanned starts
   const uint32_t cb_rel = (spill && *spill == 0) ? cbl * CB_REGION : cb_start[cb];
@@ -733,7 +726,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     // new entries first, then the old run, loaded raw (one load per element from a selected
     // address: nothing computed on the data before the barrier below, so it does not wait
     // for the loads); old values get their flag (<< 1) when stored into s_b
-    const uint32_t nn = n - obn;
+    const uint32_t nn = n - ob_n[cb];
     const uint32_t* osrc = (P.old_direct ? P.old_entries : old32 + P.old_first) + ob_lo[cb];
 #pragma unroll
     for (int k = 0; k < PER; k++) {
@@ -752,7 +745,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   DBG_PHASE(0);
   // the entries ranked and sorted here: all of them, or (DUAL) the new ones
   uint32_t nsort = n;
-  if constexpr (DUAL) nsort = n - obn;
+  if constexpr (DUAL) nsort = n - ob_n[cb];
   // per-bin rank (bin = filter bucket within the coarse bucket)
 #pragma unroll
   for (int k = 0; k < PER; k++) {
@@ -893,70 +886,6 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
   DBG_PHASE(4);
-  if constexpr (DUAL) {
-    if (P.merge6) {
-      // merge6: s_b[0, n) holds this coarse bucket's new entries, sorted, flagged odd. Keep
-      // a new entry unless it equals its predecessor (:465-482), compact the kept ones
-      // (unflagged) back into the bucket's region of `part` for K6, and per index record the
-      // new run (first_old = its start relative to the filter's entries, has_old = the old
-      // run length K6 merges in), the merged count and the merged start (idx_cnt / idx_start:
-      // K5 lays the pages out, K6 writes the merged entries there for the next round).
-      // num_unique is counted by K6, which sees the merged order.
-      const uint32_t drun = min((uint32_t)PER, ((n + SORT_NT - 1) / SORT_NT) | 1u);
-      const uint32_t i0 = threadIdx.x * drun;
-      uint32_t km = 0, kc = 0, xv[PER];
-      {
-        uint32_t prev = (i0 > 0 && i0 <= n) ? (uint32_t)s_b[i0 - 1] : 0u;  // odd values: 0 matches none
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-          const uint32_t i = i0 + k;
-          xv[k] = 0;
-          if ((uint32_t)k < drun && i < n) {
-            xv[k] = (uint32_t)s_b[i];
-            if (i == 0 || xv[k] != prev) { km |= 1u << k; kc++; }
-            prev = xv[k];
-          }
-        }
-      }
-      uint32_t kept;
-      uint32_t pos = block_excl_scan<SORT_NT>(kc, s_tmp, &kept);  // barriers: s_b reads done
-      uint32_t* s_new = reinterpret_cast<uint32_t*>(s_b);
-#pragma unroll
-      for (int k = 0; k < PER; k++)
-        if (km >> k & 1u) s_new[pos++] = xv[k] >> 1;
-      __syncthreads();
-      // per index: its new run (binary search of the compacted list) and its old run
-      const uint32_t lcb0 = cbl << (P.bbits - lis);  // the bucket's first index in the filter
-      uint32_t nlo = 0, ncnt = 0, ocnt = 0;
-      const uint32_t li = threadIdx.x;  // ipc <= MAX_IPC = SORT_NT: one index per thread
-      if (li < ipc) {
-        auto lb = [&](uint32_t key) {
-          uint32_t lo = 0, hi = kept;
-          while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            const uint32_t x = ish >= 32 ? 0u : ((s_new[m] >> ish) & (ipc - 1));
-            if (x < key) lo = m + 1; else hi = m;
-          }
-          return lo;
-        };
-        nlo = lb(li);
-        ncnt = (li + 1 < ipc ? lb(li + 1) : kept) - nlo;
-        ocnt = P.old_idx_cnt[lcb0 + li];
-      }
-      uint32_t mtot;
-      const uint32_t mstart = block_excl_scan<SORT_NT>(li < ipc ? ncnt + ocnt : 0u, s_tmp, &mtot);
-      if (li < ipc) {
-        const uint32_t g = c.idx0 + li;
-        idx_cnt[g] = ncnt + ocnt;
-        idx_start[g] = cb_out + mstart;
-        has_old[g] = ocnt;
-        first_old[g] = cb_rel + nlo;
-      }
-      uint32_t* dst = reinterpret_cast<uint32_t*>(part) + P.e_first + cb_rel;
-      for (uint32_t i = threadIdx.x; i < kept; i += SORT_NT) dst[i] = s_new[i];  // coalesced
-      return;
-    }
-  }
   if constexpr (DUAL && DIRECT) {
     // 32-bit incremental builds: every entry's place in the merged, deduplicated order is
     // computed directly and written straight to the output -- old entries are always kept,
@@ -1348,11 +1277,9 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
     }
     const uint32_t kept = s_run;
     if constexpr (FL) {
-      // merge6 filters: these indices' entries are merged here already (PREMERGED: K6 takes
-      // them from the sorted array and does not count their num_unique again)
       for (uint32_t i = threadIdx.x; i < ipc; i += BIG_NT) {
-        first_old[c.idx0 + i] = P.merge6 ? PREMERGED : s_fo[i];
-        has_old[c.idx0 + i] = P.merge6 ? 0u : s_ho[i];
+        first_old[c.idx0 + i] = s_fo[i];
+        has_old[c.idx0 + i] = s_ho[i];
       }
     }
     uint32_t uniq, tot_uniq;
@@ -1701,41 +1628,6 @@ __device__ __forceinline__ uint64_t lds_bits64(const uint32_t* s_pg, uint32_t bi
   return (lo >> sh) | (sh ? (uint64_t)s_pg[w + 2] << (64 - sh) : 0ull);
 }
 
-// merge6 (K6 merges the old entries in place with K4's new ones): an old entry read from the
-// old batch, its value bits re-widened to this filter's value size (src/routing_filter.c:536-543)
-__device__ __forceinline__ uint32_t rewiden(const FilterPlan& P, uint32_t eo) {
-  return ((eo >> P.old_vs) << P.vs) | (eo & ((1u << P.old_vs) - 1u));
-}
-
-// merge6, pages that take an image fallback (assemble_atomic): the merged entries of the
-// page's blocks written to the sorted array first, one thread per block (src/routing_filter.c
-// :546-597: old first on equal entries); returns this thread's num_unique count
-__device__ uint32_t merge6_materialize(const FilterPlan& P, uint32_t b0, uint32_t b1,
-                                       const uint32_t* __restrict__ idx_cnt, const uint32_t* __restrict__ idx_start,
-                                       const uint32_t* __restrict__ first_old, const uint32_t* __restrict__ has_old,
-                                       const uint32_t* __restrict__ part_new, uint32_t* __restrict__ sorted32) {
-  uint32_t uniq = 0;
-  const uint32_t FPNONE = 0xffffffffu >> P.vs;
-  for (uint32_t b = b0 + threadIdx.x; b < b1; b += ASM_NT) {
-    const uint32_t g = P.idx_base + b, ns = first_old[g];
-    if (ns == PREMERGED) continue;  // merged (and counted) by K4b
-    const uint32_t oc = has_old[g], nc = idx_cnt[g] - oc;
-    const uint32_t* o = P.old_entries + P.old_idx_start[b];
-    const uint32_t* nw = part_new + P.e_first + ns;
-    uint32_t* d = sorted32 + P.e_first + idx_start[g];
-    uint32_t io = 0, jn = 0, k = 0, pfp = FPNONE;
-    while (io < oc || jn < nc) {
-      uint32_t e;
-      if (jn == nc || (io < oc && rewiden(P, o[io]) <= nw[jn])) e = rewiden(P, o[io++]);
-      else e = nw[jn++];
-      d[k++] = e;
-      uniq += (e >> P.vs) != pfp ? 1u : 0u;
-      pfp = e >> P.vs;
-    }
-  }
-  return uniq;
-}
-
 // One workgroup per page. (A) block metadata in LDS. (B) word-parallel fill of the LDS page
 // image: header counts, 0xFF encodings, zeros -- plain stores. (C) entry runs: a thread
 // takes ASM_RUN consecutive entries of the page, accumulates their encoding-clear bits
@@ -1744,36 +1636,18 @@ __device__ uint32_t merge6_materialize(const FilterPlan& P, uint32_t b0, uint32_
 // with one atomic: adjacent lanes share at most a window edge. (D) 16-byte stores.
 // Measured before: entry-parallel single-bit atomics (~19 LDS conflict cycles per LDS
 // instruction), and a byte-serial gather per 16-byte chunk (3.6x slower again).
-// MERGE (batches with merge6 filters): a merge6 filter's pages take the old entries of each
-// block in place from the old batch and its new entries from K4 (part_new at first_old[g],
-// has_old[g] old ones), and merge them while encoding: phase C runs over 16 OLD entries of a
-// block at a time, each emitting its old entries and the new entries whose place falls among
-// them (the new entries < old[i0 - 1] belong to earlier runs: a binary search; old first on
-// equal entries), and writes the merged entries to the sorted array for the next incremental
-// round; blocks without old entries run over their new entries. num_unique is counted here.
-// The page's new entries are staged in LDS (up to ASM_NCAP; beyond, read in place).
-constexpr uint32_t ASM_NCAP = 2048;
-template <bool MERGE>
 __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) void k_assemble(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ pg_filter,
                                                      const uint32_t* __restrict__ idx_cnt,
                                                      const uint32_t* __restrict__ idx_start,
-                                                     uint32_t* __restrict__ sorted32,
+                                                     const uint32_t* __restrict__ sorted32,
                                                      const uint64_t* __restrict__ slots,
                                                      const uint32_t* __restrict__ page_first,
-                                                     FilterOut* __restrict__ outs,
+                                                     const FilterOut* __restrict__ outs,
                                                      uint8_t* __restrict__ pages, uint4* __restrict__ lines,
                                                      uint32_t* __restrict__ pg_noline,
-                                                     uint32_t lis, uint32_t page_size,
-                                                     const uint32_t* __restrict__ first_old,
-                                                     const uint32_t* __restrict__ has_old,
-                                                     const uint32_t* __restrict__ part_new) {
+                                                     uint32_t lis, uint32_t page_size) {
   __shared__ __attribute__((aligned(16))) uint32_t s_pg[MAX_PAGE / 4 + 4];
-  // merge6: per block, old run length / its start in the old entries / new run start (part or
-  // PREMERGED), the first merge run of each block, and the page's staged new entries
-  __shared__ uint32_t s_oc[MERGE ? ASM_MAXB : 1], s_os[MERGE ? ASM_MAXB : 1], s_ns[MERGE ? ASM_MAXB : 1];
-  __shared__ uint32_t s_rst[MERGE ? ASM_MAXB + 1 : 1], s_nst[MERGE ? ASM_MAXB + 1 : 1];
-  __shared__ uint32_t s_new[MERGE ? ASM_NCAP : 1];
   __shared__ uint32_t s_wpre[ASM_MAXB];
   __shared__ uint32_t s_off[ASM_MAXB + 1];
   __shared__ uint32_t s_c[ASM_MAXB];
@@ -1782,8 +1656,7 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   // s_rblk (block of each run's first entry, phases A-C) and s_gs (per block: bit after each
   // line group's last terminator, phase E) share one array: 2 KiB less LDS per page lets
   // 14 pages, not 13, run on a CU
-  constexpr uint32_t RUNS_MAX = ASM_MAXE / ASM_RUN + (MERGE ? ASM_MAXB : 0u);  // merge6: a partial run per block
-  __shared__ uint16_t s_rg[RUNS_MAX > ASM_GT ? RUNS_MAX : ASM_GT];
+  __shared__ uint16_t s_rg[ASM_MAXE / ASM_RUN > ASM_GT ? ASM_MAXE / ASM_RUN : ASM_GT];
   uint16_t* const s_rblk = s_rg;
   uint16_t* const s_gs = s_rg;
   __shared__ uint32_t s_wm[MAX_PAGE / 16];  // byte w: a block j >= 1 starts in word w
@@ -1799,16 +1672,7 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   const uint32_t* pf = page_first + P.pf_base;
   const uint32_t b0 = pf[p], b1 = pf[p + 1], nb = b1 - b0;
   uint4* dst = reinterpret_cast<uint4*>(pages + (uint64_t)slot * page_size);
-  const bool m6 = MERGE && P.merge6;
   if (nb > ASM_MAXB) {  // (never with lines_asm: the host bounds blocks per page for it)
-    if (m6) {
-      const uint32_t u = merge6_materialize(P, b0, b1, idx_cnt, idx_start, first_old, has_old, part_new, sorted32);
-      uint32_t tu;
-      block_excl_scan<ASM_NT>(u, s_tmp, &tu);
-      if (threadIdx.x == 0 && tu) atomicAdd(&outs[f].num_unique, tu);
-      __threadfence_block();
-      __syncthreads();
-    }
     assemble_atomic(P, p, slot, b0, b1, idx_cnt, idx_start, sorted32, slots, pages, lis, page_size, s_pg);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < page_size / 16; i += ASM_NT) dst[i] = reinterpret_cast<const uint4*>(s_pg)[i];
@@ -1854,80 +1718,14 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   DBG_PHASE_K(3, 0);
   if (ne > ASM_MAXE) {  // uniform (scan total)
     __syncthreads();
-    if (m6) {
-      const uint32_t u = merge6_materialize(P, b0, b1, idx_cnt, idx_start, first_old, has_old, part_new, sorted32);
-      uint32_t tu;
-      block_excl_scan<ASM_NT>(u, s_tmp, &tu);
-      if (threadIdx.x == 0 && tu) atomicAdd(&outs[f].num_unique, tu);
-      __threadfence_block();
-      __syncthreads();
-    }
     assemble_atomic(P, p, slot, b0, b1, idx_cnt, idx_start, sorted32, slots, pages, lis, page_size, s_pg);
   } else {
   __syncthreads();
-  // merge6 pages: per block its old run (length, start in the old entries), its new run (start
-  // in part, or PREMERGED: the block's merged entries are in the sorted array already) and its
-  // merge runs -- ceil(old / ASM_RUN) runs over the old entries (a PREMERGED block: over its
-  // entries; a block without old entries: one run over its new ones); one packed scan (runs
-  // << 16 | new entries: both < 2^16 with ne <= ASM_MAXE) places the runs and the staged new
-  // entries
-  uint32_t m6runs = 0;
-  bool staged = false;
-  if (m6) {
-    uint32_t rq[2], nq[2], packed = 0;
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const uint32_t j = threadIdx.x * 2 + q;
-      rq[q] = nq[q] = 0;
-      if (j < nb) {
-        const uint32_t g = P.idx_base + b0 + j, ns = first_old[g], c = cj[q];
-        const uint32_t oc = ns == PREMERGED ? c : has_old[g];
-        s_ns[j] = ns;
-        s_oc[j] = oc;
-        s_os[j] = ns == PREMERGED ? 0u : P.old_idx_start[b0 + j];
-        rq[q] = oc ? (oc + ASM_RUN - 1) / ASM_RUN : (c ? 1u : 0u);
-        nq[q] = c - oc;
-      }
-      packed += rq[q] << 16 | nq[q];
-    }
-    uint32_t ptot;
-    uint32_t ex = block_excl_scan<ASM_NT>(packed, s_tmp, &ptot);
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const uint32_t j = threadIdx.x * 2 + q;
-      if (j < nb) {
-        s_rst[j] = ex >> 16;
-        s_nst[j] = ex & 0xffffu;
-      }
-      ex += rq[q] << 16 | nq[q];
-    }
-    if (threadIdx.x == 0) {
-      s_rst[nb] = ptot >> 16;
-      s_nst[nb] = ptot & 0xffffu;
-    }
-    m6runs = ptot >> 16;
-    staged = (ptot & 0xffffu) <= ASM_NCAP;
-    __syncthreads();
-    if (staged) {  // the page's new entries into LDS (binary searches and merges read them there)
-      const uint32_t nnew = ptot & 0xffffu;
-      for (uint32_t i = threadIdx.x; i < nnew; i += ASM_NT) {
-        uint32_t lo = 0, hi = nb;  // block j: s_nst[j] <= i < s_nst[j + 1]
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_nst[mid] <= i) lo = mid; else hi = mid;
-        }
-        s_new[i] = part_new[P.e_first + s_ns[lo] + (i - s_nst[lo])];
-      }
-    }
-  }
   // run table: block of each run's first entry; word marks of the block starts
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const uint32_t j = threadIdx.x * 2 + q;
-    if (m6) {
-      if (j < nb)
-        for (uint32_t r = s_rst[j]; r < s_rst[j + 1]; r++) s_rblk[r] = (uint16_t)j;
-    } else if (j < nb && s_c[j]) {
+    if (j < nb && s_c[j]) {
       const uint32_t r0 = (s_est[j] + ASM_RUN - 1) / ASM_RUN, r1 = (s_est[j + 1] + ASM_RUN - 1) / ASM_RUN;
       for (uint32_t r = r0; r < r1; r++) s_rblk[r] = (uint16_t)j;
     }
@@ -1983,7 +1781,7 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   };
   // the first run's loads are issued before the fill, so they land while it runs
   uint32_t ev0[ASM_RUN];
-  if (!m6 && threadIdx.x < nruns) load_run(threadIdx.x, ev0);
+  if (threadIdx.x < nruns) load_run(threadIdx.x, ev0);
   // (B) fill: thread t builds its quads' words (16 bytes each) and stores each quad at once
   uint32_t jw = jw0;
 #pragma unroll
@@ -2016,107 +1814,6 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   DBG_PHASE_K(3, 1);
   // (C) entry runs
   const uint32_t rmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
-  if (m6) {
-    // merge6 (src/routing_filter.c:546-597): run rr of block j takes old entries [i0, i1) =
-    // [16 rr, 16 rr + 16) and the new entries placed among them -- those from #new < old[i0]
-    // (0 in the block's first run) to #new < old[i1] (all of them in its last run): a new
-    // entry goes before an old one only if smaller (old first on equal entries). Entry k of
-    // the block is encoded as in the plain path, written to the sorted array (the next
-    // incremental round's old entries) and counted for num_unique (:572-574: a fingerprint
-    // unlike its predecessor's in the index; the first entry against UINT32_MAX >> vs).
-    const uint32_t FPNONE = 0xffffffffu >> P.vs;
-    const uint32_t ovs = P.old_vs, ovmask = (1u << P.old_vs) - 1u;
-    uint32_t* mb = sorted32 + P.e_first;
-    uint32_t uniq = 0;
-    for (uint32_t r = threadIdx.x; r < m6runs; r += ASM_NT) {
-      const uint32_t j = s_rblk[r], rr = r - s_rst[j];
-      const uint32_t c = s_c[j], ns = s_ns[j], oc = s_oc[j], nc = c - oc, dst0 = s_src[j];
-      const bool pre = ns == PREMERGED;
-      const uint32_t* O = pre ? mb + dst0 : P.old_entries + s_os[j];
-      const uint32_t* N = staged ? s_new + s_nst[j] : part_new + P.e_first + (pre ? 0u : ns);
-      auto rw = [&](uint32_t x) { return pre ? x : (((x >> ovs) << P.vs) | (x & ovmask)); };
-      const uint32_t i0 = rr * ASM_RUN, i1 = min(i0 + ASM_RUN, oc);
-      uint32_t ov[ASM_RUN];
-#pragma unroll
-      for (uint32_t i = 0; i < ASM_RUN; i++) ov[i] = i0 + i < i1 ? O[i0 + i] : 0u;
-      const uint32_t onext = i1 < oc ? rw(O[i1]) : 0u;
-      const uint32_t oprev = i0 > 0 ? rw(O[i0 - 1]) : 0u;
-#pragma unroll
-      for (uint32_t i = 0; i < ASM_RUN; i++) ov[i] = rw(ov[i]);
-      auto lbN = [&](uint32_t v) {  // new entries < v
-        uint32_t lo = 0, hi = nc;
-        while (lo < hi) {
-          const uint32_t m = (lo + hi) >> 1;
-          if (N[m] < v) lo = m + 1; else hi = m;
-        }
-        return lo;
-      };
-      uint32_t jn = (rr == 0 || i0 >= oc) ? 0u : lbN(ov[0]);
-      const uint32_t nhi = i1 >= oc ? nc : lbN(onext);
-      uint32_t k = i0 + jn;  // the block position of the run's first entry
-      uint32_t pfp = FPNONE;
-      if (k > 0) {
-        uint32_t pv = i0 > 0 ? oprev : 0u;
-        if (jn > 0) pv = max(pv, N[jn - 1]);
-        pfp = pv >> P.vs;
-      }
-      const uint32_t ebit = (s_off[j] + 2) * 8;
-      const uint32_t rbit = (s_off[j] + 2 + (c + IS - 1) / 8 + 4) * 8;
-      uint32_t eW = 0xffffffffu, rW = 0xffffffffu;
-      uint64_t eacc = 0, racc = 0;
-      auto flush_e = [&]() {
-        if (eW != 0xffffffffu) {
-          if ((uint32_t)eacc) atomicAnd(&s_pg[2 * eW], ~(uint32_t)eacc);
-          if ((uint32_t)(eacc >> 32)) atomicAnd(&s_pg[2 * eW + 1], ~(uint32_t)(eacc >> 32));
-        }
-        eacc = 0;
-      };
-      auto flush_r = [&]() {
-        if (rW != 0xffffffffu) {
-          if ((uint32_t)racc) atomicOr(&s_pg[2 * rW], (uint32_t)racc);
-          if ((uint32_t)(racc >> 32)) atomicOr(&s_pg[2 * rW + 1], (uint32_t)(racc >> 32));
-        }
-        racc = 0;
-      };
-      auto emit = [&](uint32_t e) {
-        const uint32_t hb = ebit + k + (rvs >= 32 ? 0u : ((e >> rvs) & (IS - 1)));
-        const uint32_t hw = hb >> 6;
-        if (hw != eW) { flush_e(); eW = hw; }
-        eacc |= 1ull << (hb & 63);
-        if (rvs) {
-          const uint32_t rb = rbit + k * rvs;
-          const uint32_t rwd = rb >> 6, sh = rb & 63;
-          if (rwd != rW) { flush_r(); rW = rwd; }
-          const uint64_t v = e & rmask;
-          racc |= v << sh;
-          if (sh + rvs > 64) {
-            flush_r();
-            rW = rwd + 1;
-            racc = v >> (64 - sh);
-          }
-        }
-        if (!pre) {
-          mb[dst0 + k] = e;
-          uniq += (e >> P.vs) != pfp ? 1u : 0u;
-          pfp = e >> P.vs;
-        }
-        k++;
-      };
-#pragma unroll
-      for (uint32_t i = 0; i < ASM_RUN; i++) {
-        if (i0 + i < i1) {
-          while (jn < nhi && N[jn] < ov[i]) emit(N[jn++]);
-          emit(ov[i]);
-        }
-      }
-      while (jn < nhi) emit(N[jn++]);
-      flush_e();
-      flush_r();
-    }
-    uint32_t tu;
-    block_excl_scan<ASM_NT>(uniq, s_tmp, &tu);
-    if (threadIdx.x == 0 && tu) atomicAdd(&outs[f].num_unique, tu);
-  } else
   for (uint32_t r = threadIdx.x; r < nruns; r += ASM_NT) {
     const uint32_t q0 = r * ASM_RUN, q1 = min(q0 + ASM_RUN, ne);
     const uint32_t jr = s_rblk[r];
@@ -3757,16 +3454,9 @@ extern "C" int rf_launch_build(const LaunchArgs* pa) {
                      a.idx_start, a.sorted32, a.first_old, a.has_old, a.pplans_mut, a.slots, a.page_first, a.outs, a.lis, a.page_size);
   CHECK_LAUNCH();
   REC(EV_B_LAYOUT);
-  // batches with merge6 filters: K6 merges their old entries in place (k_assemble<true>)
-  if (a.any_merge6)
-    hipLaunchKernelGGL(k_assemble<true>, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.pg_filter, a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages,
-                       a.lines, a.pg_noline, a.lis, a.page_size, a.first_old, a.has_old,
-                       (const uint32_t*)a.part);
-  else
-    hipLaunchKernelGGL(k_assemble<false>, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.pg_filter, a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages,
-                       a.lines, a.pg_noline, a.lis, a.page_size, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(k_assemble, dim3(a.num_page_slots), dim3(ASM_NT), 0, (hipStream_t)a.stream, a.plans, a.pg_filter,
+                     a.idx_cnt, a.idx_start, a.sorted32, a.slots, a.page_first, a.outs, a.pages, a.lines,
+                     a.pg_noline, a.lis, a.page_size);
   CHECK_LAUNCH();
   if (a.plines_needed)
     if (int rc = launch_plines_list(a)) return rc;

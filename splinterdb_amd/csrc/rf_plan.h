@@ -69,10 +69,6 @@ struct FilterPlan {
   // sorted entry array (old_entries, old_idx_start / old_idx_cnt relative to it) -- no
   // decode of its image. Value bits are re-widened (old_vs -> vs) as K4 loads them.
   uint32_t old_direct;
-  // old_direct with one new index per old index (npo == 1): the merge of old and new entries
-  // happens in K6 (k_assemble<true>) straight from the old entries in place; K4 sorts and
-  // deduplicates only the new entries (RF_AMD_K6_MERGE=0 keeps the K4 merge)
-  uint32_t merge6;
   const uint32_t* old_entries;
   const uint32_t* old_idx_start;
   const uint32_t* old_idx_cnt;
@@ -195,7 +191,6 @@ struct LaunchArgs {
   uint32_t* page_first;
   uint32_t* pg_noline;      // [0] = count, then the page slots whose probe lines K6 left to k_plines_list
   uint32_t* cb_outs;        // 32-bit incremental builds: per coarse bucket, where K4 writes its sorted entries
-  uint32_t any_merge6;       // some filter of the batch merges its old entries in K6 (merge6)
   const uint32_t* pg_filter;
   uint32_t num_page_slots;
   uint8_t* pages;
