@@ -330,6 +330,22 @@ registry_find_pin(const cache *cc, uint64 addr, uint32 *f)
    return sb;
 }
 
+/* n pins dropped under one lock (the async completion path: one acquisition per reap, not
+ * per state) */
+static void
+registry_unpin_many(shim_batch *const *sb, uint64 n)
+{
+   release_list rl = {NULL, 0, 0};
+   pthread_mutex_lock(&g_registry_mu);
+   for (uint64 i = 0; i < n; i++) {
+      if (sb[i]) {
+         shim_batch_drop_locked(sb[i], 0, &rl);
+      }
+   }
+   pthread_mutex_unlock(&g_registry_mu);
+   release_run(&rl);
+}
+
 static void
 registry_unpin(shim_batch *sb)
 {
@@ -1357,17 +1373,22 @@ lookup_many(cache *const          *ccs,
    free(grc);
 }
 
-/* ---- async: states answered by the engine's lookup server ---------------------------------- */
+/* ---- async: states answered by the engine's lookup server, or in batches ------------------- */
 /*
- * routing_filter_lookup_async hashes the key, pins the filter's device batch and submits ONE
- * request to the engine's lookup server (rf_amd_lookup_submit: a ring in pinned host memory
- * that a persistent GPU wave polls -- no kernel launch, no batching delay), then returns
- * ASYNC_STATUS_RUNNING without touching the state again (async.h:115-125). A completion
- * thread registered with the platform reaps answered requests in submission order
- * (rf_amd_lookup_reap) and, for each state, stores the result, marks it done and fires its
- * callback; the next call returns DONE. A polling owner's re-call reaps in its own thread.
- * The state's pin (its batch stays resident until answered) is kept in its filter_page
- * local, which the shim's coroutine never uses otherwise.
+ * routing_filter_lookup_async hashes the key and, while fewer than AQ_SERVER_MAX states wait
+ * on the engine's lookup server, pins the filter's device batch and submits ONE request to it
+ * (rf_amd_lookup_submit: a ring in pinned host memory that a persistent GPU wave polls -- no
+ * kernel launch, no batching delay: the latency path of callers that keep a few lookups in
+ * flight). Beyond that the state goes onto a lock-free stack instead (one compare-and-swap):
+ * the batch thread takes the whole stack whenever it is free and answers it with ONE launch
+ * over every filter the states name (lookup_many) -- a burst of thousands of states costs one
+ * push each instead of one ring request each. Either way the call returns
+ * ASYNC_STATUS_RUNNING without touching the state again (async.h:115-125); a completion
+ * thread registered with the platform stores each result, marks the state done and fires its
+ * callback; the next call returns DONE. A polling owner's re-call completes what it can in
+ * its own thread. The server state's pin (its batch stays resident until answered) is kept
+ * in its filter_page local, a queued state's next pointer in index_page: locals the shim's
+ * coroutine never uses otherwise.
  */
 static char g_queued_marker;
 #define ASYNC_STATE_QUEUED ((async_state)&g_queued_marker)
@@ -1384,6 +1405,131 @@ static uint64          g_async_batches, g_async_probes, g_async_submit_ns, g_asy
 
 #define AQ_PIN(st) (*(shim_batch **)&(st)->filter_page)
 
+#define AQ_SERVER_MAX 64 /* server requests outstanding beyond which states are batched */
+static rf_state *g_bq_head;     /* the stack of batched states (atomic) */
+static uint64    g_bq_count;    /* states on it (atomic) */
+static uint64    g_bq_pending;  /* batched states not yet completed (atomic) */
+static int       g_bq_sleeping; /* batch threads waiting on g_bq_cv (atomic) */
+static pthread_mutex_t g_bq_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t  g_bq_cv = PTHREAD_COND_INITIALIZER;
+/* launches and states of the batch path, ns in lookup_many (host work + GPU round trip) */
+static uint64 g_bq_batches, g_bq_probes, g_bq_ns;
+#define AQ_NEXT(st) (*(rf_state **)&(st)->index_page)
+
+/* probe and complete the n states of a taken stack (their filters in one launch); each
+ * state's callback fires after it is marked done */
+static void
+complete_states(rf_state *list, uint64 n)
+{
+   if (n == 0) {
+      return;
+   }
+   rf_state             **q    = malloc(sizeof(*q) * n);
+   cache               **ccs   = malloc(sizeof(*ccs) * n);
+   const routing_config **cfgs = malloc(sizeof(*cfgs) * n);
+   const routing_filter **fl   = malloc(sizeof(*fl) * n);
+   uint32               *h     = malloc(sizeof(uint32) * n);
+   uint64               *found = malloc(sizeof(uint64) * n);
+   platform_status      *rc    = malloc(sizeof(*rc) * n);
+   platform_assert(q && ccs && cfgs && fl && h && found && rc);
+   uint64 m = 0;
+   for (rf_state *st = list; st && m < n; st = AQ_NEXT(st)) {
+      q[m]    = st;
+      ccs[m]  = st->cc;
+      cfgs[m] = st->cfg;
+      fl[m]   = &st->filter;
+      h[m]    = st->fp; /* the full 32-bit hash, stored when queued */
+      m++;
+   }
+   const uint64 t0 = now_ns();
+   lookup_many(ccs, cfgs, fl, h, m, found, rc);
+   __atomic_fetch_add(&g_bq_ns, now_ns() - t0, __ATOMIC_RELAXED);
+   for (uint64 i = 0; i < m; i++) {
+      rf_state         *st  = q[i];
+      async_callback_fn cb  = st->callback;
+      void             *arg = st->callback_arg;
+      *st->found_values     = found[i];
+      st->__async_result    = rc[i];
+      /* from here the owner may resume (and reuse) the state: it is not touched again */
+      __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
+      __atomic_sub_fetch(&g_bq_pending, 1, __ATOMIC_RELEASE);
+      if (cb) {
+         cb(arg);
+      }
+   }
+   __atomic_fetch_add(&g_bq_batches, 1, __ATOMIC_RELAXED);
+   __atomic_fetch_add(&g_bq_probes, m, __ATOMIC_RELAXED);
+   free(q);
+   free(ccs);
+   free(cfgs);
+   free(fl);
+   free(h);
+   free(found);
+   free(rc);
+}
+
+/* takes every batched state: the stack's head and how many states it holds */
+static rf_state *
+bq_take(uint64 *n)
+{
+   rf_state *list = __atomic_exchange_n(&g_bq_head, NULL, __ATOMIC_ACQUIRE);
+   uint64    c    = 0;
+   for (rf_state *st = list; st; st = AQ_NEXT(st)) {
+      c++;
+   }
+   __atomic_fetch_sub(&g_bq_count, c, __ATOMIC_RELAXED);
+   *n = c;
+   return list;
+}
+
+static uint64
+bq_complete(void)
+{
+   uint64    n;
+   rf_state *list = bq_take(&n);
+   complete_states(list, n);
+   return n;
+}
+
+/* the batch thread: takes the whole stack whenever it is free -- what arrived during one GPU
+ * round trip goes out in the next; a burst of submissions settles first (no arrival for a
+ * microsecond, at most 4) */
+static void *
+batch_main(void *arg)
+{
+   (void)arg;
+   platform_ensure_thread_registered(); /* callbacks and cache_get (imports) run here */
+   for (;;) {
+      if (!__atomic_load_n(&g_bq_head, __ATOMIC_ACQUIRE)) {
+         const uint64 t0 = now_ns();
+         while (!__atomic_load_n(&g_bq_head, __ATOMIC_ACQUIRE) && now_ns() - t0 < 30000) {
+            __builtin_ia32_pause();
+         }
+         pthread_mutex_lock(&g_bq_mu);
+         __atomic_add_fetch(&g_bq_sleeping, 1, __ATOMIC_SEQ_CST);
+         while (!__atomic_load_n(&g_bq_head, __ATOMIC_SEQ_CST)) {
+            pthread_cond_wait(&g_bq_cv, &g_bq_mu);
+         }
+         __atomic_sub_fetch(&g_bq_sleeping, 1, __ATOMIC_SEQ_CST);
+         pthread_mutex_unlock(&g_bq_mu);
+      }
+      uint64       c0 = __atomic_load_n(&g_bq_count, __ATOMIC_RELAXED);
+      const uint64 t0 = now_ns();
+      uint64       tc = t0, t = t0;
+      while (t - t0 < 4000 && t - tc < 1000) {
+         __builtin_ia32_pause();
+         t               = now_ns();
+         const uint64 c1 = __atomic_load_n(&g_bq_count, __ATOMIC_RELAXED);
+         if (c1 != c0) {
+            c0 = c1;
+            tc = t;
+         }
+      }
+      bq_complete();
+   }
+   return NULL;
+}
+
 /* take what the server has answered and complete those states; returns how many */
 static uint64
 async_reap_complete(void)
@@ -1397,21 +1543,22 @@ async_reap_complete(void)
       return 0;
    }
    const uint64 t1 = now_ns();
+   shim_batch  *pins[REAP];
    for (uint64 i = 0; i < n; i++) {
       rf_state         *st  = tags[i];
       async_callback_fn cb  = st->callback;
       void             *arg = st->callback_arg;
-      shim_batch       *sb  = AQ_PIN(st);
+      pins[i]               = AQ_PIN(st);
       *st->found_values     = found[i];
       st->__async_result    = STATUS_OK;
       /* from here the owner may resume (and reuse) the state: it is not touched again */
       __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
-      registry_unpin(sb);
       __atomic_sub_fetch(&g_aq_outstanding, 1, __ATOMIC_RELAXED);
       if (cb) {
          cb(arg);
       }
    }
+   registry_unpin_many(pins, n); /* the batches stay pinned until their answers are stored */
    __atomic_fetch_add(&g_async_reap_ns, t1 - t0, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_cb_ns, now_ns() - t1, __ATOMIC_RELAXED);
    __atomic_fetch_add(&g_async_batches, 1, __ATOMIC_RELAXED);
@@ -1451,6 +1598,9 @@ aq_init(void)
    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
    pthread_t t;
    platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
+   /* two batch threads: a batch goes out while the previous one is on the GPU */
+   platform_assert(pthread_create(&t, &at, batch_main, NULL) == 0);
+   platform_assert(pthread_create(&t, &at, batch_main, NULL) == 0);
    pthread_attr_destroy(&at);
 }
 
@@ -1460,8 +1610,9 @@ void
 routing_filter_amd_flush(void)
 {
    pthread_once(&g_aq_once, aq_init);
-   while (__atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE)) {
-      if (!async_reap_complete()) {
+   /* until every submitted state is done, including batches a completion thread holds */
+   while (__atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE) || __atomic_load_n(&g_bq_pending, __ATOMIC_ACQUIRE)) {
+      if (!bq_complete() && !async_reap_complete()) {
          __builtin_ia32_pause();
       }
    }
@@ -1470,19 +1621,19 @@ routing_filter_amd_flush(void)
 void
 routing_filter_amd_async_stats(uint64 *batches, uint64 *probes)
 {
-   *batches = __atomic_load_n(&g_async_batches, __ATOMIC_RELAXED);
-   *probes  = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED);
+   *batches = __atomic_load_n(&g_async_batches, __ATOMIC_RELAXED) + __atomic_load_n(&g_bq_batches, __ATOMIC_RELAXED);
+   *probes  = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED) + __atomic_load_n(&g_bq_probes, __ATOMIC_RELAXED);
 }
 
-/* out[0..5]: reaps that completed states, states completed, then ns totals: submitting
- * (hash, pin, ring write), -, reaping, callbacks */
+/* out[0..5]: reaps that completed server states, server states completed, then ns totals:
+ * submitting (hash, pin, ring write), the batch path's lookup_many, reaping, callbacks */
 void
 routing_filter_amd_async_breakdown(uint64 *out)
 {
    out[0] = __atomic_load_n(&g_async_batches, __ATOMIC_RELAXED);
    out[1] = __atomic_load_n(&g_async_probes, __ATOMIC_RELAXED);
    out[2] = __atomic_load_n(&g_async_submit_ns, __ATOMIC_RELAXED);
-   out[3] = 0;
+   out[3] = __atomic_load_n(&g_bq_ns, __ATOMIC_RELAXED);
    out[4] = __atomic_load_n(&g_async_reap_ns, __ATOMIC_RELAXED);
    out[5] = __atomic_load_n(&g_async_cb_ns, __ATOMIC_RELAXED);
 }
@@ -1490,7 +1641,7 @@ routing_filter_amd_async_breakdown(uint64 *out)
 uint64
 routing_filter_amd_async_probe_ns(void)
 {
-   return __atomic_load_n(&g_async_reap_ns, __ATOMIC_RELAXED);
+   return __atomic_load_n(&g_async_reap_ns, __ATOMIC_RELAXED) + __atomic_load_n(&g_bq_ns, __ATOMIC_RELAXED);
 }
 
 async_status
@@ -1501,10 +1652,13 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
       return ASYNC_STATUS_DONE;
    }
    if (at == ASYNC_STATE_QUEUED) {
-      /* a polling owner: reap in this thread (this state among them, unless the completion
-         thread already holds it). RUNNING either way -- the state's callback may have
-         fired; the next call returns DONE */
+      /* a polling owner: complete what is answered or batched now, in this thread (this
+         state among them, unless a completion thread already holds it). RUNNING either way
+         -- the state's callback may have fired; the next call returns DONE */
       async_reap_complete();
+      if (__atomic_load_n(&g_bq_head, __ATOMIC_RELAXED)) {
+         bq_complete();
+      }
       return ASYNC_STATUS_RUNNING;
    }
    /* ASYNC_STATE_INIT (:898-905) */
@@ -1517,6 +1671,23 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    pthread_once(&g_aq_once, aq_init);
    const uint64 t0 = now_ns();
    state->fp       = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
+   if (__atomic_load_n(&g_aq_outstanding, __ATOMIC_RELAXED) >= AQ_SERVER_MAX) {
+      /* a burst: onto the batch stack (the state may complete at once on another thread; it
+         is not read again here) */
+      state->__async_state_stack[0] = ASYNC_STATE_QUEUED;
+      __atomic_add_fetch(&g_bq_pending, 1, __ATOMIC_SEQ_CST);
+      rf_state *old                 = __atomic_load_n(&g_bq_head, __ATOMIC_RELAXED);
+      do {
+         AQ_NEXT(state) = old;
+      } while (!__atomic_compare_exchange_n(&g_bq_head, &old, state, 1, __ATOMIC_SEQ_CST, __ATOMIC_RELAXED));
+      __atomic_add_fetch(&g_bq_count, 1, __ATOMIC_RELAXED);
+      if (old == NULL && __atomic_load_n(&g_bq_sleeping, __ATOMIC_SEQ_CST)) {
+         pthread_mutex_lock(&g_bq_mu);
+         pthread_cond_signal(&g_bq_cv);
+         pthread_mutex_unlock(&g_bq_mu);
+      }
+      return ASYNC_STATUS_RUNNING;
+   }
    shim_batch     *sb;
    uint32          fi;
    platform_status rc = resident_pin(state->cc, state->cfg, &state->filter, &sb, &fi);

@@ -659,7 +659,7 @@ __device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_
 // (s_b[nn, n)), and the dedupe pass reads the two sorted runs through a merge path. Old
 // flagged values are even and new ones odd, so no old value equals a new one and the merge
 // yields exactly the order a sort of all n would (old first on equal e).
-template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false, bool DIRECT = false>
+template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ cb_filter,
                                                      const uint32_t* __restrict__ cb_count,
@@ -886,152 +886,6 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
   DBG_PHASE(4);
-  if constexpr (DUAL && DIRECT) {
-    // 32-bit incremental builds: every entry's place in the merged, deduplicated order is
-    // computed directly and written straight to the output -- old entries are always kept,
-    // a new entry is dropped iff it equals the previous new one (src/routing_filter.c:465-494
-    // dedupes the new run before the merge, :546-597 merges old first on ties). A = the sorted
-    // new run s_b[0, nsort) (flagged odd), B = the old run s_b[nsort, n) (flagged even): a
-    // flagged comparison orders an old entry before a new one of equal e.
-    static_assert(sizeof(EntT) == 4, "DUAL entries are 32-bit");
-    const uint32_t na = nsort, nb = n - nsort;
-    uint32_t* Ak = reinterpret_cast<uint32_t*>(s_b);  // A, then its kept entries compacted
-    const uint32_t* B = Ak + nsort;
-    // (1) the new run: thread t owns A[t*ca, t*ca + ca); a new entry is kept unless it equals
-    // its predecessor in A
-    const uint32_t ca = (na + SORT_NT - 1) / SORT_NT;  // <= PER
-    const uint32_t a0 = threadIdx.x * ca;
-    uint32_t x[PER];
-    uint32_t kmask = 0, kc = 0;
-    {
-      uint32_t pa = (a0 > 0 && a0 <= na) ? Ak[a0 - 1] : 0u;  // flagged new values are odd: 0 matches none
-#pragma unroll
-      for (int k = 0; k < PER; k++) {
-        const uint32_t a = a0 + k;
-        x[k] = 0;
-        if ((uint32_t)k < ca && a < na) {
-          x[k] = Ak[a];
-          if (a == 0 || x[k] != pa) {
-            kmask |= 1u << k;
-            kc++;
-          }
-          pa = x[k];
-        }
-      }
-    }
-    uint32_t nkept;
-    const uint32_t kbase = block_excl_scan<SORT_NT>(kc, s_tmp, &nkept);  // barriers: A is read
-    {
-      uint32_t r = kbase;
-#pragma unroll
-      for (int k = 0; k < PER; k++)
-        if (kmask >> k & 1u) Ak[r++] = x[k];  // r < nsort: B untouched
-    }
-    __syncthreads();
-    uint32_t* dst = sorted32 + P.e_first + c.cb_rel;
-    const uint32_t FPNONE = 0xffffffffu >> P.vs;
-    auto fp_of = [&](uint32_t v) { return (v >> 1) >> P.vs; };
-    auto ix_of = [&](uint32_t v) { return ish >= 32 ? 0u : (((v >> 1) >> ish) & (ipc - 1)); };
-    auto lower = [](const uint32_t* arr, uint32_t len, uint32_t v) {  // elements < v
-      uint32_t lo = 0, hi = len;
-      while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (arr[m] < v) lo = m + 1; else hi = m;
-      }
-      return lo;
-    };
-    // num_unique (:558, :572-574): an entry counts when its fingerprint differs from its
-    // merged predecessor's in the same index (UINT32_MAX >> value_size at an index's start);
-    // the predecessor is the larger of the previous kept new entry and the previous old one
-    auto counts = [&](uint32_t v, bool hp, uint32_t p) -> uint32_t {
-      const uint32_t pfp = (hp && ix_of(p) == ix_of(v)) ? fp_of(p) : FPNONE;
-      return fp_of(v) != pfp ? 1u : 0u;
-    };
-    uint32_t uniq = 0;
-    // (2) kept new entries (in registers): merged position = kept rank + old entries before
-    // it (a binary search of B)
-    uint32_t npos[PER];
-    {
-      uint32_t r = kbase;
-#pragma unroll
-      for (int k = 0; k < PER; k++) {
-        npos[k] = 0;
-        if (kmask >> k & 1u) {
-          const uint32_t v = x[k], j = lower(B, nb, v);
-          npos[k] = r + j;
-          bool hp = r > 0;
-          uint32_t p = hp ? Ak[r - 1] : 0u;
-          if (j > 0 && (!hp || B[j - 1] > p)) { p = B[j - 1]; hp = true; }
-          uniq += counts(v, hp, p);
-          r++;
-        }
-      }
-    }
-    // (3) old entries: thread t owns B[t*cbn, t*cbn + cbn) (odd stride: distinct LDS banks);
-    // merged position = own index + kept new entries before it -- one binary search of Ak,
-    // then a walk. Values and positions stay in registers until every read of A and B is done.
-    const uint32_t cbn = min((uint32_t)PER, ((nb + SORT_NT - 1) / SORT_NT) | 1u);  // PER * SORT_NT >= nb
-    const uint32_t j0 = threadIdx.x * cbn;
-    uint32_t ov[PER], opos[PER];
-    {
-      uint32_t i = j0 < nb ? lower(Ak, nkept, B[j0]) : 0u;
-#pragma unroll
-      for (int k = 0; k < PER; k++) {
-        const uint32_t j = j0 + k;
-        ov[k] = 0;
-        opos[k] = 0;
-        if ((uint32_t)k < cbn && j < nb) {
-          const uint32_t v = B[j];
-          while (i < nkept && Ak[i] < v) i++;
-          ov[k] = v;
-          opos[k] = j + i;
-          bool hp = j > 0;
-          uint32_t p = hp ? B[j - 1] : 0u;
-          if (i > 0 && (!hp || Ak[i - 1] > p)) { p = Ak[i - 1]; hp = true; }
-          uniq += counts(v, hp, p);
-        }
-      }
-    }
-    // (4) per index: bounds, and its smallest old entry (the num_unique put-back quirk, K5)
-    auto first_of = [&](const uint32_t* arr, uint32_t len, uint32_t l) {  // first entry of index >= l
-      uint32_t lo = 0, hi = len;
-      while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (ix_of(arr[m]) < l) lo = m + 1; else hi = m;
-      }
-      return lo;
-    };
-    for (uint32_t l = threadIdx.x; l < ipc; l += SORT_NT) {
-      const uint32_t as = first_of(Ak, nkept, l), bs = first_of(B, nb, l);
-      const uint32_t ae = l + 1 < ipc ? first_of(Ak, nkept, l + 1) : nkept;
-      const uint32_t be = l + 1 < ipc ? first_of(B, nb, l + 1) : nb;
-      idx_cnt[c.idx0 + l] = (ae - as) + (be - bs);
-      idx_start[c.idx0 + l] = c.cb_rel + as + bs;
-      first_old[c.idx0 + l] = be > bs ? B[bs] >> 1 : 0xffffffffu;
-      has_old[c.idx0 + l] = be > bs ? 1u : 0u;
-    }
-    __syncthreads();  // every read of A and B is done: the merged order overwrites s_b
-    const uint32_t ntot = nkept + nb;
-    {
-      uint32_t r = 0;
-#pragma unroll
-      for (int k = 0; k < PER; k++) {
-        if (kmask >> k & 1u) Ak[npos[k]] = x[k] >> 1;
-        if ((uint32_t)k < cbn && j0 + k < nb) Ak[opos[k]] = ov[k] >> 1;
-        (void)r;
-      }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ntot; i += SORT_NT) dst[i] = Ak[i];  // coalesced
-    uint32_t tot_uniq;
-    block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
-    if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
-    DBG_PHASE(5);
-    DBG_PHASE(6);
-    DBG_PHASE(7);
-    DBG_PHASE(8);
-    return;
-  }
   // dedupe + compaction: thread t owns the contiguous run [t*drun, t*drun + drun), drun =
   // ceil(n / SORT_NT) made odd (lanes drun words apart fall on distinct LDS banks) and
   // capped at PER: every thread takes a share of a small bucket, not half of them PER each
@@ -1322,7 +1176,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   __shared__ uint8_t s_mark[MAX_INDICES + 1];
   __shared__ uint32_t s_tmp[LAYOUT_NT / WAVE + 1];
   __shared__ uint32_t s_err;
-  __shared__ uint16_t s_list[LAYOUT_LIST];  // every 2^R-th page start (<= 2 * 2^R + 2 of them)
+  __shared__ uint16_t s_list[LAYOUT_LIST];  // every 2^R-th page start (<= 2 est / 2^R + 1 <= 257 of them)
   __shared__ uint32_t s_wt[MAX_INDICES / LAYOUT_NT * (LAYOUT_NT / WAVE) + 1];  // k-major scan totals
   __shared__ uint32_t s_nlist;
   const uint32_t f = blockIdx.x;
@@ -1414,11 +1268,13 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
   // Mark the orbit of block 0 under next() (the page starts). R rounds of in-place pointer
   // doubling give J = next^(2^R) in s_jB; one lane walks the orbit with J (every 2^R-th
   // page start), then each of those points walks up to 2^R - 1 steps of next() marking the
-  // page starts in between. R ~ log2(pages) / 2 balances the two walks (C2: 1,366 pages,
-  // R = 5: 43 + 31 dependent LDS reads instead of ~12 full doubling rounds).
+  // page starts in between. A doubling round (every index, a barrier) costs about as much as
+  // ~100 dependent LDS reads of the single-lane walk, so R = log2(pages) - 7 (C2: 1,366
+  // pages, R = 4: 85 + 15 dependent reads; R = 6 took 41 % of K5, 17 us).
   {
     const uint32_t est = s_excl[n] / page_size + 1;  // pages >= est - 1, and <= 2 est
-    const uint32_t R = min(8u, (32u - __clz(est) + 1) / 2);
+    const uint32_t lg = 32u - __clz(est);
+    const uint32_t R = min(8u, lg > 8 ? lg - 7 : 1u);
     for (uint32_t j = threadIdx.x; j <= n; j += LAYOUT_NT) s_jB[j] = s_jA[j];
     __syncthreads();
     for (uint32_t r = 0; r < R; r++) {
@@ -1449,7 +1305,7 @@ __global__ __launch_bounds__(LAYOUT_NT) void k_layout(const FilterPlan* __restri
         x = s_jB[x];
       }
       s_nlist = m;
-      if (x != n) {  // cannot happen (m <= 2 * 2^R + 2); reported, never silently wrong
+      if (x != n) {  // cannot happen (m <= 257); reported, never silently wrong
         outs[f].error |= ERR_PAGE_CAP;
         pplans[f].w = ERR_PAGE_CAP;
       }
@@ -3171,28 +3027,53 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
   const uint32_t lane = threadIdx.x;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t t_busy = t0, served = 0;
+  // a pass looks at the next SRV_PER x 64 tickets (one load per lane and group, all in flight
+  // together) and serves their ready prefix, SRV_PER requests per lane: a backlog of
+  // submitted requests goes out SRV_PER times faster than one request per lane and pass
+  constexpr uint32_t SRV_PER = 4;
   for (;;) {
-    const uint32_t slot = (uint32_t)((head + lane) & (SRV_RING - 1));
-    const uint64_t tk = __hip_atomic_load(&ring[slot].ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t ready = __builtin_amdgcn_ballot_w64(tk == head + lane);
-    const uint32_t k = ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);  // the ready prefix
+    uint64_t tk[SRV_PER];
+#pragma unroll
+    for (uint32_t m = 0; m < SRV_PER; m++)
+      tk[m] = __hip_atomic_load(&ring[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))].ticket, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t k = 0;  // the ready prefix
+#pragma unroll
+    for (uint32_t m = 0; m < SRV_PER; m++) {
+      const uint64_t ready = __builtin_amdgcn_ballot_w64(tk[m] == head + lane + WAVE * m);
+      if (k == WAVE * m) k += ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
+    }
     if (k) {
       // acquire (system scope) once per served pass, not per poll: the payloads after the
       // tickets, and no stale cached device data (it invalidates this CU's L1 and the L2)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      if (lane < k) {
-        const SrvReq& q = ring[slot];
-        const ProbeGroup G = q.g;
-        const uint32_t h = q.h;
-        __hip_atomic_store(&res[slot].found, probe_group(G, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ProbeGroup G[SRV_PER];
+      uint32_t h[SRV_PER];
+#pragma unroll
+      for (uint32_t m = 0; m < SRV_PER; m++) {  // every payload load first
+        const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
+        if (i < k) {
+          G[m] = ring[slot].g;
+          h[m] = ring[slot].h;
+        }
+      }
+#pragma unroll
+      for (uint32_t m = 0; m < SRV_PER; m++) {
+        const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
+        if (i < k) __hip_atomic_store(&res[slot].found, probe_group(G[m], h[m]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       // the found words (system-coherent stores to host memory, no cached copy to write back)
       // have completed before any ticket is stored
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane < k) __hip_atomic_store(&res[slot].ticket, head + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (uint32_t m = 0; m < SRV_PER; m++) {
+        const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
+        if (i < k) __hip_atomic_store(&res[slot].ticket, head + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       head += k;
       served += k;
       t_busy = __builtin_amdgcn_s_memrealtime();
+      if (t_busy - t0 > life_ticks) break;  // the lifetime bounds a busy wave too (waiters relaunch it)
       continue;
     }
     // idle: poll the next ticket alone (one 8-byte PCIe read per poll), bounded by the clock
@@ -3335,27 +3216,11 @@ static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const ui
   return 0;
 }
 
-// 32-bit incremental builds: K4 places every entry directly (RF_AMD_K4_DIRECT=1) or merges
-// the sorted new run with the old run through a merge path (default); read per launch, so one
-// process can compare them
-static bool k4_direct() {
-  const char* v = getenv("RF_AMD_K4_DIRECT");
-  return v && v[0] == '1';
-}
-
 template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* spill) {
-  bool direct = false;
-  if constexpr (DUAL) direct = k4_direct();
-  if (direct) {
-    hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start,
-                       a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
-  } else {
-    hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start,
-                       a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
-  }
+  hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
+                     a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start,
+                     a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
   CHECK_LAUNCH();
   REC(EV_B_SORT);
   hipLaunchKernelGGL((k_cb_sort_big<EntT, FL, DUAL>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans,

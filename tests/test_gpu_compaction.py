@@ -30,16 +30,13 @@ def chain_ids(g, v, n):
 
 
 @pytest.mark.skipif(not R.available(), reason="reference library not built")
-@pytest.mark.parametrize("entries", ["flag32", "flag32_direct", "flag32_decode", "wide64"])
+@pytest.mark.parametrize("entries", ["flag32", "flag32_decode", "wide64"])
 def test_chain_rounds_match_reference(entries, monkeypatch):
     """both incremental pipelines: 32-bit flagged entries (fp_size + value_size <= 31, the
     default) and 64-bit entries (forced here). With 32-bit entries a round whose geometry is
     the previous round's (rounds 3 and 5: 40K -> 60K, 80K -> 100K fingerprints) reads the old
     entries in place from the previous batch; the others decode the old image
-    (flag32_decode forces the decode for every round; flag32_direct takes K4's direct
-    placement of every entry instead of its merge path)"""
-    if entries == "flag32_direct":
-        monkeypatch.setenv("RF_AMD_K4_DIRECT", "1")
+    (flag32_decode forces the decode for every round)"""
     if entries == "wide64":
         monkeypatch.setenv("RF_AMD_WIDE64", "1")
     if entries == "flag32_decode":
@@ -122,14 +119,12 @@ def test_bench_compaction_full_chains_golden(gpus, filters):
 
 
 @pytest.mark.skipif(not R.available(), reason="reference library not built")
-@pytest.mark.parametrize("direct", ["0", "1"])
-def test_incremental_ties_and_duplicates(direct, monkeypatch):
+def test_incremental_ties_and_duplicates():
     """an incremental add onto a filter of the same geometry (old entries read in place and
-    merged in K4: merge path, or RF_AMD_K4_DIRECT=1 direct placement) whose new keys repeat old keys under the SAME
+    merged with the sorted new ones in K4) whose new keys repeat old keys under the SAME
     value (equal old and new entries: the old one first, both kept, src/routing_filter.c
     :563-566) and repeat each other (new duplicates dropped, :473-482), over two rounds --
     byte-identical to the reference's chain, num_unique included"""
-    monkeypatch.setenv("RF_AMD_K4_DIRECT", direct)
     cfg = E.routing_config_init(fingerprint_size=26, log_index_size=8, seed=42)
     eng = E.Engine(0)
     rng = np.random.default_rng(7)

@@ -4,20 +4,10 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 O=gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_compaction.py -k "ties or chain_rounds" > $O/gt_m6.log 2>&1 || { tail -40 $O/gt_m6.log; exit 1; }
-tail -1 $O/gt_m6.log
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_shim.py tests/test_gpu_filter_test.py tests/test_gpu_parity.py > $O/gt_a.log 2>&1 || { tail -30 $O/gt_a.log; exit 1; }
-tail -1 $O/gt_a.log
-timeout -k 10 200 python tools/ab_step.py tools/ab/librf_amd_x3off.so tools/ab/librf_amd_x3on.so > $O/ab_x3.json 2>/dev/null || exit 1
-cat $O/ab_x3.json
-for m in 0 1; do
-  RF_AMD_K6_MERGE=$m timeout -k 10 300 python bench.py --workload compaction --steps 5 --warmup 1 --no-cpu-baseline > $O/bc_m$m.json 2> $O/bc_m$m.err || { tail -20 $O/bc_m$m.err; exit 1; }
-done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_server.py tests/test_gpu_shim.py tests/test_gpu_trunk.py tests/test_gpu_filter_test.py > $O/gt_d.log 2>&1 || { tail -40 $O/gt_d.log; exit 1; }
+tail -1 $O/gt_d.log
+timeout -k 10 300 python tools/shim_latency.py > $O/sl_f.json 2>/dev/null || exit 1
 python -c "
-import json
-for m in (0,1):
-    d=json.load(open('$O/bc_m%d.json'%m)); print(m, d['value'], d.get('ms_per_step'), d.get('verified'), d.get('kernels'))"
-timeout -k 10 300 python tools/shim_latency.py > $O/sl_d1.json 2>/dev/null || exit 1
-RF_SHIM_DIRECT=0 timeout -k 10 300 python tools/shim_latency.py > $O/sl_d0p1.json 2>/dev/null || exit 1
-timeout -k 10 120 python tools/phase_times.py 2 > $O/pt2.txt 2>&1 || exit 1
-timeout -k 10 120 python tools/phase_times.py 4 > $O/pt4.txt 2>&1 || exit 1
+import json; d=json.load(open('$O/sl_f.json'))['shim']; print({k:d[k] for k in ('add_fresh_ms','add_incremental_ms','mt_adds_8x_ms','lookup_one_ms','lookup_batch_8192_ms','lookup_async_8192_ms','async_driven_8192_ms','async_8192_512f_ms')}); print(d['async_driven_breakdown'])"
+timeout -k 10 300 python tools/trunk_latency.py > $O/trunk_f.json 2>/dev/null || exit 1
+cat $O/trunk_f.json
