@@ -1598,9 +1598,12 @@ aq_init(void)
    pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
    pthread_t t;
    platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
-   /* two batch threads: a batch goes out while the previous one is on the GPU */
-   platform_assert(pthread_create(&t, &at, batch_main, NULL) == 0);
-   platform_assert(pthread_create(&t, &at, batch_main, NULL) == 0);
+   /* RF_SHIM_BATCH_THREADS batch threads (default 1; 2: a batch goes out while the previous
+      one is on the GPU) */
+   uint64 nb = env_u64("RF_SHIM_BATCH_THREADS", 1);
+   for (uint64 k = 0; k < (nb >= 1 && nb <= 8 ? nb : 1); k++) {
+      platform_assert(pthread_create(&t, &at, batch_main, NULL) == 0);
+   }
    pthread_attr_destroy(&at);
 }
 
@@ -1671,9 +1674,12 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    pthread_once(&g_aq_once, aq_init);
    const uint64 t0 = now_ns();
    state->fp       = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
-   if (__atomic_load_n(&g_aq_outstanding, __ATOMIC_RELAXED) >= AQ_SERVER_MAX) {
-      /* a burst: onto the batch stack (the state may complete at once on another thread; it
-         is not read again here) */
+   if (__atomic_load_n(&g_aq_outstanding, __ATOMIC_RELAXED) >= AQ_SERVER_MAX
+       || __atomic_load_n(&g_bq_pending, __ATOMIC_RELAXED))
+   {
+      /* a burst (the server's share is full, or batched states are still in flight: the
+         burst stays on the batch path until it drains): onto the batch stack (the state may
+         complete at once on another thread; it is not read again here) */
       state->__async_state_stack[0] = ASYNC_STATE_QUEUED;
       __atomic_add_fetch(&g_bq_pending, 1, __ATOMIC_SEQ_CST);
       rf_state *old                 = __atomic_load_n(&g_bq_head, __ATOMIC_RELAXED);
