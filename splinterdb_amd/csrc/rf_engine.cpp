@@ -176,7 +176,13 @@ struct LookupServer {
   SrvRes* res = nullptr;
   SrvCtl* ctl = nullptr;
   hipStream_t st = nullptr;             // its own HSA queue (CU-masked), so it never blocks other work
-  void* tags[SRV_RING] = {};            // per slot: the submitter's tag (NULL: a waiter's ticket)
+  // per slot, host-only (the reaper never reads the request ring, whose lines the GPU polls):
+  // the slot's ticket (published after the tag) and the submitter's tag (NULL: a waiter's)
+  struct Meta {
+    std::atomic<uint64_t> ticket{~0ull};
+    void* tag = nullptr;
+  };
+  Meta meta[SRV_RING];
   std::atomic<uint64_t> consumed[SRV_RING];  // per slot: 1 + the last ticket whose result was taken
   std::atomic<uint64_t> tail{0};        // the next ticket
   std::atomic<uint64_t> state{0};       // generation << 1 | running
@@ -1348,12 +1354,15 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     }
     // the slot is being rewritten: readers that see this do not trust its payload or tag
     __atomic_store_n(&v.ring[slot].ticket, SRV_BUSY, __ATOMIC_RELEASE);
+    v.meta[slot].ticket.store(SRV_BUSY, std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_release);  // BUSY before the new tag (a seqlock)
   }
   SrvReq& q = v.ring[slot];
   q.g = probe_group_of(b, filter_index);
   q.h = hash;
   q.pad = tag ? 0u : 1u;  // 1: a waiter's ticket (rf_amd_lookup_wait takes its result)
-  v.tags[slot] = tag;
+  v.meta[slot].tag = tag;
+  v.meta[slot].ticket.store(t, std::memory_order_release);
   __atomic_store_n(&q.ticket, t, __ATOMIC_RELEASE);
   *ticket = t;
   return srv_ensure(e);
@@ -1387,16 +1396,16 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
   const uint64_t tail = v.tail.load(std::memory_order_acquire);
   while (n < max && t < tail) {
     const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
-    const uint64_t tk = __atomic_load_n(&v.ring[slot].ticket, __ATOMIC_ACQUIRE);
+    const uint64_t tk = v.meta[slot].ticket.load(std::memory_order_acquire);
     if (tk == SRV_UNPUBLISHED || tk == SRV_BUSY || tk < t) break;  // not yet published
     if (tk > t) {  // a waiter already took ticket t and its slot was reused
       t++;
       continue;
     }
-    const uint32_t waiter = v.ring[slot].pad;
-    void* tag = v.tags[slot];
-    if (__atomic_load_n(&v.ring[slot].ticket, __ATOMIC_ACQUIRE) != t) continue;  // rewritten meanwhile: re-read
-    if (waiter) {  // its waiter takes the result
+    void* tag = v.meta[slot].tag;
+    std::atomic_thread_fence(std::memory_order_acquire);  // the tag read before the re-check
+    if (v.meta[slot].ticket.load(std::memory_order_relaxed) != t) continue;  // rewritten meanwhile: re-read
+    if (!tag) {  // a waiter's ticket: its waiter takes the result
       t++;
       continue;
     }

@@ -2575,12 +2575,14 @@ __device__ __forceinline__ uint64_t field_ones64(uint32_t rvs) {
   return L;
 }
 
-// Line probe, decode half (format above): bucket j of the line's group, line bytes in Q.
-// Returns false when the image must be walked instead (overflowed line, or a bucket too
-// large for the 96-bit remainder window).
-__device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint32_t remainder, uint32_t vs,
-                                            uint32_t rvs, uint64_t& found) {
-  const uint32_t d0 = Q[0].x, d1 = Q[0].y, d2 = Q[0].z, d3 = Q[0].w;
+// Line probe, decode half (format above): bucket j of the line's group, its encoding dwords
+// in E (line bytes [0, 16)); win(wi, w0, w1, w2) fetches dwords wi, wi + 1, wi + 2 of the
+// remainder area (line dwords 4 + wi ..; past the line: 0). Returns false when the image must
+// be walked instead (overflowed line, or a bucket too large for the 96-bit remainder window).
+template <typename Win>
+__device__ __forceinline__ bool line_decode_w(const v4u& E, Win win, uint32_t j, uint32_t remainder, uint32_t vs,
+                                              uint32_t rvs, uint64_t& found) {
+  const uint32_t d0 = E.x, d1 = E.y, d2 = E.z, d3 = E.w;
   if ((d0 & d1 & d2 & d3) == 0xffffffffu) return false;  // overflow marker
   // p1 = first bit after terminator j-1 (0 for bucket 0); entries before bucket j = p1 - j
   uint32_t p1 = 0;
@@ -2607,17 +2609,8 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
   // the bucket's remainders: bits [s*rvs, (s+c)*rvs) of the 384-bit remainder area
   const uint32_t b = s * rvs, wi = b >> 5, off = b & 31;
   if (off + c * rvs > 96 || b + c * rvs > 384) return false;
-  // 96-bit window at dword wi (wi <= 9): pick the 4-dword group g = wi / 4, then dwords
-  // o..o+2 (o = wi % 4) of that group's 6-dword span -- 21 selects instead of 36
-  const uint32_t R[14] = {Q[1].x, Q[1].y, Q[1].z, Q[1].w, Q[2].x, Q[2].y, Q[2].z,
-                          Q[2].w, Q[3].x, Q[3].y, Q[3].z, Q[3].w, 0u, 0u};
-  const uint32_t g = wi >> 2, o = wi & 3;
-  uint32_t W[6];
-#pragma unroll
-  for (int k = 0; k < 6; k++) W[k] = g == 0 ? R[k] : (g == 1 ? R[4 + k] : R[8 + k]);
-  const uint32_t w0 = o == 0 ? W[0] : (o == 1 ? W[1] : (o == 2 ? W[2] : W[3]));
-  const uint32_t w1 = o == 0 ? W[1] : (o == 1 ? W[2] : (o == 2 ? W[3] : W[4]));
-  const uint32_t w2 = o == 0 ? W[2] : (o == 1 ? W[3] : (o == 2 ? W[4] : W[5]));
+  uint32_t w0, w1, w2;
+  win(wi, w0, w1, w2);
   const uint64_t wl = (uint64_t)w1 << 32 | w0;
   const uint32_t vmask = (uint32_t)((1ull << vs) - 1);
   const uint32_t nb = c * rvs, rem = rvs - vs;
@@ -2657,6 +2650,25 @@ __device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint3
     }
   }
   return true;
+}
+
+// the window from the line held in registers (Q[1..3]: the 384-bit remainder area): 96 bits at
+// dword wi (wi <= 9) -- pick the 4-dword group g = wi / 4, then dwords o..o+2 (o = wi % 4) of
+// that group's 6-dword span (21 selects instead of 36)
+__device__ __forceinline__ bool line_decode(const v4u (&Q)[4], uint32_t j, uint32_t remainder, uint32_t vs,
+                                            uint32_t rvs, uint64_t& found) {
+  auto win = [&](uint32_t wi, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
+    const uint32_t R[14] = {Q[1].x, Q[1].y, Q[1].z, Q[1].w, Q[2].x, Q[2].y, Q[2].z,
+                            Q[2].w, Q[3].x, Q[3].y, Q[3].z, Q[3].w, 0u, 0u};
+    const uint32_t g = wi >> 2, o = wi & 3;
+    uint32_t W[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) W[k] = g == 0 ? R[k] : (g == 1 ? R[4 + k] : R[8 + k]);
+    w0 = o == 0 ? W[0] : (o == 1 ? W[1] : (o == 2 ? W[2] : W[3]));
+    w1 = o == 0 ? W[1] : (o == 1 ? W[2] : (o == 2 ? W[3] : W[4]));
+    w2 = o == 0 ? W[2] : (o == 1 ? W[3] : (o == 2 ? W[4] : W[5]));
+  };
+  return line_decode_w(Q[0], win, j, remainder, vs, rvs, found);
 }
 
 // threads per probe workgroup: 1,024 for fixed-length keys and hashes (C3 probe 2.74 ->
@@ -2884,17 +2896,18 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
         const uint32_t fp = h >> (32 - fp_size);
         const uint32_t bucket = rem >= 32 ? 0u : fp >> rem;
         const uint32_t remainder = fp & (rem >= 32 ? 0xffffffffu : ((1u << rem) - 1));
-        const uint32_t li = U.y + (bucket >> (lgl - 1));
+        // the filter's line table (uniform) and this probe's line within it as a 32-bit byte
+        // offset: each load is a scalar base plus one VGPR offset (no per-load 64-bit math)
+        const uint8_t* fb = reinterpret_cast<const uint8_t*>(lines) + ((uint64_t)U.y << 6);
+        const uint32_t lo = (bucket >> (lgl - 1)) << 6;
         v4u* sw;
         if constexpr (WAVE_VAR) sw = reinterpret_cast<v4u*>(s_vk[threadIdx.x / WAVE]);
         else sw = s_wbuf[threadIdx.x / WAVE];
-        const v4u* lv = reinterpret_cast<const v4u*>(lines);
 #define RF_QUAD_LOAD(k)                                                                                      \
   {                                                                                                          \
-    const uint32_t lk = (uint32_t)__builtin_amdgcn_mov_dpp((int)li, (k) * 0x55, 0xf, 0xf, false);            \
-    __builtin_amdgcn_global_load_lds(                                                                        \
-        (const __attribute__((address_space(1))) void*)(lv + (uint64_t)lk * 4 + ((q + (k)) & 3)),          \
-        (__attribute__((address_space(3))) void*)(sw + (k) * WAVE), 16, 0, 0);                             \
+    const uint32_t lk = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, (k) * 0x55, 0xf, 0xf, false);            \
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(fb + lk + (((q + (k)) & 3u) << 4)), \
+                                     (__attribute__((address_space(3))) void*)(sw + (k) * WAVE), 16, 0, 0);  \
   }
         RF_QUAD_LOAD(0) RF_QUAD_LOAD(1) RF_QUAD_LOAD(2) RF_QUAD_LOAD(3)
 #undef RF_QUAD_LOAD
@@ -2902,12 +2915,22 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const v4u* mine = sw + (lane & 3) * WAVE + (lane >> 2) * 4;
-        v4u Q[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) Q[j] = mine[(j - lane) & 3];
+        // this probe's line in LDS: quarter j at L32 + ((j - lane) & 3) * 4 (dwords). The
+        // decode reads the encoding quarter into registers and only the three dwords of its
+        // bucket's remainder window from LDS (instead of all four quarters and a 21-way select:
+        // the probe is VALU-bound as much as memory-bound)
+        const uint32_t* L32 = reinterpret_cast<const uint32_t*>(sw + (lane & 3) * WAVE + (lane >> 2) * 4);
+        const v4u E = *reinterpret_cast<const v4u*>(L32 + ((0u - lane) & 3u) * 4);
+        auto win = [&](uint32_t wi, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
+          // line dword d = 4 + wi + t (d & 15: dwords past the line are never used, the
+          // window's bits beyond the bucket are masked)
+          auto dw = [&](uint32_t d) -> uint32_t { d &= 15u; return L32[(((d >> 2) - lane) & 3u) * 4 + (d & 3u)]; };
+          w0 = dw(4 + wi);
+          w1 = dw(5 + wi);
+          w2 = dw(6 + wi);
+        };
         uint64_t r;
-        if (!line_decode(Q, bucket & ((1u << (lgl - 1)) - 1), remainder, vs, rvs, r))
+        if (!line_decode_w(E, win, bucket & ((1u << (lgl - 1)) - 1), remainder, vs, rvs, r))
           r = probe_walk(U, h, fs, plans, pages, slots, fp_size, lis, page_size);
         __builtin_nontemporal_store(r, found + i0);
         return;
