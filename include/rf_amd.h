@@ -165,6 +165,9 @@ uint64_t rf_amd_lookup_reap(rf_amd_engine *e, void **tags, uint64_t *found_value
  * most keep_bytes stay pooled */
 int rf_amd_engine_pool_stats(rf_amd_engine *e, uint64_t *pooled_bytes, uint64_t *hits, uint64_t *misses);
 int rf_amd_engine_pool_trim(rf_amd_engine *e, uint64_t keep_bytes);
+/* the most device memory the pool keeps parked for reuse (default: RF_AMD_POOL_MIB, else a
+ * quarter of the free memory at creation, at most 16 GiB); trims to it now */
+int rf_amd_engine_set_pool_limit(rf_amd_engine *e, uint64_t bytes);
 /* the engine's stream (NULL-stream arguments, host-buffer builds and imports run there) and
  * its synchronisation (only that stream, not the device) */
 void *rf_amd_engine_stream(rf_amd_engine *e);

@@ -48,7 +48,7 @@
  * later incremental add onto it reads the old entries in place instead of decoding the image
  * -- in a registry keyed by (cache, index-extent address); lookups never re-read it. A
  * filter not in the registry (built before a restart, or evicted) is read back through
- * cache_get once and imported. The registry is bounded (RF_AMD_REGISTRY_MIB, default 32 GiB
+ * cache_get once and imported. The registry is bounded (RF_AMD_REGISTRY_MIB, default 8 GiB
  * of device memory): past the bound the least recently used batches are first trimmed to
  * their probe-only state, then evicted; batches in use by a running call are pinned and
  * never released under it. dec_ref drops the device copy when the reference's refcount
@@ -95,6 +95,11 @@ engine_init(void)
 {
    const char *d = getenv("RF_AMD_DEVICE");
    g_eng_rc      = rf_amd_engine_create(d ? atoi(d) : 0, &g_eng);
+   /* a storage engine links this: its pool keeps at most 2 GiB parked unless
+      RF_AMD_POOL_MIB says otherwise (one add's batch is at most a few hundred MB) */
+   if (g_eng_rc == 0 && !getenv("RF_AMD_POOL_MIB")) {
+      (void)rf_amd_engine_set_pool_limit(g_eng, 2048ull << 20);
+   }
 }
 
 static rf_amd_engine *
@@ -182,7 +187,7 @@ static uint64
 registry_limit(void)
 {
    if (!g_registry_limit) {
-      g_registry_limit = env_u64("RF_AMD_REGISTRY_MIB", 32768) << 20;
+      g_registry_limit = env_u64("RF_AMD_REGISTRY_MIB", 8192) << 20;
    }
    return g_registry_limit;
 }

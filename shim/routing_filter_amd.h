@@ -36,7 +36,7 @@ void
 routing_filter_amd_add_stats(uint64 *batches, uint64 *filters);
 
 /* device bytes held by the resident-filter registry (bound: RF_AMD_REGISTRY_MIB, default
- * 32768), filters evicted and batches trimmed to their probe-only state so far */
+ * 8192), filters evicted and batches trimmed to their probe-only state so far */
 void
 routing_filter_amd_registry_stats(uint64 *bytes, uint64 *evictions, uint64 *trims);
 

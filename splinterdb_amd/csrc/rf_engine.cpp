@@ -917,6 +917,17 @@ extern "C" int rf_amd_engine_pool_trim(rf_amd_engine* e, uint64_t keep_bytes) {
   return 0;
 }
 
+// the most device memory the pool keeps parked for reuse (RF_AMD_POOL_MIB at creation), trimmed
+// to it now
+extern "C" int rf_amd_engine_set_pool_limit(rf_amd_engine* e, uint64_t bytes) {
+  if (!e) return fail(RF_AMD_EINVAL, "null engine");
+  {
+    std::lock_guard<std::mutex> g(e->pool.mu);
+    e->pool.limit = bytes;
+  }
+  return rf_amd_engine_pool_trim(e, bytes);
+}
+
 extern "C" uint32_t rf_amd_batch_num_filters(const rf_amd_batch* b) { return b ? b->F : 0; }
 
 static LaunchArgs make_args(rf_amd_batch* b, hipStream_t st) {

@@ -37,7 +37,7 @@ EXPORTED = [
     "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_batch_timings_back", 
     "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer", "rf_amd_diag_lookup_stats",
     "rf_amd_host_alloc", "rf_amd_host_free", "rf_amd_engine_fence", "rf_amd_engine_fence_wait",
-    "rf_amd_host_register", "rf_amd_host_unregister", "rf_amd_batch_place_image",
+    "rf_amd_host_register", "rf_amd_host_unregister", "rf_amd_batch_place_image", "rf_amd_engine_set_pool_limit",
     "rf_amd_lookup_submit", "rf_amd_lookup_wait", "rf_amd_lookup_reap", "rf_amd_lookup_server_stats",
     "rf_amd_build_id",
     "rf_amd_filter_add", "rf_amd_filter_lookup_hashes", "rf_amd_filter_lookup_keys",

@@ -349,3 +349,45 @@ def test_registry_bound_evicts_and_reimports(pair):
         assert_same_pages(ref, shim, dr, ds, "onto evicted")
     finally:
         shim.registry_set_limit(32768)
+
+
+_BOUNCE_CHECK = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from oracle import refimpl as R
+from splinterdb_amd import keys as K
+ref, shim = R.Stack(), R.Stack(path=R.SHIM_PATH)
+rng = np.random.default_rng(5)
+prev_r = prev_s = None
+for n, value in ((1, 0), (20_000, 3), (700_000, 3), (300_000, 9)):
+    h = ref.hash_keys(K.random_keys(n, seed=int(rng.integers(1 << 30))))
+    dr = ref.add(h, value=value, old=prev_r)
+    ds = shim.add(h, value=value, old=prev_s)
+    assert (dr.addr, dr.meta_head, dr.num_fingerprints, dr.num_unique) == \
+           (ds.addr, ds.meta_head, ds.num_fingerprints, ds.num_unique), n
+    for p in range(32):
+        a = dr.addr + 4096 * p
+        assert (ref.read_page(a) == shim.read_page(a)).all(), (n, p)
+    ir, is_ = ref.image(dr), shim.image(ds)
+    assert (ir.slots == is_.slots).all() and (ir.pages == is_.pages).all(), n
+    prev_r, prev_s = dr, ds
+assert ref.device_writes() == 0 and shim.device_writes() == 0
+print("OK")
+"""
+
+
+@pytest.mark.parametrize("env", [{"RF_SHIM_DIRECT": "0"}, {"RF_SHIM_DIRECT": "0", "RF_SHIM_PINNED": "0"}])
+def test_add_bounce_paths_identical_to_reference(env):
+    """routing_filter_add's fallbacks when images cannot go straight into the cache pages
+    (RF_SHIM_DIRECT=0): read back into a recycled pinned buffer, or into malloc'd memory after
+    an engine-wide sync (RF_SHIM_PINNED=0), then copied page by page -- fresh and incremental
+    adds, pages and index extents identical to the reference's (in a subprocess: the
+    switches are read once per process)"""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    r = subprocess.run([sys.executable, "-c", _BOUNCE_CHECK, ROOT], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
