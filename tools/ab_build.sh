@@ -9,8 +9,9 @@ for f in splinterdb_amd/csrc/rf_kernels.hip splinterdb_amd/csrc/rf_engine.cpp sp
   if [ "$REV" = WT ]; then cp $ROOT/$f $D/$f; else git -C $ROOT show $REV:$f > $D/$f; fi
 done
 H=/opt/rocm/bin/hipcc
-# the working tree's build id (a variant of the tree's sources loads through engine.py's check)
-if [ "$REV" = WT ]; then DEFS="$DEFS -DRF_AMD_SRC_ID=\"$(cd $ROOT && python3 -c 'from splinterdb_amd import build; print(build.source_id())')\""; fi
+# the working tree's build id (a variant of the tree's sources loads through engine.py's check;
+# AB_TREE_ID=1 gives a revision's build the same id)
+if [ "$REV" = WT ] || [ -n "$AB_TREE_ID" ]; then DEFS="$DEFS -DRF_AMD_SRC_ID=\"$(cd $ROOT && python3 -c 'from splinterdb_amd import build; print(build.source_id())')\""; fi
 $H --offload-arch=gfx950 -O3 -std=c++17 -fPIC $DEFS -c $D/splinterdb_amd/csrc/rf_kernels.hip -o $D/k.o
 $H -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC $DEFS -c $D/splinterdb_amd/csrc/rf_engine.cpp -o $D/e.o
 $H --offload-arch=gfx950 -shared -fPIC -o $ROOT/tools/ab/librf_amd_$TAG.so $D/k.o $D/e.o
