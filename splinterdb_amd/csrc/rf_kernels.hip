@@ -882,7 +882,10 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
     }
     __syncthreads();
   }
-  if constexpr (FL) {  // s_bin is no longer read; the scan below orders these before use
+  // incremental builds that split old indices (npo > 1) need each index's smallest old entry
+  // for K5's num_unique put-back quirk; with one new index per old index nothing reads it
+  const bool track_old = FL && P.npo > 1;
+  if (track_old) {  // s_bin is no longer read; the scan below orders these before use
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) { s_fo[i] = 0xffffffffu; s_ho[i] = 0; }
   }
   DBG_PHASE(4);
@@ -915,6 +918,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       prev0 = ta ? A[ia++] : B[ib++];
     }
   }
+  DBG_PHASE(9);  // (thread 0) merge-path split found
   {
     EntT prev = prev0;
 #pragma unroll
@@ -933,6 +937,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       }
     }
   }
+  DBG_PHASE(10);  // (thread 0) its run merged and flagged
   uint32_t kept;
   uint32_t pos = block_excl_scan<SORT_NT>(cnt, s_tmp, &kept);  // has barriers: reads done
   uint32_t* s_sorted = reinterpret_cast<uint32_t*>(s_b);        // compacted e values (u32)
@@ -963,7 +968,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
           // order, so its first old entry of an index is its smallest there: one LDS atomic
           // per (run, index) instead of one per old entry (all of an index's entries would
           // otherwise contend for one address)
-          if (!(w[k] & EntT(1)) && li != fo_li) {
+          if (track_old && !(w[k] & EntT(1)) && li != fo_li) {
             atomicMin(&s_fo[li], e);
             s_ho[li] = 1;
             fo_li = li;
@@ -982,7 +987,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
       if (llast == NONE || l > llast) s_first[l] = kept;
     if (threadIdx.x == 0) s_first[ipc] = kept;
   }
-  if constexpr (FL) {
+  if (track_old) {
     for (uint32_t i = threadIdx.x; i < ipc; i += SORT_NT) {
       first_old[c.idx0 + i] = s_fo[i];
       has_old[c.idx0 + i] = s_ho[i];

@@ -51,8 +51,9 @@ ts = ts[used]
 print(f"workgroups stamped: {ts.shape[0]}")
 if KID == 1:
     names = {15: "entry", 0: "init", 1: "load+rank", 2: "bin scan", 3: "scatter", 4: "bin sort",
-             5: "dedupe+compact", 6: "write out", 7: "index bounds", 8: "uniq+end"}
-    order = [15, 0, 1, 2, 3, 4, 5, 6, 7, 8]
+             9: "merge split (t0)", 10: "merge run (t0)", 5: "scan+compact", 6: "write out",
+             7: "index bounds", 8: "uniq+end"}
+    order = [15, 0, 1, 2, 3, 4, 9, 10, 5, 6, 7, 8]
 elif KID == 4:
     names = {15: "entry", 5: "size loads (t0)", 6: "scan", 0: "excl store", 1: "next()", 2: "doubling",
              3: "pages+slots", 8: "quirk+end"}
