@@ -8,8 +8,9 @@
 #include "routing_filter.h"
 
 /* complete every routing_filter_lookup_async state submitted so far in the caller's thread
- * (their answers reaped from the engine's lookup server, callbacks fired). States also
- * complete on their own: the shim's completion thread reaps answers as they arrive */
+ * (answers reaped from the engine's lookup server, batched states probed; callbacks fired).
+ * States also complete on their own: the shim's completion threads reap answers and answer
+ * batches as they arrive */
 void
 routing_filter_amd_flush(void);
 
