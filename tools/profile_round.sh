@@ -7,6 +7,7 @@
 #      traffic from (1), the compaction chain's kernel trace, the shim's per-call costs and the
 #      reference's own kvstore driving the shim (tools/trunk_latency.py).
 # usage: bash tools/profile_round.sh <tag>      (outputs under gpurun_out/prof_<tag>/)
+# (build the per-lane probe variant first, here: tools/ab_build.sh WT quad0 "-DRF_PROBE_QUAD=0")
 set -o pipefail
 TAG=${1:-r04}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
