@@ -781,7 +781,10 @@ cache_direct(rf_amd_engine *e, cache *cc)
    if (!found && g_direct_n < DIRECT_CACHES) {
       char       *base  = ccc->data;
       uint64      bytes = ccc->cfg ? ccc->cfg->capacity : 0;
-      ok = base && bytes && rf_amd_host_register(e, base, bytes) == 0;
+      /* registering pins the whole buffer (once, ~proportional to its size): caches over
+         RF_SHIM_DIRECT_MAX_MIB (default 65,536) keep the bounce-buffer path */
+      const uint64 max_b = env_u64("RF_SHIM_DIRECT_MAX_MIB", 65536) << 20;
+      ok = base && bytes && bytes <= max_b && rf_amd_host_register(e, base, bytes) == 0;
       g_direct[g_direct_n].cc    = cc;
       g_direct[g_direct_n].base  = base;
       g_direct[g_direct_n].bytes = bytes;
