@@ -377,11 +377,13 @@ print("OK")
 """
 
 
-@pytest.mark.parametrize("env", [{"RF_SHIM_DIRECT": "0"}, {"RF_SHIM_DIRECT": "0", "RF_SHIM_PINNED": "0"}])
+@pytest.mark.parametrize("env", [{"RF_SHIM_DIRECT": "0"}, {"RF_SHIM_DIRECT": "0", "RF_SHIM_PINNED": "0"},
+                                 {"RF_SHIM_DIRECT_MAX_MIB": "0"}])
 def test_add_bounce_paths_identical_to_reference(env):
     """routing_filter_add's fallbacks when images cannot go straight into the cache pages
-    (RF_SHIM_DIRECT=0): read back into a recycled pinned buffer, or into malloc'd memory after
-    an engine-wide sync (RF_SHIM_PINNED=0), then copied page by page -- fresh and incremental
+    (RF_SHIM_DIRECT=0, or a cache buffer over RF_SHIM_DIRECT_MAX_MIB): read back into a
+    recycled pinned buffer, or into malloc'd memory after an engine-wide sync
+    (RF_SHIM_PINNED=0), then copied page by page -- fresh and incremental
     adds, pages and index extents identical to the reference's (in a subprocess: the
     switches are read once per process)"""
     import os
