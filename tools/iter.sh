@@ -4,5 +4,5 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 O=gpurun_out
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_shim.py -k "bounce" > $O/gt_b.log 2>&1 || { tail -40 $O/gt_b.log; exit 1; }
-tail -5 $O/gt_b.log
+PT_CHAIN=8 timeout -k 10 200 python tools/phase_times.py 1 64 1048575 > $O/pt1_chain8.txt 2>&1 || { tail -20 $O/pt1_chain8.txt; exit 1; }
+tail -13 $O/pt1_chain8.txt
