@@ -146,8 +146,10 @@ int rf_amd_probe_many_hashes_host(rf_amd_engine *e, rf_amd_batch *const *batches
                                   uint32_t num_groups, const uint32_t *h_hashes, uint64_t *h_found);
 /* The engine's lookup server: single lookups -- routing_filter_lookup (src/routing_filter.h:
  * 87-92) and routing_filter_lookup_async states (:130-155) -- without a kernel launch per
- * call. A persistent wave (started on demand on a queue of its own, exiting after 1 ms
- * without requests, RF_AMD_SERVER_IDLE_US) polls a ring of requests in pinned host memory and
+ * call. A persistent wave (started on demand on a queue of its own, exiting after 400 us
+ * without requests and after an 800 us lifetime -- so a device-wide synchronisation waits at
+ * most that long for it; relaunched while lookups continue) polls a ring of requests in
+ * pinned host memory and
  * answers each with filter filter_index of batch b, in submission order. submit queues the
  * lookup of `hash` and returns its ticket; the batch must stay alive until the result is
  * taken. A NULL tag: the caller takes the result with rf_amd_lookup_wait (blocking). A
@@ -159,6 +161,15 @@ int rf_amd_lookup_submit(rf_amd_engine *e, rf_amd_batch *b, uint32_t filter_inde
                          void *tag, uint64_t *ticket);
 int rf_amd_lookup_wait(rf_amd_engine *e, uint64_t ticket, uint64_t *found_values);
 uint64_t rf_amd_lookup_reap(rf_amd_engine *e, void **tags, uint64_t *found_values, uint64_t max);
+/* the server's first error (0: none; sticky: a launch that failed, a faulted stream). Once it
+ * is set, submit and wait return it, and rf_amd_lookup_server_failed hands back (consumes) the
+ * tags of tagged lookups that will not be answered, so their owners can complete them with an
+ * error instead of waiting */
+int rf_amd_lookup_server_error(rf_amd_engine *e);
+uint64_t rf_amd_lookup_server_failed(rf_amd_engine *e, void **tags, uint64_t max);
+/* idle exit and lifetime (microseconds) of the server waves launched from now on (defaults
+ * 400 / 800; RF_AMD_SERVER_IDLE_US / _LIFE_US): a host-controlled keep-alive */
+int rf_amd_lookup_server_set_times(rf_amd_engine *e, uint64_t idle_us, uint64_t life_us);
 /* device-allocation pool of the engine (batch work buffers are recycled across batches; up
  * to RF_AMD_POOL_MIB MiB stay pooled, by default a quarter of the device memory free at
  * engine creation and at most 16 GiB); trim hands pooled blocks back to the device until at

@@ -26,6 +26,7 @@
 #include "routing_filter.h"
 #include "core.h"
 #include "lookup_result.h"
+#include "clockcache.h"
 
 #include <stdatomic.h>
 #include <time.h>
@@ -209,21 +210,67 @@ rfk_open(uint64 cache_mib,
    return k;
 }
 
-/* the shim's release of a cache whose page buffer took images directly (weak: absent from
- * the reference's own library) */
+/* the shim's release of a cache whose page buffer took images directly, and its registration
+ * counters (weak: absent from the reference's own library) */
 __attribute__((weak)) void
 routing_filter_amd_cache_release(cache *cc);
+__attribute__((weak)) void
+routing_filter_amd_direct_stats(uint64 *out);
+__attribute__((weak)) void
+routing_filter_amd_add_breakdown(uint64 *out);
+__attribute__((weak)) void
+routing_filter_amd_prewarm(cache *cc);
 
+/* the shim's routing_filter_add breakdown (out[0..10], zeros with the reference) */
 void
-rfk_close(rfk_kvs *k)
+rfk_add_breakdown(uint64 *out)
+{
+   for (int i = 0; i < 11; i++) {
+      out[i] = 0;
+   }
+   if (routing_filter_amd_add_breakdown) {
+      routing_filter_amd_add_breakdown(out);
+   }
+}
+
+/* the shim's engine and this store's cache registration made now (no-op with the reference) */
+void
+rfk_prewarm(rfk_kvs *k)
+{
+   if (routing_filter_amd_prewarm) {
+      routing_filter_amd_prewarm((cache *)splinterdb_get_cache_handle(k->kvs));
+   }
+}
+
+/* release = 0 closes the store as the unmodified reference does: without telling the shim */
+void
+rfk_close_ex(rfk_kvs *k, int release)
 {
    if (k) {
-      if (routing_filter_amd_cache_release) {
+      if (release && routing_filter_amd_cache_release) {
          routing_filter_amd_cache_release((cache *)splinterdb_get_cache_handle(k->kvs));
       }
       splinterdb_close(&k->kvs);
       free(k);
    }
+}
+
+void
+rfk_close(rfk_kvs *k)
+{
+   rfk_close_ex(k, 1);
+}
+
+/* out[0] caches registered now, out[1] registrations found stale, out[2] adds placing now
+ * (zeros without the shim); out[3] the address of the store's cache page buffer */
+void
+rfk_direct_stats(rfk_kvs *k, uint64 *out)
+{
+   out[0] = out[1] = out[2] = 0;
+   if (routing_filter_amd_direct_stats) {
+      routing_filter_amd_direct_stats(out);
+   }
+   out[3] = k ? (uint64)(uintptr_t)((clockcache *)splinterdb_get_cache_handle(k->kvs))->data : 0;
 }
 
 /* n inserts of key i = keys[i * key_len ...], value i = values[i * val_len ...] */

@@ -41,6 +41,14 @@ def lib(path):
         L.rfk_open.restype = vp
         L.rfk_close.argtypes = [vp]
         L.rfk_close.restype = None
+        L.rfk_close_ex.argtypes = [vp, i32]
+        L.rfk_close_ex.restype = None
+        L.rfk_direct_stats.argtypes = [vp, ctypes.POINTER(u64)]
+        L.rfk_direct_stats.restype = None
+        L.rfk_add_breakdown.argtypes = [ctypes.POINTER(u64)]
+        L.rfk_add_breakdown.restype = None
+        L.rfk_prewarm.argtypes = [vp]
+        L.rfk_prewarm.restype = None
         L.rfk_insert.argtypes = [vp, vp, u32, vp, u32, u64]
         L.rfk_insert.restype = i32
         L.rfk_lookup.argtypes = [vp, vp, u32, u64, vp, vp]
@@ -59,8 +67,11 @@ def _p(a):
 
 class Kvs:
     def __init__(self, path=KVS_REF, cache_mib=1024, disk_mib=8192, memtable_mib=4, filter_hash_size=26,
-                 filter_log_index_size=8, record_digest=True):
+                 filter_log_index_size=8, record_digest=True, release=True):
+        """release=False: close without routing_filter_amd_cache_release, as the unmodified
+        reference's splinterdb_close does"""
         self.L = lib(path)
+        self.release = release
         self.h = self.L.rfk_open(cache_mib, disk_mib, memtable_mib, filter_hash_size, filter_log_index_size,
                                  int(record_digest))
         if not self.h:
@@ -68,8 +79,27 @@ class Kvs:
 
     def close(self):
         if self.h:
-            self.L.rfk_close(self.h)
+            self.L.rfk_close_ex(self.h, int(self.release))
             self.h = None
+
+    def prewarm(self):
+        """the shim's engine and this store's cache registration now (no-op: reference)"""
+        self.L.rfk_prewarm(self.h)
+
+    def add_breakdown(self):
+        """the shim's routing_filter_add time split (ns totals; zeros with the reference)"""
+        out = (ctypes.c_uint64 * 11)()
+        self.L.rfk_add_breakdown(out)
+        keys = ("calls", "batches", "create", "stage", "build", "infos", "readback", "wait", "place",
+                "engine_create", "register")
+        return dict(zip(keys, [int(x) for x in out]))
+
+    def direct_stats(self):
+        """(caches registered, registrations found stale, adds placing now, this store's
+        page-buffer address)"""
+        out = (ctypes.c_uint64 * 4)()
+        self.L.rfk_direct_stats(self.h, out)
+        return tuple(out)
 
     def __enter__(self):
         return self

@@ -90,16 +90,28 @@ static rf_amd_engine  *g_eng;
 static int             g_eng_rc;
 static pthread_once_t  g_eng_once = PTHREAD_ONCE_INIT;
 
+static uint64 g_engine_ns, g_register_ns; /* one-time costs: engine creation, cache registrations */
+
+static uint64
+mono_ns(void)
+{
+   struct timespec ts;
+   clock_gettime(CLOCK_MONOTONIC, &ts);
+   return (uint64)ts.tv_sec * 1000000000ull + (uint64)ts.tv_nsec;
+}
+
 static void
 engine_init(void)
 {
-   const char *d = getenv("RF_AMD_DEVICE");
-   g_eng_rc      = rf_amd_engine_create(d ? atoi(d) : 0, &g_eng);
+   const uint64 t0 = mono_ns();
+   const char  *d  = getenv("RF_AMD_DEVICE");
+   g_eng_rc        = rf_amd_engine_create(d ? atoi(d) : 0, &g_eng);
    /* a storage engine links this: its pool keeps at most 2 GiB parked unless
       RF_AMD_POOL_MIB says otherwise (one add's batch is at most a few hundred MB) */
    if (g_eng_rc == 0 && !getenv("RF_AMD_POOL_MIB")) {
       (void)rf_amd_engine_set_pool_limit(g_eng, 2048ull << 20);
    }
+   g_engine_ns = mono_ns() - t0;
 }
 
 static rf_amd_engine *
@@ -593,7 +605,7 @@ typedef struct add_req {
    uint64            *slots;
    uint64             pin_cap; /* bytes of the pinned buffer (returned to the pool) */
    uint64             fence;   /* the read-back's completion point on the engine stream */
-   int                direct;  /* no read-back: the adding thread places the image itself */
+   uint32             direct;  /* 1 + registration slot: no read-back, the adding thread places the image itself */
    shim_batch        *sb; /* the built batch, pinned once for this request */
    uint32             f;
    int                done;
@@ -616,12 +628,15 @@ enum { AB_CALLS, AB_BATCHES, AB_CREATE, AB_STAGE, AB_BUILD, AB_INFOS, AB_READBAC
 static uint64 g_add_ns[AB_N];
 #define AB_ADD(k, v) __atomic_fetch_add(&g_add_ns[k], (v), __ATOMIC_RELAXED)
 
+/* out[0..8] as AB_*, out[9] ns creating the engine, out[10] ns registering cache buffers */
 void
 routing_filter_amd_add_breakdown(uint64 *out)
 {
    for (int k = 0; k < AB_N; k++) {
       out[k] = __atomic_load_n(&g_add_ns[k], __ATOMIC_RELAXED);
    }
+   out[AB_N]     = g_engine_ns;
+   out[AB_N + 1] = g_register_ns;
 }
 
 /* copies a request's fingerprints into its staging slot, unless another thread has claimed it */
@@ -737,10 +752,16 @@ static struct {
    const cache *cc;
    char        *base;
    uint64       bytes;
-   int          ok;
+   int          ok;       /* registered, placements go straight into its pages */
+   int          stale;    /* a placement's canary showed the registration no longer maps the buffer */
+   int          released; /* routing_filter_amd_cache_release: no registration of this buffer again
+                             (adds while the store closes) until prewarm or another buffer */
+   uint32       inflight; /* adds placing through this registration now */
 } g_direct[DIRECT_CACHES];
 static uint32          g_direct_n;
+static uint64          g_direct_stale_seen; /* registrations found stale (routing_filter_amd_direct_stats) */
 static pthread_mutex_t g_direct_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t  g_direct_cv = PTHREAD_COND_INITIALIZER;
 
 static int
 direct_enabled(void)
@@ -753,64 +774,153 @@ direct_enabled(void)
    return v;
 }
 
-/* 1 when cc's page buffer is registered with the engine (registering it on first use) */
+/* registers cc's page buffer (caller holds g_direct_mu) */
 static int
+direct_register(rf_amd_engine *e, uint32 i, char *base, uint64 bytes)
+{
+   /* registering pins the whole buffer (once, ~proportional to its size): caches over
+      RF_SHIM_DIRECT_MAX_MIB (default 65,536) keep the bounce-buffer path */
+   const uint64 max_b = env_u64("RF_SHIM_DIRECT_MAX_MIB", 65536) << 20;
+   const uint64 t0    = mono_ns();
+   g_direct[i].base     = base;
+   g_direct[i].bytes    = bytes;
+   g_direct[i].stale    = 0;
+   g_direct[i].released = 0;
+   g_direct[i].ok     = base && bytes && bytes <= max_b && rf_amd_host_register(e, base, bytes) == 0;
+   g_register_ns += mono_ns() - t0;
+   return g_direct[i].ok;
+}
+
+/* The registration an add places through: 1 + its slot when cc's page buffer is registered
+ * with the engine (registering it on first use), 0 for the bounce-buffer path. The caller owns
+ * one in-flight count on the slot until direct_done. The unmodified reference never tells the
+ * shim that a cache closed (routing_filter_amd_cache_release is an extension), so a cache
+ * whose buffer was unmapped and mapped again at the same address with the same size looks
+ * unchanged here; every placement therefore verifies that its stores reached the pages the
+ * host sees (place_direct's canary) and a registration found stale is replaced here. */
+static uint32
 cache_direct(rf_amd_engine *e, cache *cc)
 {
    if (!direct_enabled()) {
       return 0;
    }
-   int         ok = 0, found = 0;
-   clockcache *ccc = (clockcache *)cc;
+   uint32      slot = 0;
+   clockcache *ccc  = (clockcache *)cc;
+   char       *base  = ccc->data;
+   uint64      bytes = ccc->cfg ? ccc->cfg->capacity : 0;
    pthread_mutex_lock(&g_direct_mu);
-   for (uint32 i = 0; i < g_direct_n; i++) {
-      if (g_direct[i].cc == cc) {
-         if (g_direct[i].base != ccc->data || !ccc->cfg || g_direct[i].bytes != ccc->cfg->capacity) {
-            /* another cache at this address since: drop the old registration */
-            if (g_direct[i].ok) {
-               (void)rf_amd_host_unregister(e, g_direct[i].base);
-            }
-            g_direct[i] = g_direct[--g_direct_n];
-            break;
-         }
-         ok    = g_direct[i].ok;
-         found = 1;
-         break;
-      }
+   uint32 i = 0;
+   while (i < g_direct_n && g_direct[i].cc != cc) {
+      i++;
    }
-   if (!found && g_direct_n < DIRECT_CACHES) {
-      char       *base  = ccc->data;
-      uint64      bytes = ccc->cfg ? ccc->cfg->capacity : 0;
-      /* registering pins the whole buffer (once, ~proportional to its size): caches over
-         RF_SHIM_DIRECT_MAX_MIB (default 65,536) keep the bounce-buffer path */
-      const uint64 max_b = env_u64("RF_SHIM_DIRECT_MAX_MIB", 65536) << 20;
-      ok = base && bytes && bytes <= max_b && rf_amd_host_register(e, base, bytes) == 0;
-      g_direct[g_direct_n].cc    = cc;
-      g_direct[g_direct_n].base  = base;
-      g_direct[g_direct_n].bytes = bytes;
-      g_direct[g_direct_n].ok    = ok;
-      g_direct_n++;
+   if (i == g_direct_n) { /* first use of this cache */
+      if (g_direct_n < DIRECT_CACHES) {
+         g_direct_n++;
+         g_direct[i].cc       = cc;
+         g_direct[i].inflight = 0;
+         if (direct_register(e, i, base, bytes)) {
+            slot = i + 1;
+         }
+      }
+   } else if (g_direct[i].released && g_direct[i].base == base && g_direct[i].bytes == bytes) {
+      /* released and not reopened: the bounce path */
+   } else if (g_direct[i].stale || g_direct[i].base != base || g_direct[i].bytes != bytes) {
+      /* another buffer (or the same address mapped again) since: register anew once no add
+         still places through the old registration; until then, the bounce path */
+      if (g_direct[i].inflight == 0) {
+         if (g_direct[i].ok) {
+            (void)rf_amd_host_unregister(e, g_direct[i].base);
+         }
+         if (direct_register(e, i, base, bytes)) {
+            slot = i + 1;
+         }
+      }
+   } else if (g_direct[i].ok) {
+      slot = i + 1;
+   }
+   if (slot) {
+      g_direct[slot - 1].inflight++;
    }
    pthread_mutex_unlock(&g_direct_mu);
-   return ok;
+   return slot;
 }
 
-/* a cache is going away (its buffer may be reused): unregister it. The entry stays, marked
- * released, so adds issued while the cache closes take the bounce-buffer path instead of
- * registering it again; a later cache at this address with another buffer replaces it. */
+/* an add is done placing through its registration (stale: its canary showed the stores did
+ * not reach the host's pages) */
+static void
+direct_done(uint32 slot, int stale)
+{
+   if (!slot) {
+      return;
+   }
+   pthread_mutex_lock(&g_direct_mu);
+   g_direct[slot - 1].inflight--;
+   if (stale && !g_direct[slot - 1].stale) {
+      g_direct[slot - 1].stale = 1;
+      g_direct_stale_seen++;
+   }
+   pthread_cond_broadcast(&g_direct_cv);
+   pthread_mutex_unlock(&g_direct_mu);
+}
+
+/* the engine and cc's registration made now instead of in the first routing_filter_add (a
+ * store calls it once when it opens; optional) */
+void
+routing_filter_amd_prewarm(cache *cc)
+{
+   rf_amd_engine *e = engine();
+   if (e && cc) {
+      pthread_mutex_lock(&g_direct_mu);
+      for (uint32 i = 0; i < g_direct_n; i++) {
+         if (g_direct[i].cc == cc && g_direct[i].released) {
+            g_direct[i].released = 0;
+            g_direct[i].base     = NULL; /* registers the (new) store's buffer afresh */
+         }
+      }
+      pthread_mutex_unlock(&g_direct_mu);
+      direct_done(cache_direct(e, cc), 0);
+   }
+}
+
+/* out[0] = caches registered now, out[1] = registrations found stale by a placement */
+void
+routing_filter_amd_direct_stats(uint64 *out)
+{
+   pthread_mutex_lock(&g_direct_mu);
+   uint64 n = 0, fl = 0;
+   for (uint32 i = 0; i < g_direct_n; i++) {
+      n += g_direct[i].ok != 0;
+      fl += g_direct[i].inflight;
+   }
+   out[0] = n;
+   out[1] = g_direct_stale_seen;
+   out[2] = fl;
+   pthread_mutex_unlock(&g_direct_mu);
+}
+
+/* a cache is going away (its buffer may be reused): unregister it once no add still places
+ * through it. The entry stays, marked released, so adds issued while the store closes take
+ * the bounce-buffer path instead of registering the buffer again; a later cache with another
+ * buffer replaces it, and routing_filter_amd_prewarm (a new store at the same addresses)
+ * registers it afresh. */
 void
 routing_filter_amd_cache_release(cache *cc)
 {
    pthread_mutex_lock(&g_direct_mu);
    for (uint32 i = 0; i < g_direct_n; i++) {
       if (g_direct[i].cc == cc) {
-         if (g_direct[i].ok) {
+         const int was_ok     = g_direct[i].ok;
+         g_direct[i].ok       = 0; /* no new add takes this registration */
+         g_direct[i].released = 1;
+         while (g_direct[i].inflight) {
+            pthread_cond_wait(&g_direct_cv, &g_direct_mu);
+         }
+         if (was_ok) {
             rf_amd_engine *e = engine();
             if (e) {
                (void)rf_amd_host_unregister(e, g_direct[i].base);
             }
          }
-         g_direct[i].ok = 0;
          break;
       }
    }
@@ -1048,7 +1158,7 @@ routing_filter_amd_add_stats(uint64 *batches, uint64 *filters)
  * the index pages (:612-633), PLACE_CHUNK pages per launch, each chunk unlocked once its
  * images have landed. A launch the engine refuses (a page outside the registered buffer)
  * falls back to a read-back of the image and a copy per page. */
-static void
+static int
 place_direct(rf_amd_engine  *e,
              cache          *cc,
              add_req        *q,
@@ -1069,6 +1179,13 @@ place_direct(rf_amd_engine  *e,
    for (uint64 i = 0; i < nip; i++) {
       table[2 * np + i] = (uint64)(uintptr_t)index_page[i]->data;
    }
+   /* canary: a word the host writes into the first data page of each chunk (and into index
+      slot 0 before the last chunk) before the launch; once the chunk's images have landed it
+      must be gone. If it is not, the registration no longer maps these pages (the buffer was
+      unmapped and mapped again at the same address): the chunk and the rest of the
+      image take the bounce path and the registration is replaced on the next add. */
+   const uint64 canary = 0x5bd1e9955bd1e995ull ^ now_ns() ^ (uint64)(uintptr_t)q;
+   int          stale  = 0;
    for (uint64 k0 = 0; k0 < np || k0 == 0; k0 += PLACE_CHUNK) {
       const uint64 cnt  = np - k0 < PLACE_CHUNK ? np - k0 : PLACE_CHUNK;
       const int    last = k0 + cnt == np;
@@ -1077,6 +1194,16 @@ place_direct(rf_amd_engine  *e,
          ph[k]            = cache_alloc(cc, page_addr[k], PAGE_TYPE_FILTER);
          table[k]         = (uint64)(uintptr_t)ph[k]->data;
          table[np + k]    = page_addr[k];
+      }
+      volatile uint64 *cw0 = cnt ? (volatile uint64 *)ph[k0]->data : NULL;
+      volatile uint64 *cw1 = last && ni ? (volatile uint64 *)index_page[0]->data : NULL;
+      if (!bounce) {
+         if (cw0) {
+            *cw0 = canary;
+         }
+         if (cw1) {
+            *cw1 = canary;
+         }
       }
       int r = bounce ? 1
                      : rf_amd_batch_place_image(b, q->f, table, (uint32)np, (uint32)k0, (uint32)cnt, last,
@@ -1087,6 +1214,10 @@ place_direct(rf_amd_engine  *e,
       }
       if (!r) {
          r = rf_amd_engine_fence_wait(e, fence);
+      }
+      if (!r && ((cw0 && *cw0 == canary) || (cw1 && *cw1 == canary))) {
+         stale = 1;
+         r     = 1;
       }
       if (r) {
          if (!bounce) { /* one read-back of the whole image and its slots */
@@ -1119,6 +1250,7 @@ place_direct(rf_amd_engine  *e,
    free(ph);
    pin_give_any(e, table, tcap, 1);
    pin_give_any(e, bounce, bcap, 1);
+   return stale;
 }
 
 platform_status
@@ -1168,6 +1300,7 @@ routing_filter_add(cache                *cc,
    AB_ADD(AB_CALLS, 1);
    registry_unpin(q.old_sb);
    if (q.rc) {
+      direct_done(q.direct, 0);
       pin_give(e, q.pages, q.pin_cap);
       registry_unpin(q.sb);
       return status_of(q.rc);
@@ -1204,7 +1337,7 @@ routing_filter_add(cache                *cc,
    uint64 *page_addr = malloc(sizeof(uint64) * info.num_pages);
    platform_assert(page_addr != NULL);
    if (q.direct) {
-      place_direct(e, cc, &q, &mini, index_page, addrs_per_page, page_addr);
+      direct_done(q.direct, place_direct(e, cc, &q, &mini, index_page, addrs_per_page, page_addr));
    } else {
       for (uint32 k = 0; k < info.num_pages; k++) {
          page_addr[k]      = mini_alloc(&mini, 0, NULL);
@@ -1548,7 +1681,25 @@ async_reap_complete(void)
    const uint64 t0 = now_ns();
    uint64       n  = rf_amd_lookup_reap(engine(), tags, found, REAP);
    if (n == 0) {
-      return 0;
+      /* a dead lookup server (a launch failed, its stream faulted) never answers: complete
+         its states with the error instead of leaving their owners waiting */
+      const int err = __atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE) ? rf_amd_lookup_server_error(engine()) : 0;
+      uint64    k   = err ? rf_amd_lookup_server_failed(engine(), tags, REAP) : 0;
+      for (uint64 i = 0; i < k; i++) {
+         rf_state         *st  = tags[i];
+         async_callback_fn cb  = st->callback;
+         void             *arg = st->callback_arg;
+         shim_batch       *sb  = AQ_PIN(st);
+         *st->found_values     = 0;
+         st->__async_result    = status_of(err);
+         __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
+         __atomic_sub_fetch(&g_aq_outstanding, 1, __ATOMIC_RELAXED);
+         registry_unpin(sb);
+         if (cb) {
+            cb(arg);
+         }
+      }
+      return k;
    }
    const uint64 t1 = now_ns();
    shim_batch  *pins[REAP];

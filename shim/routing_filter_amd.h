@@ -26,9 +26,10 @@ routing_filter_amd_async_probe_ns(void);
 void
 routing_filter_amd_async_breakdown(uint64 *out);
 
-/* out[0..8]: routing_filter_add calls, combiner batches, then ns totals: batch creation,
+/* out[0..10]: routing_filter_add calls, combiner batches, then ns totals: batch creation,
  * staging copies, build, info read-back, image read-back (per batch); the wait for the batch,
- * page allocation and fill (per add) -- diagnostics */
+ * page allocation and fill (per add); the one-time costs: engine creation, cache-buffer
+ * registrations -- diagnostics */
 void
 routing_filter_amd_add_breakdown(uint64 *out);
 
@@ -58,6 +59,19 @@ routing_filter_amd_lookup_batch(cache                *cc,
 
 /* routing_filter_add writes its images straight into the cache's page buffer, which it
  * registers with the GPU on the cache's first add (RF_SHIM_DIRECT=0: a bounce buffer and a
- * copy per page instead). Before a cache is destroyed, this releases that registration. */
+ * copy per page instead). Before a cache is destroyed, this releases that registration (after
+ * the adds placing through it are done). Optional: the unmodified reference never calls it;
+ * every placement checks that its stores reached the pages the host sees and a registration
+ * that no longer maps the cache's buffer is replaced. */
 void
 routing_filter_amd_cache_release(cache *cc);
+
+/* creates the engine and registers cc's page buffer now rather than in the first
+ * routing_filter_add (optional: for a store to call when it opens) */
+void
+routing_filter_amd_prewarm(cache *cc);
+
+/* out[0]: caches registered now; out[1]: registrations a placement found stale; out[2]: adds
+ * placing through a registration now */
+void
+routing_filter_amd_direct_stats(uint64 *out);

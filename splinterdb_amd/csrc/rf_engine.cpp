@@ -189,7 +189,11 @@ struct LookupServer {
   std::mutex reap_mu;
   uint64_t reap_next = 0;               // the next ticket reap() looks at (under reap_mu)
   std::atomic<uint64_t> launches{0};
-  uint64_t idle_ticks = 0, life_ticks = 0;
+  std::atomic<uint64_t> idle_ticks{0}, life_ticks{0};  // of the next launch (rf_amd_lookup_server_set_times)
+  // sticky: the first error of the server (a launch that failed, a faulted stream). Every
+  // waiter then returns it, submits fail at once, and rf_amd_lookup_server_failed hands the
+  // unanswered tickets' tags back, so no caller spins on an answer that cannot come
+  std::atomic<int> dead{0};
 };
 
 struct rf_amd_engine {
@@ -280,10 +284,12 @@ struct rf_amd_batch {
   std::vector<uint32_t> err_host;  // per-filter build error bits once read back (err_ready)
   std::atomic<bool> err_ready{false};
   std::mutex err_mu;
+  hipEvent_t built_ev = nullptr;   // recorded after the last build's kernels (on the stream it ran on)
   std::vector<hipEvent_t> events;  // per-stage timing: ev_sets rings of NUM_EVENTS (rf_amd_batch_set_timing)
   uint32_t ev_sets = 0, ev_set = 0;  // each build starts the next set; probes record into the current one
   uint32_t ev_mask = EV_MASK_ALL;     // EV_MASK_PROBE: the probe's two events only
   ~rf_amd_batch() {
+    if (built_ev) (void)hipEventDestroy(built_ev);
     for (auto ev : events) (void)hipEventDestroy(ev);
   }
   std::vector<DevBuf*> bufs() {
@@ -994,6 +1000,19 @@ static int do_probe(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
                     const uint32_t* fid, uint64_t n, uint64_t* found, void* stream,
                     const uint64_t* d_runs = nullptr);
 
+// The build's completion point: host reads of the batch (info, images) wait for this event
+// and then copy on the engine stream -- never a device-wide synchronisation or a null-stream
+// copy, which would also wait for the lookup server's wave
+static int note_built(rf_amd_batch* b, hipStream_t st) {
+  if (!b->built_ev) HIPCHK(hipEventCreateWithFlags(&b->built_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(b->built_ev, st));
+  return 0;
+}
+static int wait_built(rf_amd_batch* b) {
+  if (b->built_ev) HIPCHK(hipEventSynchronize(b->built_ev));
+  return 0;
+}
+
 static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* offs, uint32_t key_len,
                     void* stream) {
   if (!b) return fail(RF_AMD_EINVAL, "null batch");
@@ -1025,6 +1044,7 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   // after reading this count cannot miss a build it covers
   if (st == b->eng->stream) b->eng->builds_issued.fetch_add(1, std::memory_order_acq_rel);
   if (rc) return fail(RF_AMD_EINVAL, std::string("build launch: ") + hipGetErrorString((hipError_t)rc));
+  if (int erc = note_built(b, st)) return erc;
   b->built = true;
   b->has_entries = true;
   return 0;
@@ -1289,14 +1309,15 @@ static int srv_init(rf_amd_engine* e) {
       v.init_rc = RF_AMD_EINVAL;
       return;
     }
-    // s_memrealtime runs at 100 MHz: idle 1 ms; lifetime 20 ms on a queue of its own (a bound
-    // on every wave, relaunched if lookups continue), 2 ms when it shares a queue. The masked
-    // stream synchronises with the legacy null stream, so a device-wide synchronisation or
-    // null-stream work in the process waits at most one lifetime for a busy wave.
+    // s_memrealtime runs at 100 MHz. Idle exit 400 us, lifetime 800 us (busy or not; waiters
+    // relaunch it, a few us per relaunch): the masked stream synchronises with the legacy null
+    // stream and hipDeviceSynchronize waits for every stream, so a device-wide sync or a
+    // null-stream op waits at most one lifetime, under 1 ms, for a running wave.
+    // rf_amd_lookup_server_set_times (or RF_AMD_SERVER_IDLE_US / _LIFE_US) sets others.
     const char* idle = getenv("RF_AMD_SERVER_IDLE_US");
     const char* life = getenv("RF_AMD_SERVER_LIFE_US");
-    v.idle_ticks = (idle ? strtoull(idle, nullptr, 10) : 1000) * 100;
-    v.life_ticks = masked ? (life ? strtoull(life, nullptr, 10) : 20000) * 100 : 200000ull;
+    if (!v.idle_ticks.load()) v.idle_ticks = (idle ? strtoull(idle, nullptr, 10) : 400) * 100;
+    if (!v.life_ticks.load()) v.life_ticks = (life ? strtoull(life, nullptr, 10) : 800) * 100;
   });
   return v.init_rc ? fail(v.init_rc, "lookup server allocation failed") : 0;
 }
@@ -1315,8 +1336,12 @@ static int srv_ensure(rf_amd_engine* e) {
   if (!v.state.compare_exchange_strong(s, next, std::memory_order_acq_rel)) return 0;  // another launched
   const uint64_t head = __atomic_load_n(&v.ctl->exit_head, __ATOMIC_ACQUIRE);
   (void)hipSetDevice(e->device);
-  if (int rc = rf_launch_lookup_server(v.st, v.ring, v.res, v.ctl, head, gen + 1, v.idle_ticks, v.life_ticks))
+  if (int rc = rf_launch_lookup_server(v.st, v.ring, v.res, v.ctl, head, gen + 1, v.idle_ticks.load(),
+                                       v.life_ticks.load())) {
+    int z = 0;
+    v.dead.compare_exchange_strong(z, RF_AMD_EINVAL);
     return fail(RF_AMD_EINVAL, std::string("lookup server launch: ") + hipGetErrorString((hipError_t)rc));
+  }
   v.launches.fetch_add(1, std::memory_order_relaxed);
   return 0;
 }
@@ -1338,7 +1363,13 @@ static void srv_stop(rf_amd_engine* e) {
 static int srv_check(rf_amd_engine* e) {
   const hipError_t q = hipStreamQuery(e->srv.st);
   if (q == hipSuccess || q == hipErrorNotReady) return 0;
+  int z = 0;
+  e->srv.dead.compare_exchange_strong(z, RF_AMD_EINVAL);
   return fail(RF_AMD_EINVAL, std::string("lookup server: ") + hipGetErrorString(q));
+}
+static int srv_dead(rf_amd_engine* e) {
+  const int d = e->srv.dead.load(std::memory_order_acquire);
+  return d ? fail(d, "lookup server failed earlier") : 0;
 }
 
 static ProbeGroup probe_group_of(const rf_amd_batch* b, uint32_t f);
@@ -1352,15 +1383,17 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
   if (!ticket) return fail(RF_AMD_EINVAL, "null ticket");
   if (int rc = srv_init(e)) return rc;
   if (int rc = batch_errors(b)) return rc;
+  if (int rc = srv_dead(e)) return rc;
   LookupServer& v = e->srv;
   const uint64_t t = v.tail.fetch_add(1, std::memory_order_acq_rel);
   const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
   if (t >= SRV_RING) {  // the slot's previous ticket must have been taken
     for (uint32_t spin = 1; v.consumed[slot].load(std::memory_order_acquire) != t - SRV_RING + 1; spin++) {
       __builtin_ia32_pause();
-      if ((spin & 1023) == 0) {
+      if ((spin & 1023) == 0) {  // ticket t stays unpublished only on a server that is dead
         if (int rc = srv_ensure(e)) return rc;
         if (int rc = srv_check(e)) return rc;
+        if (int rc = srv_dead(e)) return rc;
       }
     }
     // the slot is being rewritten: readers that see this do not trust its payload or tag
@@ -1391,6 +1424,7 @@ extern "C" int rf_amd_lookup_wait(rf_amd_engine* e, uint64_t ticket, uint64_t* f
     }
     __builtin_ia32_pause();
     if ((spin & 255) == 0) {
+      if (int rc = srv_dead(e)) return rc;
       if (int rc = srv_ensure(e)) return rc;
       if ((spin & 65535) == 0)
         if (int rc = srv_check(e)) return rc;
@@ -1431,6 +1465,38 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
   lk.unlock();
   if (n == 0 && t < tail) (void)srv_ensure(e);
   return n;
+}
+
+// a dead server's unanswered tickets: the tags of the published ones from the reap cursor on
+// (waiters' tickets skipped: rf_amd_lookup_wait returns the error to them), consumed here
+extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, uint64_t max) {
+  if (!e || !e->srv.ring || !tags || !e->srv.dead.load(std::memory_order_acquire)) return 0;
+  LookupServer& v = e->srv;
+  std::lock_guard<std::mutex> lk(v.reap_mu);
+  uint64_t n = 0, t = v.reap_next;
+  const uint64_t tail = v.tail.load(std::memory_order_acquire);
+  for (; n < max && t < tail; t++) {
+    const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
+    if (v.meta[slot].ticket.load(std::memory_order_acquire) != t) continue;  // unpublished or reused
+    void* tag = v.meta[slot].tag;
+    if (!tag) continue;
+    if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) == t) break;  // answered: reap takes it
+    tags[n++] = tag;
+    v.consumed[slot].store(t + 1, std::memory_order_release);
+  }
+  v.reap_next = t;
+  return n;
+}
+
+extern "C" int rf_amd_lookup_server_error(rf_amd_engine* e) { return e ? e->srv.dead.load() : RF_AMD_ENODEV; }
+
+// the idle exit and lifetime (microseconds) of the server waves launched from now on (a
+// host-controlled keep-alive: a caller that needs one wave across a long stretch raises them)
+extern "C" int rf_amd_lookup_server_set_times(rf_amd_engine* e, uint64_t idle_us, uint64_t life_us) {
+  if (!e || !idle_us || !life_us) return fail(RF_AMD_EINVAL, "bad server times");
+  e->srv.idle_ticks = idle_us * 100;
+  e->srv.life_ticks = life_us * 100;
+  return 0;
 }
 
 extern "C" int rf_amd_lookup_server_stats(rf_amd_engine* e, uint64_t* out) {
@@ -1658,7 +1724,8 @@ static int probe_runs(rf_amd_batch* b, int kind, const void* in0, uint32_t key_l
     HIPCHK(hipStreamSynchronize(st));  // earlier probes may still read the old bounds
     const uint64_t nw = (n + 63) / 64;
     if (b->d_wave_tab.n < 4 * nw && b->d_wave_tab.alloc(4 * nw, &b->eng->pool)) return RF_AMD_ENOMEM;
-    HIPCHK(hipMemcpy(b->d_runs.p, runs.data(), 8ull * (b->F + 1), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(b->d_runs.p, runs.data(), 8ull * (b->F + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
     if (rf_launch_wave_tab(st, b->d_runs.as<uint64_t>(), b->F, n, b->d_wave_tab.as<uint32_t>()))
       return fail(RF_AMD_EINVAL, "wave table launch failed");
     b->runs_host = runs;
@@ -1696,15 +1763,16 @@ extern "C" int rf_amd_debug_read_lines(rf_amd_batch* b, uint8_t* h_lines, uint64
   if (!h_lines) return 0;
   if (bytes < 64ull * b->NL) return fail(RF_AMD_EINVAL, "lines buffer too small");
   HIPCHK(hipSetDevice(b->eng->device));
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(h_lines, b->d_lines.p, 64ull * b->NL, hipMemcpyDeviceToHost));
+  if (int rc = wait_built(b)) return rc;
+  HIPCHK(hipMemcpyAsync(h_lines, b->d_lines.p, 64ull * b->NL, hipMemcpyDeviceToHost, b->eng->stream));
+  HIPCHK(hipStreamSynchronize(b->eng->stream));
   return 0;
 }
 
 extern "C" int rf_amd_debug_rebuild_lines(rf_amd_batch* b) {
   if (!b || !b->built) return fail(RF_AMD_EINVAL, "unbuilt batch");
   HIPCHK(hipSetDevice(b->eng->device));
-  HIPCHK(hipDeviceSynchronize());
+  if (int rc = wait_built(b)) return rc;
   (void)hipGetLastError();
   LaunchArgs a = make_args(b, b->eng->stream);
   a.plines_force = 1;  // every filter, also those whose lines K6 cut
@@ -1755,9 +1823,10 @@ extern "C" int rf_amd_batch_info(rf_amd_batch* b, uint32_t f, rf_amd_filter_info
   if (!b || f >= b->F || !out) return fail(RF_AMD_EINVAL, "bad batch/filter");
   HIPCHK(hipSetDevice(b->eng->device));
   FilterOut o;
-  HIPCHK(hipStreamSynchronize(b->eng->stream));
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(&o, b->d_outs.as<FilterOut>() + f, sizeof(o), hipMemcpyDeviceToHost));
+  if (int rc = wait_built(b)) return rc;
+  hipStream_t st = b->eng->stream;
+  HIPCHK(hipMemcpyAsync(&o, b->d_outs.as<FilterOut>() + f, sizeof(o), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   const FilterPlan& p = b->plans[f];
   out->num_fingerprints = p.num_fp;
   out->num_unique = o.num_unique;
@@ -1777,9 +1846,10 @@ extern "C" int rf_amd_batch_infos(rf_amd_batch* b, rf_amd_filter_info* out, void
     HIPCHK(hipMemcpyAsync(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost,
                           (hipStream_t)stream));
     HIPCHK(hipStreamSynchronize((hipStream_t)stream));
-  } else {
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost));
+  } else {  // wherever the build ran: its event, then a copy on the engine stream
+    if (int rc = wait_built(b)) return rc;
+    HIPCHK(hipMemcpyAsync(o.data(), b->d_outs.p, sizeof(FilterOut) * b->F, hipMemcpyDeviceToHost, b->eng->stream));
+    HIPCHK(hipStreamSynchronize(b->eng->stream));
   }
   {
     std::lock_guard<std::mutex> lk(b->err_mu);
@@ -1806,16 +1876,18 @@ extern "C" int rf_amd_batch_read_image(rf_amd_batch* b, uint32_t f, uint8_t* h_p
   if (info.error) return fail(RF_AMD_EINVAL, "filter build reported error bits");
   const FilterPlan& p = b->plans[f];
   const uint64_t need = (uint64_t)info.num_pages * b->cfg.page_size;
+  hipStream_t st = b->eng->stream;  // after rf_amd_batch_info waited for the build
   if (h_pages) {
     if (pages_bytes < need) return fail(RF_AMD_EINVAL, "pages buffer too small");
-    HIPCHK(hipMemcpy(h_pages, b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size, need,
-                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(h_pages, b->d_pages.as<uint8_t>() + (uint64_t)p.page_base * b->cfg.page_size, need,
+                          hipMemcpyDeviceToHost, st));
   }
   if (h_slots) {
     if (num_slots < p.num_indices) return fail(RF_AMD_EINVAL, "slots buffer too small");
-    HIPCHK(hipMemcpy(h_slots, b->d_slots.as<uint64_t>() + p.idx_base, 8ull * p.num_indices,
-                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(h_slots, b->d_slots.as<uint64_t>() + p.idx_base, 8ull * p.num_indices,
+                          hipMemcpyDeviceToHost, st));
   }
+  HIPCHK(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -1933,6 +2005,10 @@ static int batch_import(rf_amd_engine* e, const rf_amd_config* cfg, uint32_t F, 
     }
   }
   HIPCHK(hipStreamSynchronize(st));  // host vectors above are released on return
+  if (int erc = note_built(b, st)) {
+    delete b;
+    return erc;
+  }
   b->err_host.assign(F, 0u);  // imports carry no error bits (checked above)
   b->err_ready.store(true, std::memory_order_release);
   b->built = true;

@@ -2779,6 +2779,171 @@ __device__ __forceinline__ uint64_t probe_walk(const uint4 P, uint32_t h, uint32
   return probe_stream(bucket & ((1u << lis) - 1), remainder, vs, rvs, pg, hdr, lis);
 }
 
+// ---- the probe's fast path ---------------------------------------------------------------
+// A full wave of probes that all look into ONE filter (per-filter runs, the usual case) runs with
+// every plan field, base address and loop bound in scalar registers, and its lines land in LDS in
+// natural order (quad q of the wave reads the line of probe 4q + k in instruction k, lane 4q + t
+// loading its quarter t), so each probe reads its encoding with one ds_read_b128 and its remainder
+// window with three ds_read_b32 off one address. The SWAR field pattern comes from a table in
+// constant memory (one scalar load) instead of being built per wave.
+struct FieldOnes {
+  uint64_t v[33];
+  constexpr FieldOnes() : v() {
+    for (uint32_t r = 1; r <= 32; r++) {
+      uint64_t L = 0;
+      for (uint32_t k = 0; k < 64; k += r) L |= 1ull << k;
+      v[r] = L;
+    }
+  }
+};
+__constant__ FieldOnes c_field_ones = FieldOnes();
+
+// uniform 32-bit loads through the constant address space: always scalar (SMEM) loads
+__device__ __forceinline__ uint32_t sload32(const void* p) {
+#if __HIP_DEVICE_COMPILE__
+  typedef __attribute__((address_space(4))) const uint32_t cu32;
+  return *reinterpret_cast<const cu32*>(reinterpret_cast<uintptr_t>(p));
+#else
+  return *static_cast<const uint32_t*>(p);
+#endif
+}
+__device__ __forceinline__ uint64_t sload64(const void* p) {
+  return (uint64_t)sload32(p) | (uint64_t)sload32(static_cast<const uint32_t*>(p) + 1) << 32;
+}
+
+// routing_get_bucket_bounds + the remainder scan (src/routing_filter.c:230-279, :1051-1067) on a
+// probe line held in LDS (Lw: its 16 dwords, natural order); vs, rvs, L (rvs-bit field ones) are
+// wave-uniform. Returns false when the image must be walked (overflowed line, a bucket too big
+// for the 96-bit window or for one 64-bit SWAR compare).
+__device__ __forceinline__ bool line_decode_u(const uint32_t* Lw, uint32_t j, uint32_t remainder, uint32_t vs,
+                                              uint32_t rvs, uint64_t L, uint64_t& found) {
+  const v4u E = *reinterpret_cast<const v4u*>(Lw);
+  const uint32_t d0 = E.x, d1 = E.y, d2 = E.z, d3 = E.w;
+  if ((d0 & d1 & d2 & d3) == 0xffffffffu) return false;  // overflow marker
+  uint32_t p1 = 0;  // first bit after terminator j - 1
+  if (j) {
+    const uint32_t r = j - 1, c0 = __popc(d0), c1 = c0 + __popc(d1), c2 = c1 + __popc(d2);
+    const uint32_t x = r >= c2 ? d3 : (r >= c1 ? d2 : (r >= c0 ? d1 : d0));
+    const uint32_t base = r >= c2 ? 96u : (r >= c1 ? 64u : (r >= c0 ? 32u : 0u));
+    const uint32_t rr = r - (r >= c2 ? c2 : (r >= c1 ? c1 : (r >= c0 ? c0 : 0u)));
+    p1 = base + select32(x, rr) + 1;
+  }
+  const uint64_t e0 = (uint64_t)d1 << 32 | d0, e1 = (uint64_t)d3 << 32 | d2;
+  const uint64_t y = p1 >= 128 ? 0ull : (p1 >= 64 ? e1 >> (p1 - 64) : (e0 >> p1) | (p1 ? e1 << (64 - p1) : 0ull));
+  if (y == 0) return false;
+  const uint32_t c = (uint32_t)__builtin_ctzll(y);  // entries of bucket j
+  found = 0;
+  if (c == 0) return true;
+  const uint32_t b = (p1 - j) * rvs, nb = c * rvs, wi = b >> 5, off = b & 31;
+  if (off + nb > 96 || b + nb > 384 || nb > 64) return false;
+  const uint32_t w0 = Lw[4 + wi], w1 = Lw[5 + wi], w2 = Lw[6 + wi];
+  // the c fields as one 64-bit word (funnel shifts), compared at once (SWAR, as line_decode_w)
+  const uint64_t W = (uint64_t)__builtin_amdgcn_alignbit(w2, w1, off) << 32 | __builtin_amdgcn_alignbit(w1, w0, off);
+  const uint64_t M = (L << rvs) - (L << vs);  // remainder part of every field (uniform)
+  const uint64_t H = L << (rvs - 1);          // top bit of every remainder part (uniform)
+  const uint64_t MH = M & ~H;
+  const uint64_t Y = W ^ ((uint64_t)(remainder << vs) * L);
+  const uint64_t valid = nb == 64 ? ~0ull : (1ull << nb) - 1;
+  uint64_t Z = H & valid & ~(((Y & MH) + MH) | Y);  // top bits of the matching fields
+  if (vs == 0) {
+    found = Z ? 1ull : 0ull;
+  } else {
+    const uint32_t vmask = (1u << vs) - 1;
+    while (Z) {  // one pass per match (usually 0 or 1)
+      const uint32_t p = (uint32_t)__builtin_ctzll(Z) + 1 - rvs;  // the field's first bit
+      const uint32_t val = (uint32_t)(W >> p) & vmask;
+      if (val < 64) found |= 1ull << val;
+      Z &= Z - 1;
+    }
+  }
+  return true;
+}
+
+// The fast path's LDS buffer per wave: instruction k of the quad gather lands its 1 KiB (16
+// lines) at byte k * FAST_KSTRIDE, so the line of probe p = 4g + k sits at k * 1040 + 64 g: the
+// 16-byte skew per k puts the 16 lanes of each ds_read_b128 lane group on 16 distinct bank
+// quads (without it the four probes of a quad hit the same banks: 4-way conflicts). One extra
+// 16-byte slot: a remainder window read at the last line's end (masked bits) stays inside.
+#ifndef RF_FAST_KSTRIDE
+#define RF_FAST_KSTRIDE 1040
+#endif
+constexpr uint32_t FAST_KSTRIDE = RF_FAST_KSTRIDE;
+constexpr int FAST_WBUF = (3 * FAST_KSTRIDE + 1024) / 16 + 1;
+
+// Sweep 0.. of a full wave of one filter: hash (24-byte keys staged through LDS by LDS-DMA, or
+// hashes), gather each probe's 64-B line (quad-cooperative LDS-DMA), decode, one coalesced
+// store. False when the wave is not fast-path material (the caller takes the general path).
+template <int KIND>
+__device__ __forceinline__ bool probe_fast(const uint4* __restrict__ pplans, const FilterPlan* __restrict__ plans,
+                                           const uint8_t* __restrict__ pages, const uint64_t* __restrict__ slots,
+                                           const uint4* __restrict__ lines, const void* __restrict__ in0,
+                                           const uint32_t* __restrict__ wave_tab, uint64_t n,
+                                           uint64_t* __restrict__ found, uint32_t fp_size, uint32_t seed, uint32_t lis,
+                                           uint32_t page_size, uint32_t nf, uint64_t wf, v4u* sw) {
+  if (wf + WAVE > n) return false;
+  if (KIND == IN_KEYS24 && ((uintptr_t)in0 & 15)) return false;
+  const uint32_t t = sload32(wave_tab + wf / WAVE);
+  if ((t & 127u) != WAVE) return false;  // the wave spans a run boundary
+  const uint32_t fs = t >> 7;
+  if (fs >= nf) return false;
+  const uint4 U = make_uint4(sload32(&pplans[fs].x), sload32(&pplans[fs].y), sload32(&pplans[fs].z),
+                             sload32(&pplans[fs].w));
+  const uint32_t vs = U.x & 0xff, rem = (U.x >> 8) & 0xff, rvs = (U.x >> 16) & 0xff, lgl = U.x >> 24;
+  if (U.w || !lgl || rem == 0 || rem >= 32 || rvs > 32) return false;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  uint32_t h;
+  if constexpr (KIND == IN_KEYS24) {
+    // the wave's 64 keys (1,536 contiguous bytes): 16-byte LDS-DMA loads, 12 cache lines
+    const uint8_t* kb = static_cast<const uint8_t*>(in0) + wf * 24;
+    const uint8_t* kb2 = kb + 1024;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + lane * 16),
+                                     (__attribute__((address_space(3))) void*)sw, 16, 0, 2);
+    if (lane < 32)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb2 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(sw + WAVE), 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync_lds();
+    const uint2* k2 = reinterpret_cast<const uint2*>(sw) + 3 * lane;
+    const uint2 a = k2[0], b = k2[1], c = k2[2];
+    const uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    h = xxh32_24(w, seed);
+  } else {
+    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + wf + lane);
+  }
+  const uint32_t lgG = lgl - 1;
+  const uint32_t fp = h >> (32 - fp_size);
+  const uint32_t bucket = fp >> rem;
+  const uint32_t remainder = fp & ((1u << rem) - 1);
+  const uint8_t* fb = reinterpret_cast<const uint8_t*>(lines) + ((uint64_t)U.y << 6);  // the filter's lines
+  const uint32_t lo = (bucket >> lgG) << 6, q16 = (lane & 3) << 4;
+  uint8_t* sb = reinterpret_cast<uint8_t*>(sw);
+#define RF_FAST_LOAD(k)                                                                                       \
+  {                                                                                                           \
+    const uint32_t lk = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, (k) * 0x55, 0xf, 0xf, false);             \
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(fb + (lk + q16)),        \
+                                     (__attribute__((address_space(3))) void*)(sb + (k) * FAST_KSTRIDE), 16, 0, 0); \
+  }
+  RF_FAST_LOAD(0) RF_FAST_LOAD(1) RF_FAST_LOAD(2) RF_FAST_LOAD(3)
+#undef RF_FAST_LOAD
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wave_sync_lds();
+  const uint32_t* Lw = reinterpret_cast<const uint32_t*>(sb + (lane & 3) * FAST_KSTRIDE + (lane >> 2) * 64);
+  const uint64_t L = sload64(&c_field_ones.v[rvs]);
+  uint64_t r;
+  if (!line_decode_u(Lw, bucket & ((1u << lgG) - 1), remainder, vs, rvs, L, r))
+    r = probe_walk(U, h, fs, plans, pages, slots, fp_size, lis, page_size);
+#ifdef RF_PROBE_PAD
+  {  // diagnostics builds only (tools/ab_build.sh): RF_PROBE_PAD extra VALU per lane
+    uint32_t x = h;
+#pragma unroll
+    for (int k = 0; k < RF_PROBE_PAD; k++) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x) : "v"(remainder));
+    asm volatile("" ::"v"(x));
+  }
+#endif
+  __builtin_nontemporal_store(r, found + wf + lane);
+  return true;
+}
+
 template <int KIND>
 __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restrict__ pplans,
                                                     const FilterPlan* __restrict__ plans,
@@ -2802,12 +2967,21 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
   // per wave: the 24-byte keys' staging (96 x 16 B), then the quad-gathered probe lines
   // (64 x 64 B); variable-length keys stage their window in s_vk and reuse it for the lines
   constexpr bool QUAD = RF_PROBE_QUAD;
-  constexpr int WBUF = (QUAD && !WAVE_VAR) ? 256 : (WAVE_KEYS ? 96 : 1);
+  constexpr int WBUF = (QUAD && !WAVE_VAR) ? FAST_WBUF : (WAVE_KEYS ? 96 : 1);
   __shared__ v4u s_wbuf[NT / WAVE][WBUF];
   constexpr uint32_t VCAP = 4096;
   __shared__ __attribute__((aligned(16))) uint32_t s_vk[WAVE_VAR ? NT / WAVE : 1][WAVE_VAR ? VCAP / 4 + 4 : 1];
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint64_t wf = i0 - lane;  // the wave's first probe
+  if constexpr ((KIND == IN_KEYS24 || KIND == IN_HASH) && QUAD) {
+    if (runs) {
+      const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x) / WAVE;
+      const uint64_t wfs = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * NT + wv * WAVE;  // = wf, in SGPRs
+      if (wfs < n && probe_fast<KIND>(pplans, plans, pages, slots, lines, in0, wave_tab, n, found, fp_size, seed,
+                                      lis, page_size, num_filters, wfs, s_wbuf[wv]))
+        return;
+    }
+  }
   if constexpr (WAVE_KEYS) {
     // 24-byte keys: the wave's 64 keys (1,536 contiguous bytes) are read with 16-byte
     // coalesced loads -- 12 cache lines per wave, where three strided 8-byte loads per lane

@@ -3,7 +3,10 @@ lookups answered by a persistent wave that polls a ring in pinned host memory. E
 must equal the batch probe's (k_probe) for the same filter and hash, through the waiting and
 the reaping forms, from several threads at once, across the wave's idle exit and relaunch,
 and after the batch's device memory was reused by another build while the wave kept running
-(the wave must not answer from stale cached lines)."""
+(the wave must not answer from stale cached lines). The server runs with its default idle exit
+(400 us) and lifetime (800 us) except where a test raises them through the host-controlled
+keep-alive (rf_amd_lookup_server_set_times); a device-wide synchronisation taken while lookups
+keep the server busy returns within about one lifetime."""
 import ctypes
 import os
 import threading
@@ -17,12 +20,6 @@ from splinterdb_amd import engine as E
 from splinterdb_amd import keys as K
 
 pytestmark = pytest.mark.gpu
-
-# the wave's idle exit (default 1 ms) would otherwise end it whenever this module's Python
-# threads wait on the GIL, and its lifetime bound (default 20 ms) before a rebuild is done;
-# set before the engine's server starts (the first submit)
-os.environ.setdefault("RF_AMD_SERVER_IDLE_US", "300000")
-os.environ.setdefault("RF_AMD_SERVER_LIFE_US", "5000000")
 
 # The server's CU-masked stream synchronises with the legacy null stream, so this module
 # works on a non-blocking torch stream and synchronises that stream, never the device: a
@@ -158,18 +155,22 @@ def test_threads_idle_relaunch_and_reused_memory():
     for t in ths:
         t.join(60)
     assert (out == want).all()
-    # the wave exits after RF_AMD_SERVER_IDLE_US without requests (300 ms here); the next
-    # lookup relaunches it and is answered
+    # the wave exits after its idle time without requests (default 400 us); the next lookup
+    # relaunches it and is answered
     st = (ctypes.c_uint64 * 3)()
     E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
     launches0 = st[1]
-    time.sleep(0.5)
+    time.sleep(0.05)
     assert wait(b, submit(b, fid[0], ph[0], None)) == want[0]
     E._check(lib().rf_amd_lookup_server_stats(b.engine.h, st))
     assert st[1] > launches0
     # a keeper thread's lookups keep the wave busy (no idle exit) while the batch is replaced
     # by other builds in the same (pooled) device memory: the new batches' answers must not
-    # come from lines the running wave cached before
+    # come from lines the running wave cached before. The host-controlled keep-alive makes the
+    # waves launched from here live long enough (5 s, 300 ms idle) to span a rebuild; the
+    # next relaunch takes it (the current wave lives at most its default 800 us more).
+    E._check(lib().rf_amd_lookup_server_set_times(b.engine.h, 300_000, 5_000_000))
+    time.sleep(0.01)
     bk, hk = build(cfg, [5000], [0], seed=99)
     stop = threading.Event()
     kept = []
@@ -201,4 +202,48 @@ def test_threads_idle_relaunch_and_reused_memory():
         kt.join(30)
     assert spanned >= 1
     assert len(kept) > 100 and all(v & 1 for v in kept)  # every kept hash was inserted, value 0
+    E._check(lib().rf_amd_lookup_server_set_times(b.engine.h, 400, 800))  # the defaults again
+    stop_wave(b)
     bk.close(stream().cuda_stream)
+
+
+def stop_wave(b):
+    """lets a long-lived wave run out: one lookup after its idle time has passed relaunches a
+    wave with the current (default) times"""
+    time.sleep(0.35)
+    bk, hk = build(E.routing_config_init(log_index_size=8), [100], [0], seed=5)
+    wait(bk, submit(bk, 0, hk[0], None))
+    bk.close(stream().cuda_stream)
+
+
+def test_device_sync_while_server_busy_is_short():
+    """hipDeviceSynchronize waits for every stream, the server's too: with the default 800-us
+    lifetime it returns within about that long even while a thread keeps the server busy
+    (up to 20 ms before)"""
+    cfg = E.routing_config_init(log_index_size=8)
+    b, h = build(cfg, [50_000], [0], seed=7)
+    stop = threading.Event()
+    n = [0]
+
+    def keeper():
+        while not stop.is_set():
+            wait(b, submit(b, 0, h[n[0] % 50_000], None))
+            n[0] += 1
+
+    kt = threading.Thread(target=keeper)
+    kt.start()
+    try:
+        time.sleep(0.05)
+        ts = []
+        for _ in range(30):
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()  # device-wide
+            ts.append(time.perf_counter() - t0)
+            time.sleep(0.003)
+    finally:
+        stop.set()
+        kt.join(30)
+    ts.sort()
+    assert n[0] > 100, n[0]
+    assert ts[len(ts) // 2] < 1.0e-3 and ts[-1] < 3.0e-3, ts
+    b.close(stream().cuda_stream)

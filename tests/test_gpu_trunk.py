@@ -21,13 +21,15 @@ pytestmark = [pytest.mark.gpu,
                                  reason="oracle/_ref/libkvs_{ref,shim}.so not built")]
 
 
-def run(path, keys, vals, probe, memtable_mib):
-    with RK.Kvs(path, memtable_mib=memtable_mib) as db:
+def run(path, keys, vals, probe, memtable_mib, release=True, stats=None):
+    with RK.Kvs(path, memtable_mib=memtable_mib, release=release) as db:
         db.insert(keys, vals)
         recs, nl0, na0 = db.adds()
         f, v, _ = db.lookup(probe)
         fa, va, _ = db.lookup_async(probe, 64)
         _, nl, na = db.adds()
+        if stats is not None:
+            stats.append(db.direct_stats())
     return recs, (f, v), (fa, va), nl - nl0, na - na0
 
 
@@ -49,3 +51,25 @@ def test_trunk_filters_and_lookups_identical_to_reference(n, memtable_mib):
         assert (v[:40_000] == want_v).all()
     # the same filter calls reached the filter (the trunk prunes by the filter's answers)
     assert ref[3] == shim[3] and ref[4] == shim[4]
+
+
+def test_reopen_without_release_filters_identical():
+    """The unmodified reference closes a store without routing_filter_amd_cache_release (the
+    shim's extension). Three stores opened one after another in one process, each
+    closed without it -- their cache buffers may be mapped again at the same address with the
+    same size -- must each get the reference's filters byte for byte and its lookups; a
+    registration that no longer maps its buffer is detected by the placement canary and
+    replaced."""
+    stats = []
+    for i, seed in enumerate((21, 22, 23)):
+        keys, vals, absent = workload(300_000, seed=seed)
+        probe = np.concatenate([keys[:20_000], absent[:20_000]])
+        ref = run(RK.KVS_REF, keys, vals, probe, 2)
+        shim = run(RK.KVS_SHIM, keys, vals, probe, 2, release=False, stats=stats)
+        assert len(ref[0]) == len(shim[0]) and len(ref[0]) > 3
+        for j, (a, b) in enumerate(zip(ref[0], shim[0])):
+            assert a.tolist() == b.tolist(), (i, j)
+        for (f, v), (g, w) in ((ref[1], shim[1]), (ref[2], shim[2])):
+            assert (f == g).all() and (v == w).all(), i
+    # what happened to the registrations (printed for the record; correctness is asserted above)
+    print("direct stats per store (registered, stale seen, buffer address):", stats)

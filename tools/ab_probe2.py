@@ -17,13 +17,17 @@ vp = ctypes.c_void_p
 dev = torch.device("cuda", 0)
 cfg = E.RfConfig(26, 8, 42, 4096, 32)
 shapes = {"c2": (8, 8_000_000), "c3": (256, 1 << 20)}
+if os.environ.get("AB_SHAPES"):  # e.g. AB_SHAPES=c3: one shape per process (PMC passes)
+    shapes = {k: shapes[k] for k in os.environ["AB_SHAPES"].split(",")}
 out = {}
 for shape, (F, n) in shapes.items():
     N = F * n
     keys = K.seq_keys_torch(0, N, 24, dev)
     counts = (ctypes.c_uint64 * F)(*([n] * F))
     libs = []
-    for path in sys.argv[1:]:
+    for arg in sys.argv[1:]:
+        # path[:VAR=V,VAR2=V2] -- environment set around this entry's calls
+        path, _, sw = arg.partition(":")
         L = ctypes.CDLL(os.path.abspath(path))
         L.rf_amd_engine_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
         L.rf_amd_batch_create.argtypes = [vp, ctypes.POINTER(E.RfConfig), ctypes.c_uint32, vp, vp, vp, vp,
@@ -42,12 +46,16 @@ for shape, (F, n) in shapes.items():
                                      ctypes.byref(b)) == 0
         assert L.rf_amd_batch_set_timing(b, 1) == 0
         found = torch.empty(N, dtype=torch.int64, device=dev)
-        libs.append((os.path.basename(os.path.dirname(path)) + "/" + os.path.basename(path), L, b, found, nn, vals))
+        libs.append((os.path.basename(os.path.dirname(path)) + "/" + os.path.basename(path) + (":" + sw if sw else ""),
+                     L, b, found, nn, vals, sw))
     torch.cuda.synchronize()
     res = {name: {"probe": [], "build": [], "assemble": [], "sort": [], "partition": [], "layout": []} for name, *_ in libs}
     arr = (ctypes.c_float * 9)()
     for rnd in range(7):
-        for name, L, b, found, *_ in libs:
+        for name, L, b, found, nn_, vals_, sw in libs:
+            for kv in (sw.split(",") if sw else []):
+                k_, _, v_ = kv.partition("=")
+                os.environ[k_] = v_
             assert L.rf_amd_batch_build_keys(b, keys.data_ptr(), 24, None) == 0
             assert L.rf_amd_batch_probe_keys_runs(b, keys.data_ptr(), 24, counts, found.data_ptr(), None) == 0
             torch.cuda.synchronize()

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
+#include <algorithm>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
@@ -82,17 +83,30 @@ int main() {
     while (__atomic_load_n(res, __ATOMIC_ACQUIRE) != (uint64_t)i) __builtin_ia32_pause();
   }
   const double persist_us = (now_us() - t) / N;
-  // meanwhile other work on another stream must not be blocked by the server
-  double other_us = -1;
-  {
-    const double t1 = now_us();
-    hipLaunchKernelGGL(k_once, dim3(1), dim3(64), 0, st, res + 1, 7);
-    CK(hipStreamSynchronize(st));
-    other_us = now_us() - t1;
-  }
+  // meanwhile other work on another stream must not be blocked by the server: 200 launch +
+  // stream-sync round trips on a plain stream while the server runs, then the same after it
+  // stopped (first sample and median of each: a cold first launch vs a steady cost)
+  auto other = [&](double* first, double* med) {
+    double v[200];
+    for (int i = 0; i < 200; i++) {
+      const double t1 = now_us();
+      hipLaunchKernelGGL(k_once, dim3(1), dim3(64), 0, st, res + 1, (uint64_t)i);
+      CK(hipStreamSynchronize(st));
+      v[i] = now_us() - t1;
+    }
+    *first = v[0];
+    std::sort(v, v + 200);
+    *med = v[100];
+  };
+  double run_first, run_med, idle_first, idle_med;
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));  // st idle for a while, as in round 4
+  other(&run_first, &run_med);
   __atomic_store_n(ctl, (uint64_t)1, __ATOMIC_RELEASE);
   CK(hipStreamSynchronize(sm));
-  printf("{\"launch_roundtrip_us\": %.2f, \"persistent_roundtrip_us\": %.2f, \"other_stream_kernel_us_while_server_runs\": %.1f, \"served\": %llu}\n",
-         launch_us, persist_us, other_us, (unsigned long long)ctl[1]);
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  other(&idle_first, &idle_med);
+  const double other_us = run_first;
+  printf("{\"launch_roundtrip_us\": %.2f, \"persistent_roundtrip_us\": %.2f, \"other_stream_kernel_us_while_server_runs\": {\"first\": %.1f, \"median\": %.1f}, \"other_stream_kernel_us_server_stopped\": {\"first\": %.1f, \"median\": %.1f}, \"served\": %llu}\n",
+         launch_us, persist_us, other_us, run_med, idle_first, idle_med, (unsigned long long)ctl[1]);
   return 0;
 }
