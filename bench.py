@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="CPU baseline threads (0 = every usable core: the affinity set capped by the cgroup quota)")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--dist-always", action="store_true",
+                   help="initialise torch.distributed (RCCL) and run every collective even with one rank: "
+                        "exercises the multi-rank code path on a one-GPU box")
     p.add_argument("--routed-probe", action="store_true",
                    help="also time routed probes: each rank probes keys of every rank's filters, "
                         "moved to the owner by all-to-all (route.py); reported beside value")
@@ -206,8 +209,16 @@ def main():
     backend = os.environ.get("RF_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     local = local % max(1, ndev)
-    if world > 1:
+    if world > 1 or args.dist_always:
         import torch.distributed as dist
+        if world == 1 and "MASTER_PORT" not in os.environ:  # one rank without torchrun
+            import socket
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -305,6 +316,20 @@ def main():
         ok = bool(((found[positive] & 1) == 1).all().item())
     else:
         ok = bool(((found & 1) == 1).all().item())
+    # ---- the probe's measured memory floor (after the results were checked: it overwrites
+    # `found`): the fast path's key staging, line gather and store over the same runs with the
+    # hash and decode removed (rf_amd_debug_probe_floor), HIP events on the probe's stream
+    floor_ms = None
+    if not var:
+        batch.probe_floor(keys, 24, counts, found, stream=stream.cuda_stream)
+        fe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        freps = 5
+        fe[0].record(stream)
+        for _ in range(freps):
+            batch.probe_floor(keys, 24, counts, found, stream=stream.cuda_stream)
+        fe[1].record(stream)
+        stream.synchronize()
+        floor_ms = S.max_over_ranks(fe[0].elapsed_time(fe[1]) / freps, dist, coll_dev)
     infos = [batch.info(f) for f in range(F)]
     image_bytes = sum(i.num_pages for i in infos) * cfg.page_size
     slot_bytes = sum(i.num_indices for i in infos) * 8
@@ -418,7 +443,7 @@ def main():
         rfound = torch.zeros(N, dtype=torch.int64, device=dev)
         router = R.ProbeRouter(S.plan_shards(F_total, n, world), rank, batch, dev, dist=dist,
                                coll_device=coll_dev if coll_dev is not None else "cpu",
-                               ops=R.GpuRouteOps(eng))
+                               ops=R.GpuRouteOps(eng), collective_at_one=args.dist_always)
         reps = max(1, min(args.steps, 5))
 
         def rstep():
@@ -439,8 +464,9 @@ def main():
         r_ok = S.max_over_ranks(0.0 if r_ok else 1.0, dist, coll_dev) == 0.0  # every rank's probes
         routed = {"mkeys_s": round(keys_all * reps / tr / 1e6, 1), "ms": round(tr / reps * 1e3, 3),
                   "reps": reps, "verified": r_ok,
-                  "exchange": "none (1 rank)" if world == 1 else
-                  ("all-to-all over RCCL" if coll_dev is not None else "all-to-all over gloo (rehearsal)")}
+                  "exchange": "none (1 rank)" if (world == 1 and not args.dist_always) else
+                  ("all-to-all over RCCL" if coll_dev is not None else "all-to-all over gloo (rehearsal)")
+                  + (" (1 rank)" if world == 1 else "")}
         del rkeys, rfid, d_rh, rfound, router
 
     # every rank's checks, not only rank 0's: the line says verified only if all ranks agree
@@ -503,7 +529,14 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": peak,
                      "unit": "GB/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": traffic, "gpus": world,
-                     "per_gpu_achieved": kern[dom].get("gbs"), "per_gpu_peak": HBM_PEAK_GBS},
+                     "per_gpu_achieved": kern[dom].get("gbs"), "per_gpu_peak": HBM_PEAK_GBS,
+                     "floor_ms": round(floor_ms, 4) if (floor_ms and dom == "probe") else None},
+        # the probe's measured floor (ms per launch, slowest rank) and the probe's time over it
+        "probe_floor": ({"floor_ms": round(floor_ms, 4), "probe_ms": round(probe_ms, 4),
+                         "probe_over_floor": round(probe_ms / floor_ms, 3),
+                         "what": "k_probe_floor: the probe's fast-path memory traffic (key staging, "
+                                 "one 64-B line gather per probe, 8-B store) over the same runs, "
+                                 "hash and decode removed"} if floor_ms else None),
         "kernels": kern,
         "build_total_stage_pass_ms": round(ms["build_total"], 4),
         "verified": verified,

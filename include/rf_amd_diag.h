@@ -21,6 +21,14 @@ extern "C" {
 int rf_amd_debug_read_lines(rf_amd_batch *b, uint8_t *h_lines, uint64_t bytes, uint64_t *num_lines);
 int rf_amd_debug_rebuild_lines(rf_amd_batch *b);
 
+/* the probe's memory floor, measured (bench.py `roofline.floor_ms`): one launch of a kernel
+ * with k_probe's fast-path memory traffic and wave order over the same runs as
+ * rf_amd_batch_probe_{keys,hashes}_runs (key_len 24: 16-byte-aligned keys; 4: hashes) --
+ * key staging, one 64-B line gather per probe from its filter, one 8-byte store -- with the
+ * hash and the decode replaced by a few integer operations. d_out receives no lookup results. */
+int rf_amd_debug_probe_floor(rf_amd_batch *b, const void *d_in, uint32_t key_len, const uint64_t *h_counts,
+                             uint64_t *d_out, void *stream);
+
 /* diagnostics library only (librf_amd_stamps.so): a device buffer of 16 u64 per workgroup
  * (NULL = off); the instrumented kernel chosen by `kernel` (1 = bucket sort, 2 = fused
  * partition, 3 = page assembly, 4 = layout) stamps the shader clock at each of its phases

@@ -658,7 +658,22 @@ static struct {
    uint64 cap;
 } g_pin_pool[PIN_POOL];
 static uint32          g_pin_n;
+static uint64          g_pin_bytes; /* bytes held by the pool */
 static pthread_mutex_t g_pin_mu = PTHREAD_MUTEX_INITIALIZER;
+
+/* RF_SHIM_PIN_POOL_MIB (default 256): the pinned bytes the pool may keep between adds; a
+ * buffer that would take it over the cap is freed instead of pooled */
+static uint64
+pin_pool_cap(void)
+{
+   static uint64 v = 0;
+   if (!v) {
+      const char *s = getenv("RF_SHIM_PIN_POOL_MIB");
+      uint64      m = s ? strtoull(s, NULL, 10) : 256;
+      v             = (m << 20) + 1;
+   }
+   return v - 1;
+}
 
 /* RF_SHIM_PINNED=0: read-backs into malloc'd memory after one engine-wide sync (A/B) */
 static int
@@ -690,6 +705,7 @@ pin_take_any(rf_amd_engine *e, uint64 bytes, uint64 *cap, int force)
          }
          void *p = g_pin_pool[best].p;
          *cap    = g_pin_pool[best].cap;
+         g_pin_bytes -= *cap;
          g_pin_pool[best] = g_pin_pool[--g_pin_n];
          pthread_mutex_unlock(&g_pin_mu);
          return p;
@@ -716,10 +732,11 @@ pin_give_any(rf_amd_engine *e, void *p, uint64 cap, int force)
       return;
    }
    pthread_mutex_lock(&g_pin_mu);
-   if (g_pin_n < PIN_POOL) {
+   if (g_pin_n < PIN_POOL && g_pin_bytes + cap <= pin_pool_cap()) {
       g_pin_pool[g_pin_n].p   = p;
       g_pin_pool[g_pin_n].cap = cap;
       g_pin_n++;
+      g_pin_bytes += cap;
       p = NULL;
    }
    pthread_mutex_unlock(&g_pin_mu);
@@ -1703,7 +1720,13 @@ async_reap_complete(void)
    }
    const uint64 t1 = now_ns();
    shim_batch  *pins[REAP];
+   for (uint64 i = 0; i < n && i < 4; i++) {
+      __builtin_prefetch(tags[i], 1, 3);
+   }
    for (uint64 i = 0; i < n; i++) {
+      if (i + 4 < n) {
+         __builtin_prefetch(tags[i + 4], 1, 3); /* the owners' states: misses overlapped */
+      }
       rf_state         *st  = tags[i];
       async_callback_fn cb  = st->callback;
       void             *arg = st->callback_arg;

@@ -1439,8 +1439,19 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
   if (!lk.owns_lock()) return 0;  // another thread is reaping
   uint64_t n = 0, t = v.reap_next;
   const uint64_t tail = v.tail.load(std::memory_order_acquire);
+  // the result lines (written by the GPU over PCIe: a miss each) and the request metadata
+  // (written by the submitting threads) of the next tickets are fetched ahead, so the misses
+  // of consecutive tickets overlap instead of costing one round trip per state
+  for (uint64_t q = t; q < tail && q < t + 16; q += 4) {
+    __builtin_prefetch(&v.res[q & (SRV_RING - 1)], 0, 0);
+    __builtin_prefetch(&v.meta[q & (SRV_RING - 1)], 0, 0);
+  }
   while (n < max && t < tail) {
     const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
+    if ((t & 3) == 0 && t + 16 < tail) {
+      __builtin_prefetch(&v.res[(t + 16) & (SRV_RING - 1)], 0, 0);
+      __builtin_prefetch(&v.meta[(t + 16) & (SRV_RING - 1)], 0, 0);
+    }
     const uint64_t tk = v.meta[slot].ticket.load(std::memory_order_acquire);
     if (tk == SRV_UNPUBLISHED || tk == SRV_BUSY || tk < t) break;  // not yet published
     if (tk > t) {  // a waiter already took ticket t and its slot was reused
@@ -1709,13 +1720,13 @@ extern "C" int rf_amd_batch_probe_hashes(rf_amd_batch* b, const uint32_t* d_hash
 // Probes grouped by filter (filter f's h_counts[f] probes follow filter f-1's): the filter of
 // a probe comes from its position, so no per-probe filter id is read. The run bounds are
 // uploaded when they change.
-static int probe_runs(rf_amd_batch* b, int kind, const void* in0, uint32_t key_len, const uint64_t* h_counts,
-                      uint64_t* d_found, void* stream) {
+static int upload_runs(rf_amd_batch* b, const uint64_t* h_counts, void* stream, uint64_t* n_out) {
   if (!b || !b->built) return fail(RF_AMD_EINVAL, "probe on an unbuilt batch");
   if (!h_counts) return fail(RF_AMD_EINVAL, "null counts");
   std::vector<uint64_t> runs(b->F + 1, 0);
   for (uint32_t f = 0; f < b->F; f++) runs[f + 1] = runs[f] + h_counts[f];
   const uint64_t n = runs[b->F];
+  *n_out = n;
   if (n == 0) return 0;
   HIPCHK(hipSetDevice(b->eng->device));
   if (runs != b->runs_host) {
@@ -1730,7 +1741,35 @@ static int probe_runs(rf_amd_batch* b, int kind, const void* in0, uint32_t key_l
       return fail(RF_AMD_EINVAL, "wave table launch failed");
     b->runs_host = runs;
   }
+  return 0;
+}
+
+static int probe_runs(rf_amd_batch* b, int kind, const void* in0, uint32_t key_len, const uint64_t* h_counts,
+                      uint64_t* d_found, void* stream) {
+  uint64_t n = 0;
+  if (int rc = upload_runs(b, h_counts, stream, &n)) return rc;
+  if (n == 0) return 0;
   return do_probe(b, kind, in0, nullptr, key_len, nullptr, n, d_found, stream, b->d_runs.as<uint64_t>());
+}
+
+// bench.py's measured probe floor: k_probe_floor over the same runs (rf_amd_diag.h)
+extern "C" int rf_launch_probe_floor(const LaunchArgs* pa, int kind, const void* in0, uint64_t n, uint64_t* found);
+extern "C" int rf_amd_debug_probe_floor(rf_amd_batch* b, const void* d_in, uint32_t key_len, const uint64_t* h_counts,
+                                        uint64_t* d_out, void* stream) {
+  if (key_len != 24 && key_len != 4) return fail(RF_AMD_EINVAL, "probe floor: 24-byte keys or 4-byte hashes");
+  if (!d_in || !d_out) return fail(RF_AMD_EINVAL, "null probe buffer");
+  if (key_len == 24 && ((uintptr_t)d_in & 15)) return fail(RF_AMD_EINVAL, "probe floor: keys 16-byte aligned");
+  uint64_t n = 0;
+  if (int rc = upload_runs(b, h_counts, stream, &n)) return rc;
+  if (n == 0) return 0;
+  hipStream_t st = stream ? (hipStream_t)stream : b->eng->stream;
+  (void)hipGetLastError();
+  LaunchArgs a = make_args(b, st);
+  a.probe_runs = b->d_runs.as<uint64_t>();
+  a.wave_tab = b->d_wave_tab.as<uint32_t>();
+  int rc = rf_launch_probe_floor(&a, key_len == 24 ? IN_KEYS24 : IN_HASH, d_in, n, d_out);
+  if (rc) return fail(RF_AMD_EINVAL, std::string("probe floor launch: ") + hipGetErrorString((hipError_t)rc));
+  return 0;
 }
 
 extern "C" int rf_amd_batch_probe_keys_runs(rf_amd_batch* b, const void* d_keys, uint32_t key_len,
@@ -1742,10 +1781,6 @@ extern "C" int rf_amd_batch_probe_hashes_runs(rf_amd_batch* b, const uint32_t* d
                                               uint64_t* d_found, void* stream) {
   return probe_runs(b, IN_HASH, d_hashes, 4, h_counts, d_found, stream);
 }
-
-// Diagnostic (diagnostics library only; EINVAL in the product): low byte 1 = hash only,
-// 2 = + probe line load; 0 = normal probe. Bits 8-15: cap the probe kernel at that many
-// waves per SIMD via LDS padding; bits 16-23: probes per lane.
 
 extern "C" int rf_debug_set_phase_buffer(uint64_t* d_buf, uint32_t kid);
 extern "C" int rf_amd_debug_phase_buffer(void* d_buf, uint32_t kernel) {

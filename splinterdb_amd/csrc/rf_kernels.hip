@@ -676,7 +676,8 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
                                                      uint32_t lis, uint32_t* __restrict__ first_old,
                                                      uint32_t* __restrict__ has_old,
                                                      const uint32_t* __restrict__ spill,
-                                                     const uint32_t* __restrict__ cb_outs) {
+                                                     const uint32_t* __restrict__ cb_outs,
+                                                     const uint32_t* __restrict__ cb_list) {
   constexpr int PER = SORT_CAP / SORT_NT;
   DBG_PHASE(15);
   __shared__ EntT s_b[SORT_CAP];
@@ -692,7 +693,18 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   uint32_t* s_first = s_bin;  // compacted start of each index: reuses s_bin once bins are sorted
   uint32_t* s_fo = s_bin + 2048;
   uint32_t* s_ho = s_bin + 2048 + MAX_IPC;
-  const uint32_t cb = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's buckets share an XCD (its partition's L2)
+  // cb_list (K4m's fallback, 32-bit incremental builds): the coarse buckets K4m listed with
+  // bit 31 set (more new entries than it takes, or a bin of duplicates), one after another
+  const uint32_t nit = cb_list ? cb_list[0] : 1u;
+  for (uint32_t it = cb_list ? blockIdx.x : 0u; it < nit; it += cb_list ? gridDim.x : 1u) {
+  uint32_t cb;
+  if (cb_list) {
+    cb = cb_list[1 + it];
+    if (!(cb >> 31)) continue;  // K4b's (over SORT_CAP)
+    cb &= 0x7fffffffu;
+  } else {
+    cb = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's buckets share an XCD (its partition's L2)
+  }
   const uint32_t f = cb_filter[cb];
   const FilterPlan& P = plans[f];
   const uint32_t n = cb_count[cb];
@@ -704,8 +716,8 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   const uint32_t cb_out = (DUAL && spill) ? cb_outs[cb] : cb_rel;
   CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_out, P.e_first};
   if (n > SORT_CAP) {  // handled by k_cb_sort_big
-    if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
-    return;
+    if (threadIdx.x == 0 && !cb_list) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
+    continue;
   }
   const uint32_t nbins = 1u << (P.bbits - P.binsh);  // a bin = 2^binsh filter buckets
   const uint32_t bmask = nbins - 1, bsh = P.rvs + P.binsh;
@@ -1006,6 +1018,299 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
   if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
   DBG_PHASE(8);
+  __syncthreads();  // list mode: the next bucket reuses the LDS
+  }
+}
+
+// K4m: the bucket sort of 32-bit incremental builds (routing_filter_add with an old filter,
+// src/routing_filter.c:496-597). A coarse bucket's entries are its old run -- the old filter's
+// entries, already in order -- and a small share of new ones (an eighth in round 8 of a
+// compaction chain). Only the new entries are sorted (bins over their top bits sized to their
+// count, then sorting networks); each new entry is dropped if it equals the previous new one
+// or an old one (old first on equal entries, src/routing_filter.c:559-597) -- found by a
+// binary search of the old run, which also gives the kept entry's final position (its rank
+// among the kept new + the old entries not above it). The output is then written 64 slots
+// per wave step: the step's new slots form a bit mask, each lane takes its entry from the new
+// list (mbcnt of the mask) or the old run (slot - new entries before it); num_unique compares
+// each entry with its predecessor (a lane shift). The old run reaches LDS by LDS-DMA and is
+// never sorted, scattered or compacted (the K4 DUAL path did all three). Buckets with more new
+// entries than MRG_NEW_CAP, or a bin of more than 64 equal-bin new entries, go to k_cb_sort in
+// list mode (bit 31 on their overflow-list entry); buckets over SORT_CAP to K4b as before.
+constexpr uint32_t MRG_NEW_CAP = 2048;
+constexpr uint32_t MRG_LNB_MAX = 9;  // at most 512 bins
+__global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __restrict__ plans,
+                                                      const uint32_t* __restrict__ cb_filter,
+                                                      const uint32_t* __restrict__ cb_count,
+                                                      const uint32_t* __restrict__ cb_start,
+                                                      const uint32_t* __restrict__ part,
+                                                      const uint32_t* __restrict__ old32,
+                                                      const uint32_t* __restrict__ ob_lo,
+                                                      const uint32_t* __restrict__ ob_n,
+                                                      uint32_t* __restrict__ sorted32,
+                                                      uint32_t* __restrict__ idx_cnt,
+                                                      uint32_t* __restrict__ idx_start,
+                                                      FilterOut* __restrict__ outs,
+                                                      uint32_t* __restrict__ overflow,
+                                                      uint32_t lis, uint32_t* __restrict__ first_old,
+                                                      uint32_t* __restrict__ has_old,
+                                                      const uint32_t* __restrict__ spill,
+                                                      const uint32_t* __restrict__ cb_outs) {
+  constexpr int NPER = MRG_NEW_CAP / SORT_NT;
+  __shared__ uint32_t s_old[SORT_CAP];
+  __shared__ uint32_t s_new[MRG_NEW_CAP];
+  __shared__ uint16_t s_kpos[MRG_NEW_CAP];
+  __shared__ uint32_t s_bin[(1u << MRG_LNB_MAX) + 1];
+  __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
+  __shared__ uint32_t s_big;
+  DBG_PHASE_K(5, 15);
+  const uint32_t cb = xcd_chunk(blockIdx.x, gridDim.x);
+  const uint32_t f = cb_filter[cb];
+  const FilterPlan& P = plans[f];
+  const uint32_t n = cb_count[cb];
+  if (n > SORT_CAP) {  // K4b
+    if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
+    return;
+  }
+  const uint32_t no = ob_n[cb], nn = n - no;
+  if (nn > MRG_NEW_CAP) {  // k_cb_sort, list mode
+    if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb | 0x80000000u;
+    return;
+  }
+  const uint32_t cbl = cb - P.cb_base;
+  const uint32_t cb_rel = (spill && *spill == 0) ? cbl * CB_REGION : cb_start[cb];
+  const uint32_t cb_out = cb_outs[cb];
+  const uint32_t vs = P.vs, rvs = P.rvs, ovs = P.old_vs, bbits = P.bbits;
+  const bool od = P.old_direct != 0;
+  const uint32_t ipc = 1u << (bbits - lis), ish = lis + rvs;
+  const uint32_t idx0 = P.idx_base + (cbl << (bbits - lis));
+  // an old entry as this filter sees it (read in place from an engine-built old batch: value
+  // bits re-widened to the new value_size, src/routing_filter.c:536-543; the order is unchanged)
+  auto okey = [&](uint32_t raw) -> uint32_t { return od ? ((raw >> ovs) << vs) | (raw & ((1u << ovs) - 1u)) : raw; };
+  auto index_of = [&](uint32_t e) -> uint32_t { return ish >= 32 ? 0u : ((e >> ish) & (ipc - 1)); };
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+  // 1. the old run into LDS (LDS-DMA, a dword per lane), landing while the new entries sort
+  {
+    const uint32_t* osrc = (od ? P.old_entries : old32 + P.old_first) + ob_lo[cb];
+    for (uint32_t i0 = wv * WAVE; i0 < no; i0 += SORT_NT)
+      if (i0 + lane < no)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(osrc + i0 + lane),
+                                         (__attribute__((address_space(3))) void*)(s_old + i0), 4, 0, 0);
+  }
+  // 2. the new entries ((e << 1) | 1 in the partition region): bins over their top bits,
+  //    about four entries per bin
+  uint32_t lnb = 0;
+  while (lnb < MRG_LNB_MAX && lnb < bbits && (8u << lnb) <= nn) lnb++;
+  const uint32_t nb = 1u << lnb, bsh = rvs + bbits - lnb;
+  auto bin_of = [&](uint32_t e) -> uint32_t { return lnb ? (e >> bsh) & (nb - 1) : 0u; };
+  const uint32_t* nsrc = part + P.e_first + cb_rel;
+  uint32_t v[NPER], rk[NPER];
+#pragma unroll
+  for (int k = 0; k < NPER; k++) {
+    const uint32_t j = threadIdx.x + k * SORT_NT;
+    v[k] = j < nn ? nsrc[j] >> 1 : 0u;
+  }
+  for (uint32_t i = threadIdx.x; i <= nb; i += SORT_NT) s_bin[i] = 0;
+  if (threadIdx.x == 0) s_big = 0;
+  __syncthreads();
+  DBG_PHASE_K(5, 0);
+#pragma unroll
+  for (int k = 0; k < NPER; k++)
+    if (threadIdx.x + k * SORT_NT < nn) rk[k] = atomicAdd(&s_bin[bin_of(v[k])], 1u);
+  __syncthreads();
+  DBG_PHASE_K(5, 1);
+  if (wv == 0) {  // exclusive scan of the nb <= 512 counts: 8 per lane
+    uint32_t c8[8], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t b = lane * 8 + q;
+      c8[q] = b < nb ? s_bin[b] : 0u;
+      sum += c8[q];
+    }
+    uint32_t run = wave_incl_scan(sum) - sum;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t b = lane * 8 + q;
+      if (b < nb) s_bin[b] = run;
+      run += c8[q];
+    }
+    if (lane == WAVE - 1) s_bin[nb] = run;
+  }
+  __syncthreads();
+  DBG_PHASE_K(5, 2);
+#pragma unroll
+  for (int k = 0; k < NPER; k++)
+    if (threadIdx.x + k * SORT_NT < nn) s_new[s_bin[bin_of(v[k])] + rk[k]] = v[k];
+  __syncthreads();
+  DBG_PHASE_K(5, 3);
+  {  // order inside the bins: segments of S bins (about 8 entries) sorted by one thread each
+    uint32_t S = 8;
+    while (S > 1 && S * nn > 8 * nb) S >>= 1;
+    if (S > nb) S = nb;
+    const uint32_t nseg = nb / S;
+    for (uint32_t sg = threadIdx.x; sg < nseg; sg += SORT_NT) {
+      const uint32_t b0 = sg * S, st = s_bin[b0], c = s_bin[b0 + S] - st;
+      if (c <= 16) {
+        uint32_t x[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) x[j] = (uint32_t)j < c ? s_new[st + j] : 0xffffffffu;
+        sort16(x);
+        if (c >= 2) {
+#pragma unroll
+          for (int j = 0; j < 16; j++)
+            if ((uint32_t)j < c) s_new[st + j] = x[j];
+        }
+      } else {
+        for (uint32_t b = b0; b < b0 + S; b++) {
+          const uint32_t bs = s_bin[b], bc = s_bin[b + 1] - bs;
+          if (bc > WAVE) {
+            s_big = 1;  // duplicate-heavy input: k_cb_sort takes the bucket
+          } else {
+            for (uint32_t i = bs + 1; i < bs + bc; i++) {  // insertion sort, at most 64
+              const uint32_t x = s_new[i];
+              uint32_t q = i;
+              while (q > bs && s_new[q - 1] > x) {
+                s_new[q] = s_new[q - 1];
+                q--;
+              }
+              s_new[q] = x;
+            }
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the old run has landed
+  __syncthreads();                                   // ... and every wave's
+  DBG_PHASE_K(5, 4);
+  if (s_big) {
+    if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb | 0x80000000u;
+    return;
+  }
+  // 3. drop new duplicates (of the previous new entry, or of an old one); the kept ones'
+  //    final positions. Thread t takes new entries [t NPER, t NPER + NPER).
+  uint32_t kv[NPER], kp[NPER], kc = 0;
+  bool keep[NPER];
+#pragma unroll
+  for (int k = 0; k < NPER; k++) {
+    const uint32_t j = threadIdx.x * NPER + k;
+    keep[k] = false;
+    kv[k] = 0;
+    kp[k] = 0;
+    if (j < nn) {
+      const uint32_t e = s_new[j];
+      kv[k] = e;
+      if (j == 0 || s_new[j - 1] != e) {
+        uint32_t lo = 0, hi = no;  // old entries <= e
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (okey(s_old[mid]) <= e) lo = mid + 1; else hi = mid;
+        }
+        keep[k] = !(lo > 0 && okey(s_old[lo - 1]) == e);
+        kp[k] = lo;
+      }
+    }
+    kc += keep[k] ? 1u : 0u;
+  }
+  uint32_t kn;
+  uint32_t r = block_excl_scan<SORT_NT>(kc, s_tmp, &kn);  // its barriers: every s_new read done
+#pragma unroll
+  for (int k = 0; k < NPER; k++)
+    if (keep[k]) {
+      s_new[r] = kv[k];
+      s_kpos[r] = (uint16_t)(r + kp[k]);  // < n <= SORT_CAP
+      r++;
+    }
+  __syncthreads();
+  DBG_PHASE_K(5, 5);
+  // 4. the merged entries, 64 output slots per wave step, each wave a contiguous range
+  const uint32_t tot = no + kn;
+  uint32_t* dst = sorted32 + P.e_first + cb_out;
+  const uint32_t nch = (tot + WAVE - 1) / WAVE, cpw = (nch + SORT_NT / WAVE - 1) / (SORT_NT / WAVE);
+  const uint32_t c0 = wv * cpw, c1 = min(nch, c0 + cpw);
+  uint32_t uniq = 0;
+  if (c0 < c1) {
+    // kept new entries before the range (positions are increasing)
+    uint32_t j = 0;
+    {
+      uint32_t lo = 0, hi = kn;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_kpos[mid] < c0 * WAVE) lo = mid + 1; else hi = mid;
+      }
+      j = lo;
+    }
+    // the entry just before the range
+    uint32_t carry = 0;
+    bool carry_ok = false;
+    if (c0 > 0) {
+      const uint32_t sl = c0 * WAVE - 1;
+      carry = (j > 0 && s_kpos[j - 1] == sl) ? s_new[j - 1] : okey(s_old[sl - j]);
+      carry_ok = true;
+    }
+    for (uint32_t c = c0; c < c1; c++) {
+      const uint32_t base = c * WAVE;
+      const uint32_t p = j + lane < kn ? (uint32_t)s_kpos[j + lane] - base : WAVE;
+      const uint32_t m = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(p < WAVE));
+      uint64_t mask = 0;
+      for (uint32_t t = 0; t < m; t++) mask |= 1ull << __builtin_amdgcn_readlane((int)p, t);
+      const uint32_t sl = base + lane;
+      const bool valid = sl < tot;
+      const bool isn = (mask >> lane) & 1ull;
+      const uint32_t kb = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+      uint32_t e = 0;
+      if (valid) e = isn ? s_new[j + kb] : okey(s_old[sl - j - kb]);
+      uint32_t prev = __shfl_up(e, 1, WAVE);
+      bool has_prev = lane > 0;
+      if (lane == 0) {
+        prev = carry;
+        has_prev = carry_ok;
+      }
+      // num_unique (:558, :572-574): an entry whose fingerprint differs from its predecessor's;
+      // an index's first entry compares against UINT32_MAX >> value_size
+      const uint32_t li = index_of(e), fp = e >> vs;
+      const bool first = !has_prev || index_of(prev) != li;
+      if (valid && fp != (first ? (0xffffffffu >> vs) : (prev >> vs))) uniq++;
+      if (valid) dst[sl] = e;
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)e, WAVE - 1);
+      carry_ok = true;
+      j += m;
+    }
+  }
+  DBG_PHASE_K(5, 6);
+  // 5. per index: its entries' start and count; the smallest old entry (num_unique quirk, only
+  //    for builds that split old indices: npo > 1)
+  const bool track_old = P.npo > 1;
+  for (uint32_t li = threadIdx.x; li < ipc; li += SORT_NT) {
+    auto lb_old = [&](uint32_t key) {
+      uint32_t lo = 0, hi = no;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (index_of(okey(s_old[mid])) < key) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    auto lb_new = [&](uint32_t key) {
+      uint32_t lo = 0, hi = kn;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (index_of(s_new[mid]) < key) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    const uint32_t ol = lb_old(li), oh = li + 1 < ipc ? lb_old(li + 1) : no;
+    const uint32_t nl = lb_new(li), nh = li + 1 < ipc ? lb_new(li + 1) : kn;
+    idx_cnt[idx0 + li] = (oh - ol) + (nh - nl);
+    idx_start[idx0 + li] = cb_out + ol + nl;
+    if (track_old) {
+      first_old[idx0 + li] = oh > ol ? okey(s_old[ol]) : 0xffffffffu;
+      has_old[idx0 + li] = oh > ol ? 1u : 0u;
+    }
+  }
+  DBG_PHASE_K(5, 7);
+  uint32_t tot_uniq;
+  block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
+  if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
+  DBG_PHASE_K(5, 8);
 }
 
 // K4b: coarse buckets larger than LDS (duplicate-heavy inputs). One workgroup per listed
@@ -1038,6 +1343,7 @@ __global__ __launch_bounds__(BIG_NT) void k_cb_sort_big(const FilterPlan* __rest
   const uint32_t nover = overflow[0];
   for (uint32_t it = blockIdx.x; it < nover; it += gridDim.x) {
     const uint32_t cb = overflow[1 + it];
+    if (cb >> 31) continue;  // K4m's fallback entries: k_cb_sort in list mode
     const uint32_t f = cb_filter[cb];
     const FilterPlan& P = plans[f];
     const uint32_t n = cb_count[cb];
@@ -3131,6 +3437,75 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe(const uint4* __restric
   __builtin_nontemporal_store(r, found + i0);
 }
 
+// The probe's memory floor (bench.py roofline.floor_ms; not a lookup): k_probe's fast path with
+// its arithmetic taken out -- the same grid and wave order, the same 24-byte key staging by
+// LDS-DMA (or hash loads), the same quad gather of one 64-B line per probe from the probe's own
+// filter into the same LDS slots, the same coalesced 8-byte store -- but the line comes from a
+// multiply-xorshift of the key words instead of XXH32, and the stored word is an XOR of the
+// line's quarter instead of its decode. Waves that are not fast-path material store 0.
+template <int KIND>
+__global__ __launch_bounds__(probe_nt(KIND)) void k_probe_floor(const uint4* __restrict__ pplans,
+                                                          const uint4* __restrict__ lines,
+                                                          const void* __restrict__ in0,
+                                                          const uint32_t* __restrict__ wave_tab, uint64_t n,
+                                                          uint64_t* __restrict__ found, uint32_t fp_size,
+                                                          uint32_t nf) {
+  constexpr int NT = probe_nt(KIND);
+  __shared__ v4u s_wbuf[NT / WAVE][FAST_WBUF];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x) / WAVE;
+  const uint64_t wf = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * NT + wv * WAVE;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  if (wf >= n) return;
+  const uint32_t t = sload32(wave_tab + wf / WAVE);
+  const uint32_t fs = t >> 7;
+  uint32_t lgl = 0, rem = 0, base = 0;
+  if ((t & 127u) == WAVE && fs < nf && wf + WAVE <= n) {
+    const uint32_t x = sload32(&pplans[fs].x);
+    lgl = x >> 24;
+    rem = (x >> 8) & 0xff;
+    base = sload32(&pplans[fs].y);
+  }
+  if (!lgl || rem == 0 || rem >= 32) {
+    if (wf + lane < n) found[wf + lane] = 0;
+    return;
+  }
+  v4u* sw = s_wbuf[wv];
+  uint32_t h;
+  if constexpr (KIND == IN_KEYS24) {
+    const uint8_t* kb = static_cast<const uint8_t*>(in0) + wf * 24;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + lane * 16),
+                                     (__attribute__((address_space(3))) void*)sw, 16, 0, 2);
+    if (lane < 32)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)(sw + WAVE), 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync_lds();
+    const uint2* k2 = reinterpret_cast<const uint2*>(sw) + 3 * lane;
+    const uint2 a = k2[0], b = k2[1], c = k2[2];
+    h = (a.x ^ a.y ^ b.x ^ b.y ^ c.x ^ c.y) * 0x9e3779b1u;
+    h ^= h >> 15;
+    h *= 0x85ebca77u;
+  } else {
+    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + wf + lane);
+  }
+  const uint32_t bucket = (h >> (32 - fp_size)) >> rem;
+  const uint8_t* fb = reinterpret_cast<const uint8_t*>(lines) + ((uint64_t)base << 6);
+  const uint32_t lo = (bucket >> (lgl - 1)) << 6, q16 = (lane & 3) << 4;
+  uint8_t* sb = reinterpret_cast<uint8_t*>(sw);
+#define RF_FLOOR_LOAD(k)                                                                                      \
+  {                                                                                                           \
+    const uint32_t lk = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, (k) * 0x55, 0xf, 0xf, false);             \
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(fb + (lk + q16)),        \
+                                     (__attribute__((address_space(3))) void*)(sb + (k) * FAST_KSTRIDE), 16, 0, 0); \
+  }
+  RF_FLOOR_LOAD(0) RF_FLOOR_LOAD(1) RF_FLOOR_LOAD(2) RF_FLOOR_LOAD(3)
+#undef RF_FLOOR_LOAD
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wave_sync_lds();
+  const v4u E = *reinterpret_cast<const v4u*>(sb + (lane & 3) * FAST_KSTRIDE + (lane >> 2) * 64);
+  __builtin_nontemporal_store((uint64_t)(E[0] ^ E[1] ^ E[2] ^ E[3]), found + wf + lane);
+}
+
 // one lookup of hash h in a resident filter given by its group descriptor (its own routing
 // config: one launch may answer filters of differently configured kvstores)
 __device__ __forceinline__ uint64_t probe_group(const ProbeGroup& G, uint32_t h) {
@@ -3418,11 +3793,32 @@ static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const ui
   return 0;
 }
 
+// K4m for 32-bit incremental builds (RF_AMD_K4M=1; default: the K4 DUAL sort)
+static bool k4m_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RF_AMD_K4M");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v != 0;
+}
+
 template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* spill) {
-  hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
-                     a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt, a.idx_start,
-                     a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
+  if (DUAL && k4m_enabled()) {
+    hipLaunchKernelGGL(k_cb_merge, dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
+                       a.cb_count, a.cb_start, (const uint32_t*)part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt,
+                       a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
+    CHECK_LAUNCH();
+    // the buckets K4m handed back (bit 31 on their overflow-list entry)
+    hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(BIG_GRID), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
+                       a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt,
+                       a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs, a.overflow);
+  } else {
+    hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
+                       a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt,
+                       a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs, nullptr);
+  }
   CHECK_LAUNCH();
   REC(EV_B_SORT);
   hipLaunchKernelGGL((k_cb_sort_big<EntT, FL, DUAL>), dim3(BIG_GRID), dim3(BIG_NT), 0, (hipStream_t)a.stream, a.plans,
@@ -3599,6 +3995,22 @@ extern "C" int rf_launch_wave_tab(void* stream, const uint64_t* runs, uint32_t n
   const uint64_t nw = (n + WAVE - 1) / WAVE;
   if (nw == 0) return 0;
   hipLaunchKernelGGL(k_wave_tab, dim3((uint32_t)((nw + 255) / 256)), dim3(256), 0, (hipStream_t)stream, runs, nf, n, tab);
+  CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rf_launch_probe_floor(const LaunchArgs* pa, int kind, const void* in0, uint64_t n, uint64_t* found) {
+  const LaunchArgs& a = *pa;
+  if (n == 0) return 0;
+  if (!a.wave_tab || (kind != IN_KEYS24 && kind != IN_HASH)) return (int)hipErrorInvalidValue;
+  const int nt = probe_nt(kind);
+  dim3 g((uint32_t)((n + nt - 1) / nt)), b(nt);
+  if (kind == IN_KEYS24)
+    hipLaunchKernelGGL((k_probe_floor<IN_KEYS24>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.lines, in0, a.wave_tab, n,
+                       found, a.fp_size, a.num_filters);
+  else
+    hipLaunchKernelGGL((k_probe_floor<IN_HASH>), g, b, 0, (hipStream_t)a.stream, a.pplans, a.lines, in0, a.wave_tab, n,
+                       found, a.fp_size, a.num_filters);
   CHECK_LAUNCH();
   return 0;
 }

@@ -36,6 +36,7 @@ EXPORTED = [
     "rf_amd_batch_read_image", "rf_amd_batch_read_image_async", "rf_amd_batch_image_ptrs", "rf_amd_batch_num_filters",
     "rf_amd_batch_set_timing", "rf_amd_batch_timings", "rf_amd_batch_timings_back", 
     "rf_amd_debug_read_lines", "rf_amd_debug_rebuild_lines", "rf_amd_debug_phase_buffer", "rf_amd_diag_lookup_stats",
+    "rf_amd_debug_probe_floor",
     "rf_amd_host_alloc", "rf_amd_host_free", "rf_amd_engine_fence", "rf_amd_engine_fence_wait",
     "rf_amd_host_register", "rf_amd_host_unregister", "rf_amd_batch_place_image", "rf_amd_engine_set_pool_limit",
     "rf_amd_lookup_submit", "rf_amd_lookup_wait", "rf_amd_lookup_reap", "rf_amd_lookup_server_stats",
@@ -143,6 +144,7 @@ def load_library(build_if_missing=True):
     L.rf_amd_debug_read_lines.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
     L.rf_amd_debug_rebuild_lines.argtypes = [vp]
     L.rf_amd_debug_phase_buffer.argtypes = [vp, u32]
+    L.rf_amd_debug_probe_floor.argtypes = [vp, vp, u32, vp, vp, vp]
     L.rf_amd_diag_lookup_stats.argtypes = [vp, ctypes.c_int]
     L.rf_amd_lookup_submit.argtypes = [vp, vp, u32, u32, vp, ctypes.POINTER(u64)]
     L.rf_amd_lookup_wait.argtypes = [vp, u64, ctypes.POINTER(u64)]
@@ -698,6 +700,13 @@ class FilterBatch:
         c = (ctypes.c_uint64 * self.F)(*[int(x) for x in counts])
         _check(load_library().rf_amd_batch_probe_hashes_runs(self.h, _dptr(d_hashes), c, _dptr(d_found),
                                                              _stream(stream)))
+
+    def probe_floor(self, d_in, key_len, counts, d_out, stream=None):
+        """The probe's memory floor (rf_amd_debug_probe_floor): the fast path's traffic over the
+        same runs with the arithmetic removed; d_out gets no lookup results."""
+        c = (ctypes.c_uint64 * self.F)(*[int(x) for x in counts])
+        _check(load_library().rf_amd_debug_probe_floor(self.h, _dptr(d_in), key_len, c, _dptr(d_out),
+                                                       _stream(stream)))
 
     def probe_pairs(self, d_pairs, n, d_found, stream=None):
         """Probes given as (local filter id << 32 | hash) u64 pairs (routed probes, route.py)."""

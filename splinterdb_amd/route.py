@@ -60,9 +60,12 @@ class ProbeRouter:
     shards: shard.plan_shards(...) (the same on every rank); batch: this rank's FilterBatch
     (its filters in global order, local id = global id - filter_begin). coll_device is
     where the collectives run: the GPU under RCCL, "cpu" under gloo (rehearsal/tests).
+    collective_at_one: run the all-to-alls through `dist` with one rank too (the RCCL path of
+    a multi-GPU run, exercised on one GPU), instead of a local copy.
     """
 
-    def __init__(self, shards, rank, batch, device, dist=None, coll_device=None, ops=None):
+    def __init__(self, shards, rank, batch, device, dist=None, coll_device=None, ops=None,
+                 collective_at_one=False):
         import torch
         self.torch = torch
         self.shards, self.rank, self.batch = shards, rank, batch
@@ -74,6 +77,7 @@ class ProbeRouter:
         self.dist = dist
         self.coll_device = torch.device(coll_device) if coll_device is not None else self.device
         self.ops = ops or GpuRouteOps()
+        self.local = self.world == 1 and not (collective_at_one and dist is not None)
         self.d_route = torch.from_numpy(route_table(shards).view(np.int32)).to(self.device)
         self._cap = -1
 
@@ -89,7 +93,7 @@ class ProbeRouter:
     def _a2a(self, out, inp, out_splits, in_splits):
         """all_to_all_single on the collective device (copies through it under gloo)."""
         t = self.torch
-        if self.world == 1:
+        if self.local:
             out.copy_(inp)
             return
         if self.coll_device == out.device and self.coll_device == inp.device:
@@ -105,7 +109,7 @@ class ProbeRouter:
         self._buffers(n)
         send = self.ops.route(d_hashes, d_gfid, n, self.d_route, self.num_filters, self.world,
                               self.d_pairs, self.d_perm, self.d_scratch)
-        if self.world == 1:
+        if self.local:
             recv = list(send)
         else:
             sc = t.tensor(send, dtype=t.int64, device=self.coll_device)

@@ -122,3 +122,25 @@ def test_fast_path_equals_general_path_at_c2_size():
     torch.cuda.synchronize()
     assert bool(((f_fast >> 7) & 1).all())
     assert torch.equal(f_fast, f_gen)
+
+
+def test_probe_floor_stays_in_bounds():
+    """rf_amd_debug_probe_floor (bench.py's measured floor) over runs that do and do not fall on
+    wave boundaries: it writes exactly the n output words, nothing past them"""
+    cfg = E.routing_config_init(log_index_size=8)
+    sizes = [300000, 5000, 200001]
+    keys = K.seq_keys_torch(0, sum(sizes), 24, torch.device("cuda", 0))
+    b = E.FilterBatch(cfg, sizes, [0, 1, 2])
+    b.build_keys(keys, 24)
+    for counts in ([64 * 3000, 64 * 50, 64 * 2500], [191999, 3333, 160007]):
+        N = sum(counts)
+        out = torch.full((N + 4096,), -7, dtype=torch.int64, device="cuda:0")
+        b.probe_floor(keys, 24, counts, out)
+        h = torch.zeros(N, dtype=torch.int32, device="cuda:0")
+        E.hash_keys(cfg, keys[:N], 24, N, h)
+        b.probe_floor(h, 4, counts, out)
+        torch.cuda.synchronize()
+        assert bool((out[N:] == -7).all())
+        assert int((out[:N] == -7).sum()) == 0
+    with pytest.raises(Exception):
+        b.probe_floor(keys, 8, [1, 1, 1], out)

@@ -7,9 +7,8 @@
 #      traffic from (1), the compaction chain's kernel trace, the shim's per-call costs and the
 #      reference's own kvstore driving the shim (tools/trunk_latency.py).
 # usage: bash tools/profile_round.sh <tag>      (outputs under gpurun_out/prof_<tag>/)
-# (build the per-lane probe variant first, here: tools/ab_build.sh WT quad0 "-DRF_PROBE_QUAD=0")
 set -o pipefail
-TAG=${1:-r04}
+TAG=${1:-r05}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/prof_$TAG
@@ -32,17 +31,10 @@ TCC="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"
 timeout -s KILL 120 rocprofv3 --pmc $TCC --output-format csv -d $O/tcc2 -o c2 -- python3 $BENCH > $O/tcc2.log 2>&1 || { echo "pmc tcc c2 failed"; exit 1; }
 timeout -s KILL 180 rocprofv3 --pmc $TCC --output-format csv -d $O/tcc3 -o c3 -- python3 $BENCH --workload c3 > $O/tcc3.log 2>&1 || { echo "pmc tcc c3 failed"; exit 1; }
 python3 tools/tcc_summary.py $O/tcc2/c2_counter_collection.csv $O/tcc3/c3_counter_collection.csv > $O/tcc_$TAG.txt || exit 1
-# the probe's per-lane line gather (RF_PROBE_QUAD=0, tools/ab/librf_amd_quad0.so built by
-# tools/ab_build.sh) beside the shipped quad-cooperative one: kernel trace, L2 and SQ counters
-if [ -f tools/ab/librf_amd_quad0.so ]; then
-  export RF_AMD_LIB=tools/ab/librf_amd_quad0.so
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktq0 -o c2 -- python3 $BENCH > $O/ktq0.log 2>&1 || { echo "quad0 kernel trace failed"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc $TCC --output-format csv -d $O/tccq0 -o c2 -- python3 $BENCH > $O/tccq0.log 2>&1 || { echo "pmc tcc quad0 failed"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d $O/sqq0 -o c2 -- python3 $BENCH > $O/sqq0.log 2>&1 || { echo "pmc sq quad0 failed"; exit 1; }
-  unset RF_AMD_LIB
-  python3 tools/tcc_summary.py $O/tccq0/c2_counter_collection.csv > $O/tcc_quad0_$TAG.txt || exit 1
-  python3 tools/sq_summary.py $O/sqq0/c2_counter_collection.csv > $O/sq_quad0_$TAG.txt || exit 1
-fi
+# C3 (L2-resident line tables): kernel trace and SQ counters of the probe and the build
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt3 -o c3 -- python3 $BENCH --workload c3 > $O/kt3.log 2>&1 || { echo "c3 kernel trace failed"; exit 1; }
+timeout -s KILL 180 rocprofv3 --pmc $SQ --output-format csv -d $O/sq3 -o c3 -- python3 $BENCH --workload c3 > $O/sq3.log 2>&1 || { echo "pmc sq c3 failed"; exit 1; }
+python3 tools/sq_summary.py $O/sq3/c3_counter_collection.csv > $O/sq_c3_$TAG.txt || exit 1
 timeout -k 10 300 python3 bench.py --workload compaction --steps 5 --warmup 1 > $O/bench_compaction.json 2> $O/bench_compaction.err || { echo "bench compaction failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktc -o comp -- python3 bench.py --workload compaction --steps 2 --warmup 0 --no-cpu-baseline > $O/ktc.log 2>&1 || { echo "compaction kernel trace failed"; exit 1; }
 # the drop-in's per-call costs beside the reference's routing_filter.c (tools/shim_latency.py)
