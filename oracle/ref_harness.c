@@ -295,6 +295,13 @@ typedef struct rfr_stack {
 
 static _Atomic int g_registered_main = 0;
 
+
+/* the shim's cache attach / release (weak: absent from the reference's own library) */
+__attribute__((weak)) int
+routing_filter_amd_cache_attach(cache *cc);
+__attribute__((weak)) void
+routing_filter_amd_cache_release(cache *cc);
+
 rfr_stack *
 rfr_create(uint32 fingerprint_size, uint32 log_index_size, uint64 cache_mib, uint64 disk_mib)
 {
@@ -339,16 +346,17 @@ rfr_create(uint32 fingerprint_size, uint32 log_index_size, uint64 cache_mib, uin
       return NULL;
    }
    default_data_config_init(&s->data_cfg);
+   /* the shim: this cache attached (images placed straight into its pages; released in
+      rfr_destroy before the buffer is unmapped) */
+   if (routing_filter_amd_cache_attach) {
+      (void)routing_filter_amd_cache_attach((cache *)&s->cc);
+   }
    /* splinterdb.c:270-276 / tests/functional/test.h: hash argument ignored, seed 42 */
    routing_config_init(&s->rcfg, (cache_config *)&s->cc_cfg, &s->data_cfg, fingerprint_size,
                        log_index_size, NULL, 42);
    return s;
 }
 
-/* the shim's release of a cache whose page buffer took images directly (weak: absent from
- * the reference's own library) */
-__attribute__((weak)) void
-routing_filter_amd_cache_release(cache *cc);
 
 void
 rfr_destroy(rfr_stack *s)

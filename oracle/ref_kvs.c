@@ -218,8 +218,8 @@ __attribute__((weak)) void
 routing_filter_amd_direct_stats(uint64 *out);
 __attribute__((weak)) void
 routing_filter_amd_add_breakdown(uint64 *out);
-__attribute__((weak)) void
-routing_filter_amd_prewarm(cache *cc);
+__attribute__((weak)) int
+routing_filter_amd_cache_attach(cache *cc);
 
 /* the shim's routing_filter_add breakdown (out[0..10], zeros with the reference) */
 void
@@ -233,13 +233,14 @@ rfk_add_breakdown(uint64 *out)
    }
 }
 
-/* the shim's engine and this store's cache registration made now (no-op with the reference) */
-void
-rfk_prewarm(rfk_kvs *k)
+/* the shim's engine made now and this store's cache attached: its page buffer registered for
+ * direct placement (-1 with the reference, or when the shim keeps the bounce path) */
+int
+rfk_attach(rfk_kvs *k)
 {
-   if (routing_filter_amd_prewarm) {
-      routing_filter_amd_prewarm((cache *)splinterdb_get_cache_handle(k->kvs));
-   }
+   return routing_filter_amd_cache_attach
+             ? routing_filter_amd_cache_attach((cache *)splinterdb_get_cache_handle(k->kvs))
+             : -1;
 }
 
 /* release = 0 closes the store as the unmodified reference does: without telling the shim */

@@ -11,6 +11,7 @@ the reference's routing_filter.c (KVS_REF) and once with the drop-in shim (KVS_S
 """
 import ctypes
 import os
+import time
 
 import numpy as np
 
@@ -47,8 +48,8 @@ def lib(path):
         L.rfk_direct_stats.restype = None
         L.rfk_add_breakdown.argtypes = [ctypes.POINTER(u64)]
         L.rfk_add_breakdown.restype = None
-        L.rfk_prewarm.argtypes = [vp]
-        L.rfk_prewarm.restype = None
+        L.rfk_attach.argtypes = [vp]
+        L.rfk_attach.restype = i32
         L.rfk_insert.argtypes = [vp, vp, u32, vp, u32, u64]
         L.rfk_insert.restype = i32
         L.rfk_lookup.argtypes = [vp, vp, u32, u64, vp, vp]
@@ -67,24 +68,26 @@ def _p(a):
 
 class Kvs:
     def __init__(self, path=KVS_REF, cache_mib=1024, disk_mib=8192, memtable_mib=4, filter_hash_size=26,
-                 filter_log_index_size=8, record_digest=True, release=True):
-        """release=False: close without routing_filter_amd_cache_release, as the unmodified
-        reference's splinterdb_close does"""
+                 filter_log_index_size=8, record_digest=True, attach=True):
+        """attach=True: the shim's cache attach after the store opens (direct placement of the
+        images into the cache pages) and its release before the store closes; attach=False: the
+        store driven exactly as the unmodified reference does (no shim extension called)"""
         self.L = lib(path)
-        self.release = release
         self.h = self.L.rfk_open(cache_mib, disk_mib, memtable_mib, filter_hash_size, filter_log_index_size,
                                  int(record_digest))
         if not self.h:
             raise RuntimeError("splinterdb_create failed")
+        self.attached = False
+        self.attach_s = 0.0
+        if attach:
+            t = time.perf_counter()
+            self.attached = self.L.rfk_attach(self.h) == 0
+            self.attach_s = time.perf_counter() - t
 
     def close(self):
         if self.h:
-            self.L.rfk_close_ex(self.h, int(self.release))
+            self.L.rfk_close_ex(self.h, int(self.attached))
             self.h = None
-
-    def prewarm(self):
-        """the shim's engine and this store's cache registration now (no-op: reference)"""
-        self.L.rfk_prewarm(self.h)
 
     def add_breakdown(self):
         """the shim's routing_filter_add time split (ns totals; zeros with the reference)"""

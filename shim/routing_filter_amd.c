@@ -758,21 +758,26 @@ pin_give(rf_amd_engine *e, void *p, uint64 cap)
 }
 
 /* ---- images placed straight into the cache's pages -----------------------------------------
- * The cache's page buffer (clockcache.c:3426, one platform_buffer of cfg->capacity bytes) is
- * registered with the engine once; an add then writes its image into the pages it allocated
- * with one kernel (its stores cross PCIe), instead of a read-back into a bounce buffer and a
- * memcpy per page (src/routing_filter.c:603-633 fills the pages in place too). The cache is a
- * clockcache (SplinterDB's only cache); every destination is checked against the registered
- * range by the engine before the launch. RF_SHIM_DIRECT=0 keeps the bounce-buffer path. */
+ * A cache attached by routing_filter_amd_cache_attach has its page buffer (clockcache.c:3426,
+ * one platform_buffer of cfg->capacity bytes) registered with the engine; an add then writes
+ * its image into the pages it allocated with one kernel (its stores cross PCIe), instead of a
+ * read-back into a bounce buffer and a memcpy per page (src/routing_filter.c:603-633 fills the
+ * pages in place too). The cache is a clockcache (SplinterDB's only cache); every destination
+ * is checked against the registered range by the engine before the launch.
+ * Registration is opt-in because only the caller knows the buffer's lifetime: the unmodified
+ * reference unmaps it in splinterdb_close (clockcache.c:3546 -> platform_buffer.c:86) without
+ * telling the shim, and a GPU store through a registration whose pages were unmapped is a GPU
+ * memory fault, not a detectable miss. So caches are never registered implicitly: an
+ * unmodified caller gets the bounce-buffer path; a caller that attaches a cache after opening
+ * the store releases it (routing_filter_amd_cache_release) before closing it.
+ * RF_SHIM_DIRECT=0 keeps the bounce-buffer path even for attached caches. */
 #define DIRECT_CACHES 16
 static struct {
    const cache *cc;
    char        *base;
    uint64       bytes;
-   int          ok;       /* registered, placements go straight into its pages */
-   int          stale;    /* a placement's canary showed the registration no longer maps the buffer */
-   int          released; /* routing_filter_amd_cache_release: no registration of this buffer again
-                             (adds while the store closes) until prewarm or another buffer */
+   int          ok;       /* attached and registered: placements go straight into its pages */
+   int          stale;    /* a placement's canary showed its stores did not reach the host's pages */
    uint32       inflight; /* adds placing through this registration now */
 } g_direct[DIRECT_CACHES];
 static uint32          g_direct_n;
@@ -799,64 +804,38 @@ direct_register(rf_amd_engine *e, uint32 i, char *base, uint64 bytes)
       RF_SHIM_DIRECT_MAX_MIB (default 65,536) keep the bounce-buffer path */
    const uint64 max_b = env_u64("RF_SHIM_DIRECT_MAX_MIB", 65536) << 20;
    const uint64 t0    = mono_ns();
-   g_direct[i].base     = base;
-   g_direct[i].bytes    = bytes;
-   g_direct[i].stale    = 0;
-   g_direct[i].released = 0;
-   g_direct[i].ok     = base && bytes && bytes <= max_b && rf_amd_host_register(e, base, bytes) == 0;
+   g_direct[i].base  = base;
+   g_direct[i].bytes = bytes;
+   g_direct[i].stale = 0;
+   g_direct[i].ok    = base && bytes && bytes <= max_b && rf_amd_host_register(e, base, bytes) == 0;
    g_register_ns += mono_ns() - t0;
    return g_direct[i].ok;
 }
 
-/* The registration an add places through: 1 + its slot when cc's page buffer is registered
- * with the engine (registering it on first use), 0 for the bounce-buffer path. The caller owns
- * one in-flight count on the slot until direct_done. The unmodified reference never tells the
- * shim that a cache closed (routing_filter_amd_cache_release is an extension), so a cache
- * whose buffer was unmapped and mapped again at the same address with the same size looks
- * unchanged here; every placement therefore verifies that its stores reached the pages the
- * host sees (place_direct's canary) and a registration found stale is replaced here. */
+/* The registration an add places through: 1 + its slot when cc is attached and its page
+ * buffer is the one registered, 0 for the bounce-buffer path. The caller owns one in-flight
+ * count on the slot until direct_done. */
 static uint32
-cache_direct(rf_amd_engine *e, cache *cc)
+cache_direct(cache *cc)
 {
    if (!direct_enabled()) {
       return 0;
    }
    uint32      slot = 0;
    clockcache *ccc  = (clockcache *)cc;
-   char       *base  = ccc->data;
-   uint64      bytes = ccc->cfg ? ccc->cfg->capacity : 0;
    pthread_mutex_lock(&g_direct_mu);
-   uint32 i = 0;
-   while (i < g_direct_n && g_direct[i].cc != cc) {
-      i++;
-   }
-   if (i == g_direct_n) { /* first use of this cache */
-      if (g_direct_n < DIRECT_CACHES) {
-         g_direct_n++;
-         g_direct[i].cc       = cc;
-         g_direct[i].inflight = 0;
-         if (direct_register(e, i, base, bytes)) {
+   for (uint32 i = 0; i < g_direct_n; i++) {
+      if (g_direct[i].cc == cc) {
+         /* a placement found stale, or another buffer behind the same cache struct (attached
+            and not released): the bounce path until the cache is attached again */
+         if (g_direct[i].ok && !g_direct[i].stale && g_direct[i].base == ccc->data
+             && ccc->cfg && g_direct[i].bytes == ccc->cfg->capacity)
+         {
             slot = i + 1;
+            g_direct[i].inflight++;
          }
+         break;
       }
-   } else if (g_direct[i].released && g_direct[i].base == base && g_direct[i].bytes == bytes) {
-      /* released and not reopened: the bounce path */
-   } else if (g_direct[i].stale || g_direct[i].base != base || g_direct[i].bytes != bytes) {
-      /* another buffer (or the same address mapped again) since: register anew once no add
-         still places through the old registration; until then, the bounce path */
-      if (g_direct[i].inflight == 0) {
-         if (g_direct[i].ok) {
-            (void)rf_amd_host_unregister(e, g_direct[i].base);
-         }
-         if (direct_register(e, i, base, bytes)) {
-            slot = i + 1;
-         }
-      }
-   } else if (g_direct[i].ok) {
-      slot = i + 1;
-   }
-   if (slot) {
-      g_direct[slot - 1].inflight++;
    }
    pthread_mutex_unlock(&g_direct_mu);
    return slot;
@@ -880,23 +859,57 @@ direct_done(uint32 slot, int stale)
    pthread_mutex_unlock(&g_direct_mu);
 }
 
-/* the engine and cc's registration made now instead of in the first routing_filter_add (a
- * store calls it once when it opens; optional) */
-void
-routing_filter_amd_prewarm(cache *cc)
+/* waits until no add places through slot i, then drops its registration (caller holds
+ * g_direct_mu) */
+static void
+direct_drop(uint32 i)
+{
+   const int was_ok = g_direct[i].ok;
+   g_direct[i].ok   = 0; /* no new add takes this registration */
+   while (g_direct[i].inflight) {
+      pthread_cond_wait(&g_direct_cv, &g_direct_mu);
+   }
+   if (was_ok) {
+      rf_amd_engine *e = engine();
+      if (e) {
+         (void)rf_amd_host_unregister(e, g_direct[i].base);
+      }
+   }
+}
+
+/* Attach: the engine now (not inside the store's first routing_filter_add) and cc's page
+ * buffer registered, so adds place their images straight into its pages. Call after the
+ * store opened; release before it closes. 0 = attached, -1 = the bounce path stays (no GPU,
+ * the buffer over RF_SHIM_DIRECT_MAX_MIB, the registration failed, or too many caches). */
+int
+routing_filter_amd_cache_attach(cache *cc)
 {
    rf_amd_engine *e = engine();
-   if (e && cc) {
-      pthread_mutex_lock(&g_direct_mu);
-      for (uint32 i = 0; i < g_direct_n; i++) {
-         if (g_direct[i].cc == cc && g_direct[i].released) {
-            g_direct[i].released = 0;
-            g_direct[i].base     = NULL; /* registers the (new) store's buffer afresh */
-         }
-      }
-      pthread_mutex_unlock(&g_direct_mu);
-      direct_done(cache_direct(e, cc), 0);
+   if (!e || !cc) {
+      return -1;
    }
+   clockcache *ccc   = (clockcache *)cc;
+   char       *base  = ccc->data;
+   uint64      bytes = ccc->cfg ? ccc->cfg->capacity : 0;
+   int         ok    = 0;
+   pthread_mutex_lock(&g_direct_mu);
+   uint32 i = 0;
+   while (i < g_direct_n && g_direct[i].cc != cc) {
+      i++;
+   }
+   if (i < g_direct_n) { /* attached before: registered anew (same or another buffer) */
+      direct_drop(i);
+   } else if (g_direct_n < DIRECT_CACHES) {
+      g_direct_n++;
+      g_direct[i].cc       = cc;
+      g_direct[i].inflight = 0;
+   } else {
+      pthread_mutex_unlock(&g_direct_mu);
+      return -1;
+   }
+   ok = direct_register(e, i, base, bytes);
+   pthread_mutex_unlock(&g_direct_mu);
+   return direct_enabled() && ok ? 0 : -1;
 }
 
 /* out[0] = caches registered now, out[1] = registrations found stale by a placement */
@@ -915,29 +928,16 @@ routing_filter_amd_direct_stats(uint64 *out)
    pthread_mutex_unlock(&g_direct_mu);
 }
 
-/* a cache is going away (its buffer may be reused): unregister it once no add still places
- * through it. The entry stays, marked released, so adds issued while the store closes take
- * the bounce-buffer path instead of registering the buffer again; a later cache with another
- * buffer replaces it, and routing_filter_amd_prewarm (a new store at the same addresses)
- * registers it afresh. */
+/* a cache is going away (its buffer will be unmapped): unregister it once no add still
+ * places through it; later adds through cc take the bounce-buffer path until it is attached
+ * again */
 void
 routing_filter_amd_cache_release(cache *cc)
 {
    pthread_mutex_lock(&g_direct_mu);
    for (uint32 i = 0; i < g_direct_n; i++) {
       if (g_direct[i].cc == cc) {
-         const int was_ok     = g_direct[i].ok;
-         g_direct[i].ok       = 0; /* no new add takes this registration */
-         g_direct[i].released = 1;
-         while (g_direct[i].inflight) {
-            pthread_cond_wait(&g_direct_cv, &g_direct_mu);
-         }
-         if (was_ok) {
-            rf_amd_engine *e = engine();
-            if (e) {
-               (void)rf_amd_host_unregister(e, g_direct[i].base);
-            }
-         }
+         direct_drop(i);
          break;
       }
    }
@@ -1303,7 +1303,7 @@ routing_filter_add(cache                *cc,
    }
 
    /* the image, on the GPU (coalesced with concurrent adds) */
-   q.direct        = cache_direct(e, cc);
+   q.direct        = cache_direct(cc);
    const uint64 tw = now_ns();
    add_submit(e, &q);
    if (q.fence) { /* this request's image has landed in its pinned buffer */

@@ -57,19 +57,22 @@ routing_filter_amd_lookup_batch(cache                *cc,
                                 uint64                n,
                                 uint64               *found);
 
-/* routing_filter_add writes its images straight into the cache's page buffer, which it
- * registers with the GPU on the cache's first add (RF_SHIM_DIRECT=0: a bounce buffer and a
- * copy per page instead). Before a cache is destroyed, this releases that registration (after
- * the adds placing through it are done). Optional: the unmodified reference never calls it;
- * every placement checks that its stores reached the pages the host sees and a registration
- * that no longer maps the cache's buffer is replaced. */
+/* Direct placement (optional). By default routing_filter_add reads each image back into a
+ * pinned bounce buffer and copies it into the cache pages it allocated. After
+ * routing_filter_amd_cache_attach(cc) -- called once the store is open; it also creates the
+ * engine -- cc's page buffer is registered with the GPU and images are written straight into
+ * its pages (RF_SHIM_DIRECT=0 keeps the bounce path). A caller that attaches a cache must call
+ * routing_filter_amd_cache_release(cc) before the cache's buffer is unmapped
+ * (splinterdb_close): release waits for the adds placing through it, then unregisters. The
+ * unmodified reference calls neither and gets the bounce path: a registration is never made
+ * behind the caller's back, because a GPU store into a buffer unmapped under its registration
+ * is a GPU memory fault. attach returns 0 when the cache is attached, -1 when the bounce path
+ * stays (no GPU, a buffer over RF_SHIM_DIRECT_MAX_MIB, or the registration failed). */
+int
+routing_filter_amd_cache_attach(cache *cc);
+
 void
 routing_filter_amd_cache_release(cache *cc);
-
-/* creates the engine and registers cc's page buffer now rather than in the first
- * routing_filter_add (optional: for a store to call when it opens) */
-void
-routing_filter_amd_prewarm(cache *cc);
 
 /* out[0]: caches registered now; out[1]: registrations a placement found stale; out[2]: adds
  * placing through a registration now */

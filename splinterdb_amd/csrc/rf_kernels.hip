@@ -1026,10 +1026,10 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
 // src/routing_filter.c:496-597). A coarse bucket's entries are its old run -- the old filter's
 // entries, already in order -- and a small share of new ones (an eighth in round 8 of a
 // compaction chain). Only the new entries are sorted (bins over their top bits sized to their
-// count, then sorting networks); each new entry is dropped if it equals the previous new one
-// or an old one (old first on equal entries, src/routing_filter.c:559-597) -- found by a
-// binary search of the old run, which also gives the kept entry's final position (its rank
-// among the kept new + the old entries not above it). The output is then written 64 slots
+// count, then sorting networks); a new entry is dropped if it equals the previous new one
+// (duplicates are dropped only among the new entries; one equal to an old entry is kept after
+// it, src/routing_filter.c:559-597). A binary search of the old run gives each kept entry's
+// final position (its rank among the kept new + the old entries not above it). The output is then written 64 slots
 // per wave step: the step's new slots form a bit mask, each lane takes its entry from the new
 // list (mbcnt of the mask) or the old run (slot - new entries before it); num_unique compares
 // each entry with its predecessor (a lane shift). The old run reaches LDS by LDS-DMA and is
@@ -1186,7 +1186,8 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __res
     if (threadIdx.x == 0) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb | 0x80000000u;
     return;
   }
-  // 3. drop new duplicates (of the previous new entry, or of an old one); the kept ones'
+  // 3. drop new duplicates of the previous new entry (only among the new ones: a new entry
+  //    equal to an old one is kept, after it -- src/routing_filter.c:559-597); the kept ones'
   //    final positions. Thread t takes new entries [t NPER, t NPER + NPER).
   uint32_t kv[NPER], kp[NPER], kc = 0;
   bool keep[NPER];
@@ -1200,12 +1201,12 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __res
       const uint32_t e = s_new[j];
       kv[k] = e;
       if (j == 0 || s_new[j - 1] != e) {
-        uint32_t lo = 0, hi = no;  // old entries <= e
+        uint32_t lo = 0, hi = no;  // old entries <= e (an equal old entry stays before it)
         while (lo < hi) {
           const uint32_t mid = (lo + hi) >> 1;
           if (okey(s_old[mid]) <= e) lo = mid + 1; else hi = mid;
         }
-        keep[k] = !(lo > 0 && okey(s_old[lo - 1]) == e);
+        keep[k] = true;
         kp[k] = lo;
       }
     }
@@ -3793,7 +3794,8 @@ static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const ui
   return 0;
 }
 
-// K4m for 32-bit incremental builds (RF_AMD_K4M=1; default: the K4 DUAL sort)
+// K4m for 32-bit incremental builds (RF_AMD_K4M=1; default: the K4 DUAL sort --
+// profiles/r05_k4m_v1_ab.json: K4m v1 2.55 vs 1.85 ms at round 8)
 static bool k4m_enabled() {
   static int v = -1;
   if (v < 0) {

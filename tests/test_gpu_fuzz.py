@@ -179,3 +179,33 @@ def test_incremental_spill_and_big_buckets(oracle, entries, monkeypatch):
     b2.probe_hashes(dev(ph), dev(np.zeros(P, dtype=np.uint32)), P, found)
     torch.cuda.synchronize()
     assert (found.cpu().numpy().view(np.uint64) == of2.lookup_hashes(ph)).all()
+
+
+@pytest.mark.parametrize("lis,n_old,frac_new,overlap", [(5, 33825, 0.5, 0.0), (5, 33825, 0.5, 0.3),
+                                                        (8, 300000, 0.125, 0.2), (8, 300000, 0.4, 0.05),
+                                                        (3, 6000, 0.33, 0.5), (8, 1 << 20, 0.33, 0.1)])
+def test_incremental_new_entries_equal_to_old(oracle, lis, n_old, frac_new, overlap):
+    """Incremental adds whose new hashes repeat old ones (same value: equal entries). The
+    reference drops duplicates only among the new entries (src/routing_filter.c:559-597): a new
+    entry equal to an old one is kept after it. Coarse buckets with new-entry counts on both
+    sides of K4m's 2,048 (fuzz case 24 had one at exactly 2,048)."""
+    rng = np.random.default_rng(lis * 1000 + n_old)
+    fp, value = 26, 23
+    cfg = E.routing_config_init(fingerprint_size=fp, log_index_size=lis)
+    ocfg = oracle.make_config(fingerprint_size=fp, log_index_size=lis)
+    h1 = rng.integers(0, 1 << 32, size=n_old, dtype=np.uint64).astype(np.uint32)
+    n2 = int(n_old * frac_new)
+    h2 = rng.integers(0, 1 << 32, size=n2, dtype=np.uint64).astype(np.uint32)
+    k = int(n2 * overlap)
+    h2[:k] = h1[rng.integers(0, n_old, size=k)]
+    h2 = h2[rng.permutation(n2)]
+    of = _oracle_add(oracle, ocfg, h1, value)
+    of2 = _oracle_add(oracle, ocfg, h2, value, old=of)
+    b = E.FilterBatch(cfg, [n_old], [value])
+    b.build_hashes(dev(h1))
+    b2 = E.FilterBatch(cfg, [n2], [value], old=[(b, 0)])
+    b2.build_hashes(dev(h2))
+    img = b2.image(0)
+    assert (img.num_unique, img.num_pages) == (of2.num_unique, of2.num_pages)
+    assert (img.slots == of2.slots()[: of2.num_indices]).all()
+    assert (img.pages == of2.pages()).all()

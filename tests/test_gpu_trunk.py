@@ -21,15 +21,15 @@ pytestmark = [pytest.mark.gpu,
                                  reason="oracle/_ref/libkvs_{ref,shim}.so not built")]
 
 
-def run(path, keys, vals, probe, memtable_mib, release=True, stats=None):
-    with RK.Kvs(path, memtable_mib=memtable_mib, release=release) as db:
+def run(path, keys, vals, probe, memtable_mib, attach=True, stats=None):
+    with RK.Kvs(path, memtable_mib=memtable_mib, attach=attach) as db:
+        if stats is not None:
+            stats.append(db.direct_stats())
         db.insert(keys, vals)
         recs, nl0, na0 = db.adds()
         f, v, _ = db.lookup(probe)
         fa, va, _ = db.lookup_async(probe, 64)
         _, nl, na = db.adds()
-        if stats is not None:
-            stats.append(db.direct_stats())
     return recs, (f, v), (fa, va), nl - nl0, na - na0
 
 
@@ -53,23 +53,24 @@ def test_trunk_filters_and_lookups_identical_to_reference(n, memtable_mib):
     assert ref[3] == shim[3] and ref[4] == shim[4]
 
 
-def test_reopen_without_release_filters_identical():
-    """The unmodified reference closes a store without routing_filter_amd_cache_release (the
-    shim's extension). Three stores opened one after another in one process, each
-    closed without it -- their cache buffers may be mapped again at the same address with the
-    same size -- must each get the reference's filters byte for byte and its lookups; a
-    registration that no longer maps its buffer is detected by the placement canary and
-    replaced."""
+@pytest.mark.parametrize("attach", [False, True])
+def test_reopened_stores_filters_identical(attach):
+    """Three stores opened and closed one after another in one process (their cache buffers
+    may be mapped again at the same address with the same size). attach=False drives them as
+    the unmodified reference does -- no shim extension called, so no cache is registered and
+    every image takes the bounce-buffer path; attach=True attaches each store's cache after
+    opening and releases it before closing (direct placement). Either way each store gets the
+    reference's filters byte for byte and its lookups."""
     stats = []
     for i, seed in enumerate((21, 22, 23)):
         keys, vals, absent = workload(300_000, seed=seed)
         probe = np.concatenate([keys[:20_000], absent[:20_000]])
-        ref = run(RK.KVS_REF, keys, vals, probe, 2)
-        shim = run(RK.KVS_SHIM, keys, vals, probe, 2, release=False, stats=stats)
+        ref = run(RK.KVS_REF, keys, vals, probe, 2, attach=False)
+        shim = run(RK.KVS_SHIM, keys, vals, probe, 2, attach=attach, stats=stats)
         assert len(ref[0]) == len(shim[0]) and len(ref[0]) > 3
         for j, (a, b) in enumerate(zip(ref[0], shim[0])):
             assert a.tolist() == b.tolist(), (i, j)
         for (f, v), (g, w) in ((ref[1], shim[1]), (ref[2], shim[2])):
             assert (f == g).all() and (v == w).all(), i
-    # what happened to the registrations (printed for the record; correctness is asserted above)
-    print("direct stats per store (registered, stale seen, buffer address):", stats)
+    # (caches registered, stale placements, adds placing) while each store was open
+    assert all(s[0] == (1 if attach else 0) and s[1] == 0 for s in stats), stats

@@ -1,7 +1,8 @@
 """Diagnostics: the reference's own key-value store (oracle/ref_kvs.c) with its
 routing_filter.c and with the drop-in shim, same workload: insert wall time (the trunk's
 filter builds included), per-lookup latency of splinterdb_lookup and of core_lookup_async at
-64 in flight, filter calls per lookup. One JSON line.
+64 in flight, filter calls per lookup; stores driven as the unmodified reference drives them and with the
+shim's cache attach. One JSON line.
 usage: python tools/trunk_latency.py [n_keys] [memtable_mib]"""
 import json
 import os
@@ -24,15 +25,15 @@ probe_hit = keys[rng.choice(n, P, replace=False)]
 probe_miss = absent[:P]
 out = {"keys": n, "memtable_mib": mt, "probes": P}
 for name, path in (("reference", RK.KVS_REF), ("shim", RK.KVS_SHIM)):
-    # the first store of the process pays the one-time costs (the shim: engine creation and the
-    # cache-buffer registration inside its first routing_filter_add); a second store, opened
-    # after prewarm(), shows the steady state
-    for run in ("cold", "warm"):
-        with RK.Kvs(path, memtable_mib=mt, record_digest=False) as db:
-            if run == "warm":
-                tp = time.perf_counter()
-                db.prewarm()
-                prewarm_s = time.perf_counter() - tp
+    # three stores one after another in this process: "first" and "second" are driven as the
+    # unmodified reference drives the filter (no shim extension called: the bounce-buffer path;
+    # the first store of the process also pays the shim's engine creation inside its first
+    # routing_filter_add), "attached" calls routing_filter_amd_cache_attach after opening (its
+    # page buffer registered: images placed straight into the cache pages) and release before
+    # closing. Lookups are timed on the second store.
+    out[name] = {}
+    for run, attach in (("first", False), ("second", False), ("attached", True)):
+        with RK.Kvs(path, memtable_mib=mt, record_digest=False, attach=attach) as db:
             b0 = db.add_breakdown()
             t = time.perf_counter()
             db.insert(keys, vals)
@@ -41,24 +42,22 @@ for name, path in (("reference", RK.KVS_REF), ("shim", RK.KVS_SHIM)):
             recs, nl0, na0 = db.adds()
             bd = {k: round((b1[k] - b0[k]) / 1e6, 3) for k in b1 if k not in ("calls", "batches")}
             ds = db.direct_stats()
-            if run == "warm":
-                out[name]["direct_stats_warm"] = [int(x) for x in ds[:3]]
-                out[name]["insert_warm_s"] = round(ins, 3)
-                out[name]["prewarm_s"] = round(prewarm_s, 3)
-                out[name]["add_breakdown_warm_ms"] = bd
-                continue
-            r = {"insert_s": round(ins, 3), "filter_adds": int(len(recs)),
-                 "filter_fps_added": int(recs["num_new"].sum()) if len(recs) else 0, "add_breakdown_ms": bd,
+            r = {"insert_s": round(ins, 3), "filter_adds": int(len(recs)), "add_breakdown_ms": bd,
                  "direct_stats": [int(x) for x in ds[:3]]}
-            for kind, pr in (("hit", probe_hit), ("miss", probe_miss)):
-                f, _, ts = db.lookup(pr)
-                _, nl1, _ = db.adds()
-                fa, _, ta = db.lookup_async(pr, 64)
-                _, nl2, na2 = db.adds()
-                r[f"lookup_{kind}_us"] = round(ts / P * 1e6, 3)
-                r[f"lookup_async64_{kind}_us"] = round(ta / P * 1e6, 3)
-                r[f"filter_lookups_per_{kind}"] = round((nl1 - nl0) / P, 2)
-                r[f"found_{kind}"] = int(f.sum())
-                nl0 = nl2
-            out[name] = r
+            if attach:
+                r["attached"] = db.attached
+                r["attach_s"] = round(db.attach_s, 3)
+            if run == "second":
+                r["filter_fps_added"] = int(recs["num_new"].sum()) if len(recs) else 0
+                for kind, pr in (("hit", probe_hit), ("miss", probe_miss)):
+                    f, _, ts = db.lookup(pr)
+                    _, nl1, _ = db.adds()
+                    fa, _, ta = db.lookup_async(pr, 64)
+                    _, nl2, na2 = db.adds()
+                    r[f"lookup_{kind}_us"] = round(ts / P * 1e6, 3)
+                    r[f"lookup_async64_{kind}_us"] = round(ta / P * 1e6, 3)
+                    r[f"filter_lookups_per_{kind}"] = round((nl1 - nl0) / P, 2)
+                    r[f"found_{kind}"] = int(f.sum())
+                    nl0 = nl2
+            out[name][run] = r
 print(json.dumps(out))
