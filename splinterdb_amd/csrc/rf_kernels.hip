@@ -659,7 +659,7 @@ __device__ __forceinline__ void write_index_bounds(const CbCtx& c, const uint32_
 // (s_b[nn, n)), and the dedupe pass reads the two sorted runs through a merge path. Old
 // flagged values are even and new ones odd, so no old value equals a new one and the merge
 // yields exactly the order a sort of all n would (old first on equal e).
-template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
+template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false, bool LIST = false>
 __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __restrict__ plans,
                                                      const uint32_t* __restrict__ cb_filter,
                                                      const uint32_t* __restrict__ cb_count,
@@ -693,12 +693,14 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   uint32_t* s_first = s_bin;  // compacted start of each index: reuses s_bin once bins are sorted
   uint32_t* s_fo = s_bin + 2048;
   uint32_t* s_ho = s_bin + 2048 + MAX_IPC;
-  // cb_list (K4m's fallback, 32-bit incremental builds): the coarse buckets K4m listed with
-  // bit 31 set (more new entries than it takes, or a bin of duplicates), one after another
-  const uint32_t nit = cb_list ? cb_list[0] : 1u;
-  for (uint32_t it = cb_list ? blockIdx.x : 0u; it < nit; it += cb_list ? gridDim.x : 1u) {
+  // LIST (K4m's fallback, 32-bit incremental builds): the coarse buckets K4m listed in cb_list
+  // with bit 31 set (more new entries than it takes, or a bin of duplicates), one after
+  // another; otherwise one coarse bucket per workgroup (the loop runs once: a compile-time
+  // trip count, so the fresh build's kernel is the same code as without it)
+  const uint32_t nit = LIST ? cb_list[0] : 1u;
+  for (uint32_t it = LIST ? blockIdx.x : 0u; it < nit; it += LIST ? gridDim.x : 1u) {
   uint32_t cb;
-  if (cb_list) {
+  if constexpr (LIST) {
     cb = cb_list[1 + it];
     if (!(cb >> 31)) continue;  // K4b's (over SORT_CAP)
     cb &= 0x7fffffffu;
@@ -716,7 +718,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   const uint32_t cb_out = (DUAL && spill) ? cb_outs[cb] : cb_rel;
   CbCtx c{P.rvs, P.vs, lis, P.bbits, P.idx_base + (cbl << (P.bbits - lis)), cb_out, P.e_first};
   if (n > SORT_CAP) {  // handled by k_cb_sort_big
-    if (threadIdx.x == 0 && !cb_list) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
+    if (threadIdx.x == 0 && !LIST) overflow[1 + atomicAdd(&overflow[0], 1u)] = cb;
     continue;
   }
   const uint32_t nbins = 1u << (P.bbits - P.binsh);  // a bin = 2^binsh filter buckets
@@ -1018,7 +1020,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
   block_excl_scan<SORT_NT>(uniq, s_tmp, &tot_uniq);
   if (threadIdx.x == 0) atomicAdd(&outs[f].num_unique, tot_uniq);
   DBG_PHASE(8);
-  __syncthreads();  // list mode: the next bucket reuses the LDS
+  if constexpr (LIST) __syncthreads();  // the next bucket reuses the LDS
   }
 }
 
@@ -1038,6 +1040,7 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
 // list mode (bit 31 on their overflow-list entry); buckets over SORT_CAP to K4b as before.
 constexpr uint32_t MRG_NEW_CAP = 2048;
 constexpr uint32_t MRG_LNB_MAX = 9;  // at most 512 bins
+constexpr uint32_t MRG_RUN = (SORT_CAP + SORT_NT - 1) / SORT_NT + 1;  // output slots per thread (odd)
 __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __restrict__ plans,
                                                       const uint32_t* __restrict__ cb_filter,
                                                       const uint32_t* __restrict__ cb_count,
@@ -1056,10 +1059,11 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __res
                                                       const uint32_t* __restrict__ spill,
                                                       const uint32_t* __restrict__ cb_outs) {
   constexpr int NPER = MRG_NEW_CAP / SORT_NT;
-  __shared__ uint32_t s_old[SORT_CAP];
-  __shared__ uint32_t s_new[MRG_NEW_CAP];
-  __shared__ uint16_t s_kpos[MRG_NEW_CAP];
+  __shared__ uint32_t s_old[SORT_CAP + 1];      // + a sentinel past the last old entry
+  __shared__ uint32_t s_new[MRG_NEW_CAP + 1];   // + a sentinel past the last kept new entry
+  static_assert((1u << MRG_LNB_MAX) >= MAX_IPC, "s_start (MAX_IPC + 1 words) over s_bin");
   __shared__ uint32_t s_bin[(1u << MRG_LNB_MAX) + 1];
+  __shared__ uint32_t s_fo[MAX_IPC];
   __shared__ uint32_t s_tmp[SORT_NT / WAVE + 1];
   __shared__ uint32_t s_big;
   DBG_PHASE_K(5, 15);
@@ -1088,15 +1092,16 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __res
   auto okey = [&](uint32_t raw) -> uint32_t { return od ? ((raw >> ovs) << vs) | (raw & ((1u << ovs) - 1u)) : raw; };
   auto index_of = [&](uint32_t e) -> uint32_t { return ish >= 32 ? 0u : ((e >> ish) & (ipc - 1)); };
   const uint32_t lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-  // 1. the old run into LDS (LDS-DMA, a dword per lane), landing while the new entries sort
-  {
-    const uint32_t* osrc = (od ? P.old_entries : old32 + P.old_first) + ob_lo[cb];
-    for (uint32_t i0 = wv * WAVE; i0 < no; i0 += SORT_NT)
-      if (i0 + lane < no)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(osrc + i0 + lane),
-                                         (__attribute__((address_space(3))) void*)(s_old + i0), 4, 0, 0);
-  }
-  // 2. the new entries ((e << 1) | 1 in the partition region): bins over their top bits,
+  // a barrier ordering this workgroup's LDS accesses only: the old run's LDS-DMA stays in
+  // flight across it (__syncthreads, and even a release fence on LDS, wait for every
+  // outstanding load -- LDS-DMA writes LDS and is counted as a load)
+  auto lds_sync = [] {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // compiler-only ordering: no hardware wait implied
+    __builtin_amdgcn_s_waitcnt(0xc07f);       // lgkmcnt(0): this wave's LDS accesses done
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  };
+  // 1. the new entries ((e << 1) | 1 in the partition region): bins over their top bits,
   //    about four entries per bin
   uint32_t lnb = 0;
   while (lnb < MRG_LNB_MAX && lnb < bbits && (8u << lnb) <= nn) lnb++;
@@ -1104,19 +1109,32 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __res
   auto bin_of = [&](uint32_t e) -> uint32_t { return lnb ? (e >> bsh) & (nb - 1) : 0u; };
   const uint32_t* nsrc = part + P.e_first + cb_rel;
   uint32_t v[NPER], rk[NPER];
+  const uint32_t nm1 = nn ? nn - 1 : 0u;  // clamped, branch-free: the loads go out together
 #pragma unroll
-  for (int k = 0; k < NPER; k++) {
-    const uint32_t j = threadIdx.x + k * SORT_NT;
-    v[k] = j < nn ? nsrc[j] >> 1 : 0u;
+  for (int k = 0; k < NPER; k++) v[k] = nsrc[min(threadIdx.x + k * SORT_NT, nm1)] >> 1;
+  static_assert((1u << MRG_LNB_MAX) <= SORT_NT, "one bin counter per thread (+ the last)");
+  if (threadIdx.x <= nb) s_bin[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    s_bin[nb] = 0;
+    s_big = 0;
   }
-  for (uint32_t i = threadIdx.x; i <= nb; i += SORT_NT) s_bin[i] = 0;
-  if (threadIdx.x == 0) s_big = 0;
-  __syncthreads();
+  lds_sync();
   DBG_PHASE_K(5, 0);
 #pragma unroll
   for (int k = 0; k < NPER; k++)
     if (threadIdx.x + k * SORT_NT < nn) rk[k] = atomicAdd(&s_bin[bin_of(v[k])], 1u);
-  __syncthreads();
+  // 2. the old run into LDS (LDS-DMA, a dword per lane), in flight while the new entries sort:
+  //    issued once the new entries have landed (a wave with plain loads and LDS-DMA both
+  //    outstanding can only wait for all of them; splitting the two over different waves
+  //    measured slower: the new entries then land behind the old run's traffic)
+  {
+    const uint32_t* osrc = (od ? P.old_entries : old32 + P.old_first) + ob_lo[cb];
+    for (uint32_t i0 = wv * WAVE; i0 < no; i0 += SORT_NT)
+      if (i0 + lane < no)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(osrc + i0 + lane),
+                                         (__attribute__((address_space(3))) void*)(s_old + i0), 4, 0, 0);
+  }
+  lds_sync();
   DBG_PHASE_K(5, 1);
   if (wv == 0) {  // exclusive scan of the nb <= 512 counts: 8 per lane
     uint32_t c8[8], sum = 0;
@@ -1135,12 +1153,12 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __res
     }
     if (lane == WAVE - 1) s_bin[nb] = run;
   }
-  __syncthreads();
+  lds_sync();
   DBG_PHASE_K(5, 2);
 #pragma unroll
   for (int k = 0; k < NPER; k++)
     if (threadIdx.x + k * SORT_NT < nn) s_new[s_bin[bin_of(v[k])] + rk[k]] = v[k];
-  __syncthreads();
+  lds_sync();
   DBG_PHASE_K(5, 3);
   {  // order inside the bins: segments of S bins (about 8 entries) sorted by one thread each
     uint32_t S = 8;
@@ -1187,124 +1205,130 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_merge(const FilterPlan* __res
     return;
   }
   // 3. drop new duplicates of the previous new entry (only among the new ones: a new entry
-  //    equal to an old one is kept, after it -- src/routing_filter.c:559-597); the kept ones'
-  //    final positions. Thread t takes new entries [t NPER, t NPER + NPER).
-  uint32_t kv[NPER], kp[NPER], kc = 0;
+  //    equal to an old one is kept, after it -- src/routing_filter.c:559-597) and compact the
+  //    kept ones to s_new[0, kn). Thread t takes new entries [t NPER, t NPER + NPER).
+  uint32_t kv[NPER], kc = 0;
   bool keep[NPER];
 #pragma unroll
   for (int k = 0; k < NPER; k++) {
     const uint32_t j = threadIdx.x * NPER + k;
-    keep[k] = false;
-    kv[k] = 0;
-    kp[k] = 0;
-    if (j < nn) {
-      const uint32_t e = s_new[j];
-      kv[k] = e;
-      if (j == 0 || s_new[j - 1] != e) {
-        uint32_t lo = 0, hi = no;  // old entries <= e (an equal old entry stays before it)
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (okey(s_old[mid]) <= e) lo = mid + 1; else hi = mid;
-        }
-        keep[k] = true;
-        kp[k] = lo;
-      }
-    }
+    kv[k] = j < nn ? s_new[j] : 0u;
+    keep[k] = j < nn && (j == 0 || s_new[j - 1] != kv[k]);
     kc += keep[k] ? 1u : 0u;
   }
   uint32_t kn;
   uint32_t r = block_excl_scan<SORT_NT>(kc, s_tmp, &kn);  // its barriers: every s_new read done
 #pragma unroll
   for (int k = 0; k < NPER; k++)
-    if (keep[k]) {
-      s_new[r] = kv[k];
-      s_kpos[r] = (uint16_t)(r + kp[k]);  // < n <= SORT_CAP
-      r++;
-    }
+    if (keep[k]) s_new[r++] = kv[k];
+  // the old run as this filter sees it, once (value bits re-widened when the old filter's
+  // value_size differs), and the sentinels the merge reads past each side's end (entries are
+  // < 2^31: the sentinel sorts after every entry)
+  if (od && ovs != vs)
+    for (uint32_t i = threadIdx.x; i < no; i += SORT_NT) s_old[i] = okey(s_old[i]);
+  if (threadIdx.x == 0) {
+    s_old[no] = 0xffffffffu;
+    s_new[kn] = 0xffffffffu;
+  }
+  for (uint32_t l = threadIdx.x; l < ipc; l += SORT_NT) {
+    s_fo[l] = 0xffffffffu;
+    s_bin[l] = 0xffffffffu;  // s_start below: the start of each non-empty index
+  }
   __syncthreads();
   DBG_PHASE_K(5, 5);
-  // 4. the merged entries, 64 output slots per wave step, each wave a contiguous range
+  // 4. the merge (old first on equal entries), each thread a contiguous range of output slots
+  //    (merge-path split by binary search) merged into registers, branch-free: one LDS read per
+  //    step from the side just consumed. num_unique, the start of each non-empty index (s_start,
+  //    over s_bin) and each index's smallest old entry (s_fo, for builds that split old indices:
+  //    npo > 1) from each entry and its predecessor. After a barrier the merged run is staged in
+  //    place over s_old (slot sl holds merged entry sl; every input was read before the
+  //    barrier) and copied out with coalesced stores.
   const uint32_t tot = no + kn;
   uint32_t* dst = sorted32 + P.e_first + cb_out;
-  const uint32_t nch = (tot + WAVE - 1) / WAVE, cpw = (nch + SORT_NT / WAVE - 1) / (SORT_NT / WAVE);
-  const uint32_t c0 = wv * cpw, c1 = min(nch, c0 + cpw);
+  uint32_t* s_start = s_bin;  // MAX_IPC + 1 words
+  const bool track_old = P.npo > 1;
+  const uint32_t NONE = 0xffffffffu;
+  const uint32_t run = min((uint32_t)MRG_RUN, ((tot + SORT_NT - 1) / SORT_NT) | 1u);
+  const uint32_t d = threadIdx.x * run;
   uint32_t uniq = 0;
-  if (c0 < c1) {
-    // kept new entries before the range (positions are increasing)
-    uint32_t j = 0;
-    {
-      uint32_t lo = 0, hi = kn;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_kpos[mid] < c0 * WAVE) lo = mid + 1; else hi = mid;
-      }
-      j = lo;
+  uint32_t mv[MRG_RUN];
+  if (d < tot) {
+    uint32_t lo = d > kn ? d - kn : 0u, hi = min(d, no);
+    while (lo < hi) {  // ia = old entries among the first d merged ones
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_old[mid] <= s_new[d - mid - 1]) lo = mid + 1; else hi = mid;
     }
-    // the entry just before the range
-    uint32_t carry = 0;
-    bool carry_ok = false;
-    if (c0 > 0) {
-      const uint32_t sl = c0 * WAVE - 1;
-      carry = (j > 0 && s_kpos[j - 1] == sl) ? s_new[j - 1] : okey(s_old[sl - j]);
-      carry_ok = true;
+    uint32_t ia = lo, ib = d - lo;
+    // the merged predecessor of slot d (new after old on equal entries), its index and
+    // fingerprint; the last old entry before slot d (its index): NONE = none
+    uint32_t prev = NONE, pold = NONE;
+    if (d > 0) {
+      const uint32_t po = ia > 0 ? s_old[ia - 1] : 0u;
+      const uint32_t pn = ib > 0 ? s_new[ib - 1] : 0u;
+      prev = (ib > 0 && (ia == 0 || pn >= po)) ? pn : po;
+      if (ia > 0) pold = index_of(po);
     }
-    for (uint32_t c = c0; c < c1; c++) {
-      const uint32_t base = c * WAVE;
-      const uint32_t p = j + lane < kn ? (uint32_t)s_kpos[j + lane] - base : WAVE;
-      const uint32_t m = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(p < WAVE));
-      uint64_t mask = 0;
-      for (uint32_t t = 0; t < m; t++) mask |= 1ull << __builtin_amdgcn_readlane((int)p, t);
-      const uint32_t sl = base + lane;
-      const bool valid = sl < tot;
-      const bool isn = (mask >> lane) & 1ull;
-      const uint32_t kb = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-      uint32_t e = 0;
-      if (valid) e = isn ? s_new[j + kb] : okey(s_old[sl - j - kb]);
-      uint32_t prev = __shfl_up(e, 1, WAVE);
-      bool has_prev = lane > 0;
-      if (lane == 0) {
-        prev = carry;
-        has_prev = carry_ok;
+    uint32_t pli = prev == NONE ? NONE : index_of(prev);
+    uint32_t pfp = prev == NONE ? 0u : prev >> vs;
+    uint32_t onext = s_old[ia], nnext = s_new[ib];  // sentinels past the ends
+    const uint32_t end = min(tot, d + run);
+#pragma unroll
+    for (uint32_t k = 0; k < MRG_RUN; k++) {
+      const uint32_t sl = d + k;
+      if (sl < end) {
+        const bool take_old = onext <= nnext;  // old first on equal entries; a side's sentinel never wins
+        const uint32_t e = take_old ? onext : nnext;
+        ia += take_old ? 1u : 0u;
+        ib += take_old ? 0u : 1u;
+        const uint32_t x = take_old ? s_old[ia] : s_new[ib];
+        onext = take_old ? x : onext;
+        nnext = take_old ? nnext : x;
+        mv[k] = e;
+        const uint32_t li = index_of(e), fp = e >> vs;
+        const bool first = li != pli;  // pli NONE: no predecessor
+        uniq += fp != (first ? (0xffffffffu >> vs) : pfp) ? 1u : 0u;
+        if (first) s_start[li] = sl;
+        if (track_old && take_old) {
+          if (li != pold) s_fo[li] = e;
+          pold = li;
+        }
+        pli = li;
+        pfp = fp;
       }
-      // num_unique (:558, :572-574): an entry whose fingerprint differs from its predecessor's;
-      // an index's first entry compares against UINT32_MAX >> value_size
-      const uint32_t li = index_of(e), fp = e >> vs;
-      const bool first = !has_prev || index_of(prev) != li;
-      if (valid && fp != (first ? (0xffffffffu >> vs) : (prev >> vs))) uniq++;
-      if (valid) dst[sl] = e;
-      carry = (uint32_t)__builtin_amdgcn_readlane((int)e, WAVE - 1);
-      carry_ok = true;
-      j += m;
     }
   }
+  __syncthreads();  // every input read
+  if (d < tot) {
+#pragma unroll
+    for (uint32_t k = 0; k < MRG_RUN; k++)
+      if (k < run && d + k < tot) s_old[d + k] = mv[k];
+  }
+  // 5. per index: start (an empty index starts where the next non-empty one does: a suffix
+  //    minimum over the indices, tot past the last) and count; its smallest old entry (npo > 1)
+  static_assert(MAX_IPC <= SORT_NT, "one index per thread");
+  uint32_t st = threadIdx.x < ipc ? s_start[threadIdx.x] : NONE;
+#pragma unroll
+  for (uint32_t off = 1; off < WAVE; off <<= 1) {
+    const uint32_t y = __shfl_down(st, off, WAVE);
+    if (lane + off < WAVE) st = min(st, y);
+  }
+  if (lane == 0) s_tmp[wv] = st;
+  __syncthreads();  // also: the merged run staged in s_old
+  for (uint32_t w2 = wv + 1; w2 < SORT_NT / WAVE; w2++) st = min(st, s_tmp[w2]);
+  st = min(st, tot);
+  for (uint32_t i = threadIdx.x; i < tot; i += SORT_NT) dst[i] = s_old[i];
+  __syncthreads();  // every s_tmp and s_start read
+  if (threadIdx.x < ipc) s_start[threadIdx.x] = st;
+  if (threadIdx.x == 0) s_start[ipc] = tot;
+  __syncthreads();
   DBG_PHASE_K(5, 6);
-  // 5. per index: its entries' start and count; the smallest old entry (num_unique quirk, only
-  //    for builds that split old indices: npo > 1)
-  const bool track_old = P.npo > 1;
-  for (uint32_t li = threadIdx.x; li < ipc; li += SORT_NT) {
-    auto lb_old = [&](uint32_t key) {
-      uint32_t lo = 0, hi = no;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (index_of(okey(s_old[mid])) < key) lo = mid + 1; else hi = mid;
-      }
-      return lo;
-    };
-    auto lb_new = [&](uint32_t key) {
-      uint32_t lo = 0, hi = kn;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (index_of(s_new[mid]) < key) lo = mid + 1; else hi = mid;
-      }
-      return lo;
-    };
-    const uint32_t ol = lb_old(li), oh = li + 1 < ipc ? lb_old(li + 1) : no;
-    const uint32_t nl = lb_new(li), nh = li + 1 < ipc ? lb_new(li + 1) : kn;
-    idx_cnt[idx0 + li] = (oh - ol) + (nh - nl);
-    idx_start[idx0 + li] = cb_out + ol + nl;
+  if (threadIdx.x < ipc) {
+    const uint32_t l = threadIdx.x;
+    idx_cnt[idx0 + l] = s_start[l + 1] - st;
+    idx_start[idx0 + l] = cb_out + st;
     if (track_old) {
-      first_old[idx0 + li] = oh > ol ? okey(s_old[ol]) : 0xffffffffu;
-      has_old[idx0 + li] = oh > ol ? 1u : 0u;
+      first_old[idx0 + l] = s_fo[l];
+      has_old[idx0 + l] = s_fo[l] != NONE ? 1u : 0u;
     }
   }
   DBG_PHASE_K(5, 7);
@@ -3143,12 +3167,12 @@ __device__ __forceinline__ bool line_decode_u(const uint32_t* Lw, uint32_t j, ui
   if (c == 0) return true;
   const uint32_t b = (p1 - j) * rvs, nb = c * rvs, wi = b >> 5, off = b & 31;
   if (off + nb > 96 || b + nb > 384 || nb > 64) return false;
-  const uint32_t w0 = Lw[4 + wi], w1 = Lw[5 + wi], w2 = Lw[6 + wi];
-  // the c fields as one 64-bit word (funnel shifts), compared at once (SWAR, as line_decode_w)
-  const uint64_t W = (uint64_t)__builtin_amdgcn_alignbit(w2, w1, off) << 32 | __builtin_amdgcn_alignbit(w1, w0, off);
   const uint64_t M = (L << rvs) - (L << vs);  // remainder part of every field (uniform)
   const uint64_t H = L << (rvs - 1);          // top bit of every remainder part (uniform)
   const uint64_t MH = M & ~H;
+  const uint32_t w0 = Lw[4 + wi], w1 = Lw[5 + wi], w2 = Lw[6 + wi];
+  // the c fields as one 64-bit word (funnel shifts), compared at once (SWAR, as line_decode_w)
+  const uint64_t W = (uint64_t)__builtin_amdgcn_alignbit(w2, w1, off) << 32 | __builtin_amdgcn_alignbit(w1, w0, off);
   const uint64_t Y = W ^ ((uint64_t)(remainder << vs) * L);
   const uint64_t valid = nb == 64 ? ~0ull : (1ull << nb) - 1;
   uint64_t Z = H & valid & ~(((Y & MH) + MH) | Y);  // top bits of the matching fields
@@ -3794,29 +3818,35 @@ static int launch_scatter_t(const LaunchArgs& a, EntT* ent, EntT* part, const ui
   return 0;
 }
 
-// K4m for 32-bit incremental builds (RF_AMD_K4M=1; default: the K4 DUAL sort --
-// profiles/r05_k4m_v1_ab.json: K4m v1 2.55 vs 1.85 ms at round 8)
+// K4m for 32-bit incremental builds (RF_AMD_K4M=0: the K4 DUAL sort instead, for A/B;
+// round-8 K4 2.22 -> 1.48 ms on one box)
 static bool k4m_enabled() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("RF_AMD_K4M");
-    v = (e && e[0] == '1') ? 1 : 0;
+    v = (e && e[0] == '0') ? 0 : 1;
   }
   return v != 0;
 }
 
 template <typename EntT, bool FL = (sizeof(EntT) == 8), bool DUAL = false>
 static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint32_t* spill) {
-  if (DUAL && k4m_enabled()) {
-    hipLaunchKernelGGL(k_cb_merge, dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
+  bool merged = false;
+  if constexpr (DUAL) {
+    if (k4m_enabled()) {
+      merged = true;
+      hipLaunchKernelGGL(k_cb_merge, dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans, a.cb_filter,
                        a.cb_count, a.cb_start, (const uint32_t*)part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt,
                        a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
-    CHECK_LAUNCH();
-    // the buckets K4m handed back (bit 31 on their overflow-list entry)
-    hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(BIG_GRID), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
-                       a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt,
-                       a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs, a.overflow);
-  } else {
+      CHECK_LAUNCH();
+      // the buckets K4m handed back (bit 31 on their overflow-list entry)
+      hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL, true>), dim3(BIG_GRID), dim3(SORT_NT), 0, (hipStream_t)a.stream,
+                         a.plans, a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32,
+                         a.idx_cnt, a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs,
+                         a.overflow);
+    }
+  }
+  if (!merged) {
     hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream, a.plans,
                        a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt,
                        a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs, nullptr);

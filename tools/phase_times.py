@@ -55,8 +55,8 @@ if KID == 1:
              7: "index bounds", 8: "uniq+end"}
     order = [15, 0, 1, 2, 3, 4, 9, 10, 5, 6, 7, 8]
 elif KID == 5:
-    names = {15: "entry", 0: "DMA issue+new load", 1: "rank", 2: "bin scan", 3: "scatter", 4: "bin sort+old landed",
-             5: "search+compact", 6: "merged output", 7: "index bounds", 8: "uniq+end"}
+    names = {15: "entry", 0: "new load", 1: "rank+DMA issue", 2: "bin scan", 3: "scatter", 4: "bin sort+old landed",
+             5: "dedupe+compact", 6: "merge (split + run)", 7: "index bounds", 8: "uniq+end"}
     order = [15, 0, 1, 2, 3, 4, 5, 6, 7, 8]
 elif KID == 4:
     names = {15: "entry", 5: "size loads (t0)", 6: "scan", 0: "excl store", 1: "next()", 2: "doubling",
