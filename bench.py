@@ -84,7 +84,7 @@ def parse():
     p.add_argument("--routed-probe", action="store_true",
                    help="also time routed probes: each rank probes keys of every rank's filters, "
                         "moved to the owner by all-to-all (route.py); reported beside value")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r04.json"))
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r05.json"))
     p.add_argument("--digest-out", default="",
                    help="write each rank's per-filter image SHA-256s to <path>.rank<r> (tests)")
     return p.parse_args()

@@ -3839,8 +3839,9 @@ static int launch_sort_t(const LaunchArgs& a, EntT* ent, EntT* part, const uint3
                        a.cb_count, a.cb_start, (const uint32_t*)part, a.old32, a.ob_lo, a.ob_n, a.sorted32, a.idx_cnt,
                        a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs);
       CHECK_LAUNCH();
-      // the buckets K4m handed back (bit 31 on their overflow-list entry)
-      hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL, true>), dim3(BIG_GRID), dim3(SORT_NT), 0, (hipStream_t)a.stream,
+      // the buckets K4m handed back (bit 31 on their overflow-list entry): up to one workgroup
+      // per coarse bucket (early chain rounds hand back nearly all of them); the surplus exits
+      hipLaunchKernelGGL((k_cb_sort<EntT, FL, DUAL, true>), dim3(a.num_cb), dim3(SORT_NT), 0, (hipStream_t)a.stream,
                          a.plans, a.cb_filter, a.cb_count, a.cb_start, part, a.old32, a.ob_lo, a.ob_n, a.sorted32,
                          a.idx_cnt, a.idx_start, a.outs, a.overflow, a.lis, a.first_old, a.has_old, spill, a.cb_outs,
                          a.overflow);

@@ -94,10 +94,17 @@ res = {name: {s: [] for s in STAGES} for name, *_ in libs}
 digests = {}
 for rep in range(REPS):
     for name, L, e, envs in libs:
-        for kv in (envs.split(",") if envs else []):
+        saved = {}
+        for kv in (envs.split(",") if envs else []):  # this entry's switches, restored after it
             k_, _, v_ = kv.partition("=")
+            saved[k_] = os.environ.get(k_)
             os.environ[k_] = v_
         b, t = chain(L, e)
+        for k_, v_ in saved.items():
+            if v_ is None:
+                os.environ.pop(k_, None)
+            else:
+                os.environ[k_] = v_
         for s in STAGES:
             res[name][s].append(t[s])
         if rep == 0:

@@ -53,12 +53,19 @@ for shape, (F, n) in shapes.items():
     arr = (ctypes.c_float * 9)()
     for rnd in range(7):
         for name, L, b, found, nn_, vals_, sw in libs:
-            for kv in (sw.split(",") if sw else []):
+            saved = {}
+            for kv in (sw.split(",") if sw else []):  # this entry's switches, restored after it
                 k_, _, v_ = kv.partition("=")
+                saved[k_] = os.environ.get(k_)
                 os.environ[k_] = v_
             assert L.rf_amd_batch_build_keys(b, keys.data_ptr(), 24, None) == 0
             assert L.rf_amd_batch_probe_keys_runs(b, keys.data_ptr(), 24, counts, found.data_ptr(), None) == 0
             torch.cuda.synchronize()
+            for k_, v_ in saved.items():
+                if v_ is None:
+                    os.environ.pop(k_, None)
+                else:
+                    os.environ[k_] = v_
             L.rf_amd_batch_timings(b, arr, 9)
             r = res[name]
             r["probe"].append(arr[8]); r["build"].append(arr[7]); r["assemble"].append(arr[6])
