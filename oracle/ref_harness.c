@@ -1206,15 +1206,17 @@ actx_callback(void *arg)
 {
    rfr_actx   *c = arg;
    rfr_adrive *d = c->d;
-   atomic_fetch_add(&d->callbacks, 1);
    if (atomic_fetch_add(&c->cbs, 1) != 0 || atomic_load(&c->phase) != 1) {
       atomic_fetch_add(&d->violations, 1);
-      return;
+   } else {
+      pthread_mutex_lock(&d->mu);
+      c->next  = d->ready;
+      d->ready = c;
+      pthread_mutex_unlock(&d->mu);
    }
-   pthread_mutex_lock(&d->mu);
-   c->next  = d->ready;
-   d->ready = c;
-   pthread_mutex_unlock(&d->mu);
+   /* last: the driver frees the contexts and destroys d (its stack frame) once every owed
+      callback has counted itself, so nothing may touch them after this */
+   atomic_fetch_add(&d->callbacks, 1);
 }
 
 int
