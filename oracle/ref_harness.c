@@ -32,8 +32,13 @@
 #include "rc_allocator.h"
 #include "splinterdb/default_data_config.h"
 
+#include <execinfo.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <unistd.h>
 #include <pthread.h>
 #include <sched.h>
+#include <signal.h>
 #include <stdatomic.h>
 #include <sys/mman.h>
 #include <sys/uio.h>
@@ -302,9 +307,31 @@ routing_filter_amd_cache_attach(cache *cc);
 __attribute__((weak)) void
 routing_filter_amd_cache_release(cache *cc);
 
+/* diagnostics (RFR_ABORT_BT=1): a native backtrace on SIGABRT / SIGSEGV, to stderr */
+static void
+rfr_crash_bt(int sig)
+{
+   void *f[64];
+   int   n = backtrace(f, 64);
+   char  msg[48];
+   int   m = snprintf(msg, sizeof(msg), "rfr: signal %d, backtrace:\n", sig);
+   if (m > 0) {
+      (void)!write(2, msg, (size_t)m);
+   }
+   backtrace_symbols_fd(f, n, 2);
+   signal(sig, SIG_DFL);
+   raise(sig);
+}
+
 rfr_stack *
 rfr_create(uint32 fingerprint_size, uint32 log_index_size, uint64 cache_mib, uint64 disk_mib)
 {
+   static int bt_armed;
+   if (!bt_armed && getenv("RFR_ABORT_BT")) {
+      bt_armed = 1;
+      signal(SIGABRT, rfr_crash_bt);
+      signal(SIGSEGV, rfr_crash_bt);
+   }
    if (!atomic_exchange(&g_registered_main, 1)) {
       platform_register_thread();
    }

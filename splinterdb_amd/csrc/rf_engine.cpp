@@ -1439,20 +1439,16 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
   if (!lk.owns_lock()) return 0;  // another thread is reaping
   uint64_t n = 0, t = v.reap_next;
   const uint64_t tail = v.tail.load(std::memory_order_acquire);
-  // the tickets answered so far: one word the server stores after each pass (polling each
-  // slot's ticket instead made every poll of a line the GPU was still writing a miss); the
-  // found words of the tickets below it have landed
-  const uint64_t served = __atomic_load_n(&v.ctl->served_head, __ATOMIC_ACQUIRE);
   // the result lines (written by the GPU over PCIe: a miss each) and the request metadata
   // (written by the submitting threads) of the next tickets are fetched ahead, so the misses
   // of consecutive tickets overlap instead of costing one round trip per state
-  for (uint64_t q = t; q < served && q < t + 16; q += 4) {
+  for (uint64_t q = t; q < tail && q < t + 16; q += 4) {
     __builtin_prefetch(&v.res[q & (SRV_RING - 1)], 0, 0);
     __builtin_prefetch(&v.meta[q & (SRV_RING - 1)], 0, 0);
   }
-  while (n < max && t < tail && t < served) {
+  while (n < max && t < tail) {
     const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
-    if ((t & 3) == 0 && t + 16 < served) {
+    if ((t & 3) == 0 && t + 16 < tail) {
       __builtin_prefetch(&v.res[(t + 16) & (SRV_RING - 1)], 0, 0);
       __builtin_prefetch(&v.meta[(t + 16) & (SRV_RING - 1)], 0, 0);
     }
@@ -1469,6 +1465,7 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
       t++;
       continue;
     }
+    if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) != t) break;  // not answered yet
     tags[n] = tag;
     found_values[n] = __atomic_load_n(&v.res[slot].found, __ATOMIC_RELAXED);
     v.consumed[slot].store(t + 1, std::memory_order_release);

@@ -3678,8 +3678,6 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
         const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
         if (i < k) __hip_atomic_store(&res[slot].ticket, head + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      // one word the reaper polls for the whole pass (the found words above have completed)
-      if (lane == 0) __hip_atomic_store(&ctl->served_head, head + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       head += k;
       served += k;
       t_busy = __builtin_amdgcn_s_memrealtime();

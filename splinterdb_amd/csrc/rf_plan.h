@@ -121,11 +121,6 @@ struct SrvCtl {
   uint64_t exit_head;
   uint64_t exit_gen;
   uint64_t served;
-  uint64_t pad0[4];
-  // the first ticket not yet answered, stored by the server after each pass once that pass's
-  // found words were written (its own cache line: the reaper polls it instead of each slot)
-  uint64_t served_head;
-  uint64_t pad1[7];
 };
 
 // a lookup call small enough to travel in the kernel arguments (k_probe_small)
