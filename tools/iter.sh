@@ -1,14 +1,13 @@
 #!/bin/bash
-# r05 call 27: reaper A/B (per-slot tickets vs served head) on one box; then the exit abort's backtrace
+# r05 call 28: final validation: full GPU suite, smoke, the driver's default bench command
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r05d27
+O=gpurun_out/r05d28
 mkdir -p $O
-ulimit -c 0
-for v in 1 0 1 0; do
-  RF_AMD_REAP_TICKETS=$v timeout -k 10 600 python3 tools/shim_latency.py --fast-exit > $O/sl_$v.json 2> $O/sl_$v.err || { echo "shim_latency $v failed"; tail -5 $O/sl_$v.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/sl_$v.json'))['shim']; print('tickets=$v', d['async_driven_8192_ms'], d['async_driven_breakdown'], d['lookup_async_8192_ms'], d['lookup_one_ms'])"
-done
-RFR_ABORT_BT=1 timeout -k 10 600 python3 tools/shim_latency.py > $O/sl_bt.json 2> $O/sl_bt.err; echo "bt run rc $?"
-grep -v "UserWarning\|setattr\|return self._float" $O/sl_bt.err | tail -40
+timeout -k 10 1000 python -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/ > $O/t.log 2>&1 || { echo "tests failed"; grep -v "^  File" $O/t.log | tail -40; exit 1; }
+tail -2 $O/t.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail $O/bench.err; exit 1; }
+python3 -c "import json; d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['build_mkeys_s'], d['probe_mkeys_s'], d['roofline'], d['probe_floor']['probe_over_floor'], d['verified'], d['cpu_baseline']['value'])"
