@@ -3219,16 +3219,12 @@ __device__ __forceinline__ bool probe_fast(const uint4* __restrict__ pplans, con
                                            uint32_t page_size, uint32_t nf, uint64_t wf, v4u* sw) {
   if (wf + WAVE > n) return false;
   if (KIND == IN_KEYS24 && ((uintptr_t)in0 & 15)) return false;
-  const uint32_t t = sload32(wave_tab + wf / WAVE);
-  if ((t & 127u) != WAVE) return false;  // the wave spans a run boundary
-  const uint32_t fs = t >> 7;
-  if (fs >= nf) return false;
-  const uint4 U = make_uint4(sload32(&pplans[fs].x), sload32(&pplans[fs].y), sload32(&pplans[fs].z),
-                             sload32(&pplans[fs].w));
-  const uint32_t vs = U.x & 0xff, rem = (U.x >> 8) & 0xff, rvs = (U.x >> 16) & 0xff, lgl = U.x >> 24;
-  if (U.w || !lgl || rem == 0 || rem >= 32 || rvs > 32) return false;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
-  uint32_t h;
+  // the wave's keys (or hashes) are requested before its filter is known: their load runs
+  // under the two dependent scalar loads of the wave table and the plan instead of after them.
+  // A wave that turns out not to be fast-path material leaves the keys where the general path
+  // stages them itself (the same LDS slots, the same bytes).
+  uint32_t h = 0;
   if constexpr (KIND == IN_KEYS24) {
     // the wave's 64 keys (1,536 contiguous bytes): 16-byte LDS-DMA loads, 12 cache lines
     const uint8_t* kb = static_cast<const uint8_t*>(in0) + wf * 24;
@@ -3238,14 +3234,24 @@ __device__ __forceinline__ bool probe_fast(const uint4* __restrict__ pplans, con
     if (lane < 32)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb2 + lane * 16),
                                        (__attribute__((address_space(3))) void*)(sw + WAVE), 16, 0, 2);
+  } else {
+    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + wf + lane);
+  }
+  const uint32_t t = sload32(wave_tab + wf / WAVE);
+  if ((t & 127u) != WAVE) return false;  // the wave spans a run boundary
+  const uint32_t fs = t >> 7;
+  if (fs >= nf) return false;
+  const uint4 U = make_uint4(sload32(&pplans[fs].x), sload32(&pplans[fs].y), sload32(&pplans[fs].z),
+                             sload32(&pplans[fs].w));
+  const uint32_t vs = U.x & 0xff, rem = (U.x >> 8) & 0xff, rvs = (U.x >> 16) & 0xff, lgl = U.x >> 24;
+  if (U.w || !lgl || rem == 0 || rem >= 32 || rvs > 32) return false;
+  if constexpr (KIND == IN_KEYS24) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync_lds();
     const uint2* k2 = reinterpret_cast<const uint2*>(sw) + 3 * lane;
     const uint2 a = k2[0], b = k2[1], c = k2[2];
     const uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
     h = xxh32_24(w, seed);
-  } else {
-    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + wf + lane);
   }
   const uint32_t lgG = lgl - 1;
   const uint32_t fp = h >> (32 - fp_size);
@@ -3487,28 +3493,36 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe_floor(const uint4* __r
   const uint64_t wf = (uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * NT + wv * WAVE;
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   if (wf >= n) return;
+  v4u* sw = s_wbuf[wv];
+  uint32_t h = 0;
+  const bool full = wf + WAVE <= n;
+  if constexpr (KIND == IN_KEYS24) {  // requested before the filter is known, as the fast path
+    const uint8_t* kb = static_cast<const uint8_t*>(in0) + wf * 24;
+    if (full) {
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + lane * 16),
+                                       (__attribute__((address_space(3))) void*)sw, 16, 0, 2);
+      if (lane < 32)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(sw + WAVE), 16, 0, 2);
+    }
+  } else {
+    if (full) h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + wf + lane);
+  }
   const uint32_t t = sload32(wave_tab + wf / WAVE);
   const uint32_t fs = t >> 7;
   uint32_t lgl = 0, rem = 0, base = 0;
-  if ((t & 127u) == WAVE && fs < nf && wf + WAVE <= n) {
+  if ((t & 127u) == WAVE && fs < nf && full) {
     const uint32_t x = sload32(&pplans[fs].x);
     lgl = x >> 24;
     rem = (x >> 8) & 0xff;
     base = sload32(&pplans[fs].y);
   }
   if (!lgl || rem == 0 || rem >= 32) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA left in flight at exit
     if (wf + lane < n) found[wf + lane] = 0;
     return;
   }
-  v4u* sw = s_wbuf[wv];
-  uint32_t h;
   if constexpr (KIND == IN_KEYS24) {
-    const uint8_t* kb = static_cast<const uint8_t*>(in0) + wf * 24;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + lane * 16),
-                                     (__attribute__((address_space(3))) void*)sw, 16, 0, 2);
-    if (lane < 32)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + 1024 + lane * 16),
-                                       (__attribute__((address_space(3))) void*)(sw + WAVE), 16, 0, 2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync_lds();
     const uint2* k2 = reinterpret_cast<const uint2*>(sw) + 3 * lane;
@@ -3516,8 +3530,6 @@ __global__ __launch_bounds__(probe_nt(KIND)) void k_probe_floor(const uint4* __r
     h = (a.x ^ a.y ^ b.x ^ b.y ^ c.x ^ c.y) * 0x9e3779b1u;
     h ^= h >> 15;
     h *= 0x85ebca77u;
-  } else {
-    h = __builtin_nontemporal_load(static_cast<const uint32_t*>(in0) + wf + lane);
   }
   const uint32_t bucket = (h >> (32 - fp_size)) >> rem;
   const uint8_t* fb = reinterpret_cast<const uint8_t*>(lines) + ((uint64_t)base << 6);
