@@ -1851,13 +1851,13 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   __shared__ uint32_t s_c[ASM_MAXB];
   __shared__ uint32_t s_est[ASM_MAXB + 1];
   __shared__ uint32_t s_src[ASM_MAXB];
-  // s_rblk (block of each run's first entry, phases A-C) and s_gs (per block: bit after each
-  // line group's last terminator, phase E) share one array: 2 KiB less LDS per page lets
-  // 14 pages, not 13, run on a CU
-  __shared__ uint16_t s_rg[ASM_MAXE / ASM_RUN > ASM_GT ? ASM_MAXE / ASM_RUN : ASM_GT];
-  uint16_t* const s_rblk = s_rg;
-  uint16_t* const s_gs = s_rg;
-  __shared__ uint32_t s_wm[MAX_PAGE / 16];  // byte w: a block j >= 1 starts in word w
+  // block of each run (phases A-C; < ASM_MAXB blocks: one byte each)
+  __shared__ uint8_t s_rblk[ASM_MAXE / ASM_RUN + ASM_MAXB];
+  // s_wm (phases A-B; byte w: a block j >= 1 starts in word w) and s_gs (phases C-E; per
+  // block: bit after each line group's last terminator) share one array: 16 pages per CU
+  __shared__ __attribute__((aligned(16))) uint32_t s_wmgs[MAX_PAGE / 16 > ASM_GT / 2 ? MAX_PAGE / 16 : ASM_GT / 2];
+  uint32_t* const s_wm = s_wmgs;
+  uint16_t* const s_gs = reinterpret_cast<uint16_t*>(s_wmgs);
   __shared__ uint32_t s_tmp[ASM_NT / WAVE + 1];
   DBG_PHASE_K(3, 15);
   const uint32_t slot = xcd_chunk(blockIdx.x, gridDim.x);  // a filter's pages share an XCD
@@ -1877,6 +1877,10 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
     return;
   }
   const uint32_t IS = 1u << lis, rvs = P.rvs;
+  // probe lines cut from this page (phase E): line groups of G buckets, L per block; a page
+  // whose group table would not fit s_gs has its lines cut by k_plines_list
+  const uint32_t lgG = P.lines_asm ? P.lg_line - 1 : 0u, G = 1u << lgG, L = IS >> lgG;
+  const bool cut = P.lines_asm && !(P.lines_flag && nb * (L + 1) > ASM_GT);
   // (A) metadata + entry offsets (2 blocks per thread)
   uint32_t cj[2], oj[2], sj[2], sum = 0;
   uint64_t sl[2];
@@ -1904,28 +1908,32 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
     sum += cj[q];
   }
-  uint32_t ne;
-  uint32_t run = block_excl_scan<ASM_NT>(sum, s_tmp, &ne);
+  // runs of ASM_RUN entries start at each block's first entry (a block's last run may be
+  // short), so no run spans two blocks. One scan gives both prefixes: entries in the low 20
+  // bits (< 128 blocks * 4096), runs above them (exact whenever ne <= ASM_MAXE)
+  uint32_t tot;
+  uint32_t run = block_excl_scan<ASM_NT>(sum + (((cj[0] + ASM_RUN - 1) / ASM_RUN + (cj[1] + ASM_RUN - 1) / ASM_RUN) << 20),
+                                         s_tmp, &tot);
+  const uint32_t ne = tot & 0xfffffu, nruns = tot >> 20;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const uint32_t j = threadIdx.x * 2 + q;
-    if (j < nb) s_est[j] = run;
-    run += cj[q];
+    if (j < nb) s_est[j] = run >> 20;  // block j's first run
+    run += cj[q] + (((cj[q] + ASM_RUN - 1) / ASM_RUN) << 20);
   }
-  if (threadIdx.x == 0) { s_est[nb] = ne; s_off[nb] = page_size; }
+  if (threadIdx.x == 0) { s_est[nb] = nruns; s_off[nb] = page_size; }
   DBG_PHASE_K(3, 0);
   if (ne > ASM_MAXE) {  // uniform (scan total)
     __syncthreads();
     assemble_atomic(P, p, slot, b0, b1, idx_cnt, idx_start, sorted32, slots, pages, lis, page_size, s_pg);
   } else {
   __syncthreads();
-  // run table: block of each run's first entry; word marks of the block starts
+  // run table: block of each run; word marks of the block starts
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const uint32_t j = threadIdx.x * 2 + q;
-    if (j < nb && s_c[j]) {
-      const uint32_t r0 = (s_est[j] + ASM_RUN - 1) / ASM_RUN, r1 = (s_est[j + 1] + ASM_RUN - 1) / ASM_RUN;
-      for (uint32_t r = r0; r < r1; r++) s_rblk[r] = (uint16_t)j;
+    if (j < nb) {
+      for (uint32_t r = s_est[j]; r < s_est[j + 1]; r++) s_rblk[r] = (uint8_t)j;
     }
     if (j < nb && j > 0) reinterpret_cast<uint8_t*>(s_wm)[(oj[q] + 3) / 4] = 1;  // blocks >= 9 B apart
   }
@@ -1945,41 +1953,31 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   uint32_t mtot;
   const uint32_t jw0 = block_excl_scan<ASM_NT>(msum, s_tmp, &mtot);
   const uint32_t* base = sorted32 + P.e_first;
-  const uint32_t nruns = (ne + ASM_RUN - 1) / ASM_RUN;
-  // a run's entries: independent loads, all in flight together
-  auto load_run = [&](uint32_t r, uint32_t (&ev)[ASM_RUN]) {
-    const uint32_t q0 = r * ASM_RUN, q1 = min(q0 + ASM_RUN, ne);
-    uint32_t j = s_rblk[r], ej = s_est[j + 1];
-    const uint32_t* src = base + ((int64_t)s_src[j] - (int64_t)s_est[j]);  // src[q] = entry q
-    if (q1 == q0 + ASM_RUN && q1 <= ej) {
-      // the whole run inside block j: 16-byte loads (a quarter of the cache-line requests of
-      // 16 dword loads strided by the run); gfx950 accepts unaligned global addresses
+  // run r: block j, its entries [k0, k0 + len) of the block; independent loads, all in flight
+  // together (a full run: four 16-byte loads -- gfx950 accepts unaligned global addresses; a
+  // short one: clamped dword loads)
+  // (pv: the block's entry before the run, or 0)
+  auto load_run = [&](uint32_t r, uint32_t (&ev)[ASM_RUN], uint32_t& pv) {
+    const uint32_t j = s_rblk[r], k0 = (r - s_est[j]) * ASM_RUN, c = s_c[j];
+    const uint32_t* src = base + s_src[j] + k0;
+    pv = k0 ? src[-1] : 0u;
+    if (k0 + ASM_RUN <= c) {
       static_assert(ASM_RUN % 4 == 0, "runs of whole 16-byte loads");
 #pragma unroll
       for (uint32_t i = 0; i < ASM_RUN; i += 4) {
         v4u x;
-        __builtin_memcpy(&x, src + q0 + i, 16);
+        __builtin_memcpy(&x, src + i, 16);
         ev[i] = x.x; ev[i + 1] = x.y; ev[i + 2] = x.z; ev[i + 3] = x.w;
       }
-      return;
-    }
+    } else {
+      const uint32_t last = c - k0 - 1;
 #pragma unroll
-    for (uint32_t i = 0; i < ASM_RUN; i++) {
-      const uint32_t q = q0 + i;
-      ev[i] = 0;
-      if (q < q1) {
-        if (q >= ej) {  // next non-empty block
-          do { j++; } while (s_est[j + 1] <= q);
-          ej = s_est[j + 1];
-          src = base + ((int64_t)s_src[j] - (int64_t)s_est[j]);
-        }
-        ev[i] = src[q];
-      }
+      for (uint32_t i = 0; i < ASM_RUN; i++) ev[i] = src[min(i, last)];
     }
   };
   // the first run's loads are issued before the fill, so they land while it runs
-  uint32_t ev0[ASM_RUN];
-  if (threadIdx.x < nruns) load_run(threadIdx.x, ev0);
+  uint32_t ev0[ASM_RUN], pv0 = 0;
+  if (threadIdx.x < nruns) load_run(threadIdx.x, ev0, pv0);
   // (B) fill: thread t builds its quads' words (16 bytes each) and stores each quad at once
   uint32_t jw = jw0;
 #pragma unroll
@@ -1987,19 +1985,29 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   const uint32_t qd = threadIdx.x * QPT + q;
   const uint32_t mw = mwq[q];
   if (4 * qd < nwp) {
+    // blocks are >= 9 bytes: the quad's 16 bytes lie in blocks ja, ja + 1 and ja + 2, whose
+    // metadata is read once (independent LDS reads) instead of per byte
+    const uint32_t ja = jw + (mw & 0xffu);  // the block holding the quad's first byte
+    jw += (mw & 0xffu) + ((mw >> 8) & 0xffu) + ((mw >> 16) & 0xffu) + (mw >> 24);
+    const uint32_t jb = min(ja + 1, nb - 1), jc = min(ja + 2, nb - 1);
+    const uint32_t o0 = s_off[ja], c0 = s_c[ja];
+    const uint32_t o1 = ja + 1 < nb ? s_off[jb] : 0xffffffffu, c1 = s_c[jb];
+    const uint32_t o2 = ja + 2 < nb ? s_off[jc] : 0xffffffffu, c2 = s_c[jc];
+    const uint32_t n0 = o0 + 2 + (c0 + IS - 1) / 8 + 4;  // end of block ja's encoding bytes
+    const uint32_t n1 = o1 + 2 + (c1 + IS - 1) / 8 + 4;
+    const uint32_t n2 = o2 + 2 + (c2 + IS - 1) / 8 + 4;
     uint32_t x4[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      jw += (mw >> (8 * k)) & 0xffu;
-      const uint32_t w = 4 * qd + k;
-      uint32_t j = jw, x = 0;
+      uint32_t x = 0;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const uint32_t B = 4 * w + i;
-        if (j + 1 < nb && s_off[j + 1] <= B) j++;  // blocks are >= 9 bytes: at most one step
-        const uint32_t rel = B - s_off[j], c = s_c[j];
-        const uint32_t enc = (c + IS - 1) / 8 + 4;
-        const uint32_t byte = rel < 2 ? ((c >> (8 * rel)) & 0xffu) : (rel < 2 + enc ? 0xffu : 0u);
+        const uint32_t B = 16 * qd + 4 * k + i;
+        const bool s2 = B >= o2, s1 = B >= o1;
+        const uint32_t o = s2 ? o2 : (s1 ? o1 : o0), c = s2 ? c2 : (s1 ? c1 : c0);
+        const uint32_t en = s2 ? n2 : (s1 ? n1 : n0);
+        const uint32_t rel = B - o;
+        const uint32_t byte = rel < 2 ? ((c >> (8 * rel)) & 0xffu) : (B < en ? 0xffu : 0u);
         x |= byte << (8 * i);
       }
       x4[k] = x;
@@ -2008,71 +2016,88 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   }
   }
   if (threadIdx.x < 4) s_pg[page_size / 4 + threadIdx.x] = 0;
-  __syncthreads();
+  __syncthreads();  // (also: s_wm read, s_gs free)
   DBG_PHASE_K(3, 1);
-  // (C) entry runs
+  // (C) entry runs, unrolled: entry k of block j clears encoding bit (j's encoding start) + k
+  // + its bucket offset, and ORs its rvs remainder|value bits at (j's remainder start) + k rvs.
+  // Encoding bits go into a 64-bit mask over two words (flushed, with two atomics, when an
+  // entry lands past it); remainder bits stream through a 64-bit accumulator that emits a word
+  // each time 32 bits have filled (an OR: a run's first and last words may be shared with its
+  // neighbours). Entries past a short run's end contribute nothing.
+  // Probe-line group boundaries come from the same entries (phase E's table s_gs): bucket
+  // b's terminator is encoding bit b + (entries in buckets <= b), so the bit after group g's
+  // last terminator (bucket gG - 1) is gG + (entries in groups < g). The run holding a block's
+  // first entry of group >= g writes it (its predecessor, pv, tells whether the group starts
+  // here); the run holding the block's last entry writes the groups past it.
   const uint32_t rmask = rvs >= 32 ? 0xffffffffu : ((1u << rvs) - 1);
+  const uint32_t bsh = rvs >= 32 ? 0u : rvs, bmask = rvs >= 32 ? 0u : IS - 1;  // bucket offset
   for (uint32_t r = threadIdx.x; r < nruns; r += ASM_NT) {
-    const uint32_t q0 = r * ASM_RUN, q1 = min(q0 + ASM_RUN, ne);
-    const uint32_t jr = s_rblk[r];
-    uint32_t ev[ASM_RUN];
-    if (r == threadIdx.x) {
+    const uint32_t j = s_rblk[r], k0 = (r - s_est[j]) * ASM_RUN, c = s_c[j];
+    const uint32_t len = min((uint32_t)ASM_RUN, c - k0);
+    uint32_t (&ev)[ASM_RUN] = ev0;  // one register buffer: the first run's entries were loaded before the fill
+    uint32_t& pv = pv0;
+    if (r != threadIdx.x) load_run(r, ev, pv);
+    if (cut) {
+      const uint32_t gb = j * (L + 1);
+      const uint32_t gp = k0 ? ((pv >> bsh) & bmask) >> lgG : 0u;  // group of the entry before the run
+      uint32_t last = ev[0];
 #pragma unroll
-      for (uint32_t i = 0; i < ASM_RUN; i++) ev[i] = ev0[i];
-    } else {
-      load_run(r, ev);
+      for (uint32_t i = 1; i < ASM_RUN; i++) last = i < len ? ev[i] : last;
+      const uint32_t gl = ((last >> bsh) & bmask) >> lgG;  // group of the run's last entry
+      // groups (gp, gl] start in this run (usually none or one), at the entry after those of
+      // smaller groups: entries below hi | (gG << bsh), hi = the index bits all entries share
+      const uint32_t hi = bsh + lis >= 32 ? 0u : ev[0] & ~((IS << bsh) - 1u);
+#pragma unroll 1
+      for (uint32_t g = gp + 1; g <= gl; g++) {
+        const uint32_t lim = hi | ((g * G) << bsh);
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < ASM_RUN; i++) before += (i < len && ev[i] < lim) ? 1u : 0u;
+        s_gs[gb + g] = (uint16_t)(g * G + k0 + before);
+      }
+      if (k0 + len == c)
+#pragma unroll 1
+        for (uint32_t g = gl + 1; g < L; g++) s_gs[gb + g] = (uint16_t)(g * G + c);
     }
-    uint32_t j = jr, ej = s_est[j + 1], kq = s_est[j];
-    uint32_t ebit = (s_off[j] + 2) * 8;  // page bit offsets < 2^15: 32-bit math
-    uint32_t rbit = (s_off[j] + 2 + (s_c[j] + IS - 1) / 8 + 4) * 8;
-    uint32_t eW = 0xffffffffu, rW = 0xffffffffu;  // current 64-bit windows (page bit / 64)
-    uint64_t eacc = 0, racc = 0;
-    auto flush_e = [&]() {
-      if (eW != 0xffffffffu) {
-        if ((uint32_t)eacc) atomicAnd(&s_pg[2 * eW], ~(uint32_t)eacc);
-        if ((uint32_t)(eacc >> 32)) atomicAnd(&s_pg[2 * eW + 1], ~(uint32_t)(eacc >> 32));
-      }
-      eacc = 0;
-    };
-    auto flush_r = [&]() {
-      if (rW != 0xffffffffu) {
-        if ((uint32_t)racc) atomicOr(&s_pg[2 * rW], (uint32_t)racc);
-        if ((uint32_t)(racc >> 32)) atomicOr(&s_pg[2 * rW + 1], (uint32_t)(racc >> 32));
-      }
-      racc = 0;
-    };
+    const uint32_t eb0 = (s_off[j] + 2) * 8 + k0;  // encoding bit of entry k0 at bucket offset 0
+    const uint32_t rb0 = (s_off[j] + 2 + (c + IS - 1) / 8 + 4) * 8 + k0 * rvs;
+    uint32_t wb = (eb0 + ((ev[0] >> bsh) & bmask)) & ~31u;
+    uint64_t m = 0;
 #pragma unroll
     for (uint32_t i = 0; i < ASM_RUN; i++) {
-      const uint32_t q = q0 + i;
-      if (q >= q1) break;
-      if (q >= ej) {
-        do { j++; } while (s_est[j + 1] <= q);
-        ej = s_est[j + 1];
-        kq = s_est[j];
-        ebit = (s_off[j] + 2) * 8;
-        rbit = (s_off[j] + 2 + (s_c[j] + IS - 1) / 8 + 4) * 8;
+      const uint32_t hb = eb0 + i + ((ev[i] >> bsh) & bmask);
+      const bool live = i < len;
+      if (live && hb - wb >= 64) {
+        if ((uint32_t)m) atomicAnd(&s_pg[wb >> 5], ~(uint32_t)m);
+        if ((uint32_t)(m >> 32)) atomicAnd(&s_pg[(wb >> 5) + 1], ~(uint32_t)(m >> 32));
+        m = 0;
+        wb = hb & ~31u;
       }
-      const uint32_t e = ev[i];
-      const uint32_t k = q - kq;
-      const uint32_t hb = ebit + k + (rvs >= 32 ? 0u : ((e >> rvs) & (IS - 1)));
-      const uint32_t hw = (uint32_t)(hb >> 6);
-      if (hw != eW) { flush_e(); eW = hw; }
-      eacc |= 1ull << (hb & 63);
-      if (rvs) {
-        const uint32_t rb = rbit + k * rvs;
-        const uint32_t rw = (uint32_t)(rb >> 6), sh = (uint32_t)(rb & 63);
-        if (rw != rW) { flush_r(); rW = rw; }
-        const uint64_t v = e & rmask;
-        racc |= v << sh;
-        if (sh + rvs > 64) {  // straddles into the next window
-          flush_r();
-          rW = rw + 1;
-          racc = v >> (64 - sh);
+      m |= (uint64_t)(live ? 1u : 0u) << ((hb - wb) & 63);
+    }
+    if ((uint32_t)m) atomicAnd(&s_pg[wb >> 5], ~(uint32_t)m);
+    if ((uint32_t)(m >> 32)) atomicAnd(&s_pg[(wb >> 5) + 1], ~(uint32_t)(m >> 32));
+    if (rvs >= 32) {  // (32-bit entries: rvs == 32) one whole word per entry, at a bit offset
+#pragma unroll
+      for (uint32_t i = 0; i < ASM_RUN; i++)
+        if (i < len) lds_or_bits(s_pg, rb0 + i * rvs, ev[i], rvs);
+    } else if (rvs) {
+      uint32_t w = rb0 >> 5, nbit = rb0 & 31;
+      uint64_t acc = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < ASM_RUN; i++) {
+        const bool live = i < len;
+        acc |= (uint64_t)(live ? ev[i] & rmask : 0u) << nbit;
+        nbit += live ? rvs : 0u;
+        if (nbit >= 32) {
+          atomicOr(&s_pg[w], (uint32_t)acc);
+          acc >>= 32;
+          nbit -= 32;
+          w++;
         }
       }
+      if (nbit) atomicOr(&s_pg[w], (uint32_t)acc);
     }
-    flush_e();
-    flush_r();
   }
   }  // word-parallel path
   __syncthreads();
@@ -2083,15 +2108,28 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
   DBG_PHASE_K(3, 3);
   if (!P.lines_asm) return;
   // (E) probe lines of the page's blocks, cut from the LDS image (format: "probe lines").
-  // E1: popcount scan over the blocks' encoding words -> group boundaries in s_gs.
-  const uint32_t lgG = P.lg_line - 1, G = 1u << lgG, L = IS >> lgG;
-  if (P.lines_flag) {  // this page's group table may not fit s_gs: then k_plines cuts its lines
-    const bool over = nb * (L + 1) > ASM_GT;
-    if (over) {
-      if (threadIdx.x == 0) pg_noline[1 + atomicAdd(&pg_noline[0], 1u)] = slot;  // k_plines_list
-      return;
-    }
+  if (!cut) {  // this page's group table does not fit s_gs: k_plines cuts its lines
+    if (threadIdx.x == 0) pg_noline[1 + atomicAdd(&pg_noline[0], 1u)] = slot;  // k_plines_list
+    return;
   }
+  if (ne <= ASM_MAXE) {
+    // the entry runs wrote every group boundary of blocks with entries; the first and end
+    // entries of each block and the boundaries of empty blocks here
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t j = threadIdx.x * 2 + q;
+      if (j < nb) {
+        const uint32_t c = s_c[j];
+        s_gs[j * (L + 1)] = 0;
+        s_gs[j * (L + 1) + L] = (uint16_t)(c + IS);
+        if (c == 0)
+          for (uint32_t g = 1; g < L; g++) s_gs[j * (L + 1) + g] = (uint16_t)(g * G);
+      }
+    }
+    __syncthreads();
+  } else {
+  // E1 (pages assembled by atomics): popcount scan over the blocks' encoding words -> group
+  // boundaries in s_gs.
   uint32_t wc[2], wsum = 0;  // encoding words per block (2 blocks per thread)
 #pragma unroll
   for (int q = 0; q < 2; q++) {
@@ -2144,11 +2182,12 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
     __syncthreads();
   }
+  }  // E1
   DBG_PHASE_K(3, 4);
   // E2: 4 lanes per line, 16 bytes each
   const uint32_t nt = nb * L * 4;
   for (uint32_t u = threadIdx.x; u < nt; u += ASM_NT) {
-    const uint32_t j = u / (L * 4), rest = u - j * (L * 4), gl = rest >> 2, qq = rest & 3;
+    const uint32_t j = u >> (lis - lgG + 2), rest = u & (4 * L - 1), gl = rest >> 2, qq = rest & 3;  // L = 2^(lis - lgG)
     const uint32_t c = s_c[j];
     const uint32_t ebit = (s_off[j] + 2) * 8, rbit = (s_off[j] + 2 + (c + IS - 1) / 8 + 4) * 8;
     const uint32_t a = s_gs[j * (L + 1) + gl], ne2 = s_gs[j * (L + 1) + gl + 1] - a;
