@@ -1030,14 +1030,15 @@ __global__ __launch_bounds__(SORT_NT, 6) void k_cb_sort(const FilterPlan* __rest
 // compaction chain). Only the new entries are sorted (bins over their top bits sized to their
 // count, then sorting networks); a new entry is dropped if it equals the previous new one
 // (duplicates are dropped only among the new entries; one equal to an old entry is kept after
-// it, src/routing_filter.c:559-597). A binary search of the old run gives each kept entry's
-// final position (its rank among the kept new + the old entries not above it). The output is then written 64 slots
-// per wave step: the step's new slots form a bit mask, each lane takes its entry from the new
-// list (mbcnt of the mask) or the old run (slot - new entries before it); num_unique compares
-// each entry with its predecessor (a lane shift). The old run reaches LDS by LDS-DMA and is
-// never sorted, scattered or compacted (the K4 DUAL path did all three). Buckets with more new
-// entries than MRG_NEW_CAP, or a bin of more than 64 equal-bin new entries, go to k_cb_sort in
-// list mode (bit 31 on their overflow-list entry); buckets over SORT_CAP to K4b as before.
+// it, src/routing_filter.c:559-597). The old run reaches LDS by LDS-DMA while the new entries
+// sort, and is never sorted, scattered or compacted (the K4 DUAL path did all three). The
+// merge (old first on equal entries) gives each thread a contiguous share of the output (a
+// merge-path split of both runs, merged into registers); the merged run is staged in place
+// over the old run and copied out with coalesced stores, num_unique and the index starts
+// computed on the way.
+// Buckets with more new entries than MRG_NEW_CAP, or a bin of more than 64 equal-bin new
+// entries, go to k_cb_sort in list mode (bit 31 on their overflow-list entry); buckets over
+// SORT_CAP to K4b as before.
 constexpr uint32_t MRG_NEW_CAP = 2048;
 constexpr uint32_t MRG_LNB_MAX = 9;  // at most 512 bins
 constexpr uint32_t MRG_RUN = (SORT_CAP + SORT_NT - 1) / SORT_NT + 1;  // output slots per thread (odd)
@@ -2082,19 +2083,31 @@ __global__ __launch_bounds__(ASM_NT) __attribute__((amdgpu_waves_per_eu(8))) voi
       for (uint32_t i = 0; i < ASM_RUN; i++)
         if (i < len) lds_or_bits(s_pg, rb0 + i * rvs, ev[i], rvs);
     } else if (rvs) {
-      uint32_t w = rb0 >> 5, nbit = rb0 & 31;
+      // a word can only have filled after every 32 / rvs entries (uniform check points: the
+      // accumulator then holds < 64 bits)
+      const uint32_t per = 32u / rvs;
+      uint32_t w = rb0 >> 5, nbit = rb0 & 31, since = 0;
       uint64_t acc = 0;
 #pragma unroll
       for (uint32_t i = 0; i < ASM_RUN; i++) {
         const bool live = i < len;
         acc |= (uint64_t)(live ? ev[i] & rmask : 0u) << nbit;
         nbit += live ? rvs : 0u;
-        if (nbit >= 32) {
-          atomicOr(&s_pg[w], (uint32_t)acc);
-          acc >>= 32;
-          nbit -= 32;
-          w++;
+        if (++since == per) {
+          since = 0;
+          if (nbit >= 32) {
+            atomicOr(&s_pg[w], (uint32_t)acc);
+            acc >>= 32;
+            nbit -= 32;
+            w++;
+          }
         }
+      }
+      if (nbit >= 32) {
+        atomicOr(&s_pg[w], (uint32_t)acc);
+        acc >>= 32;
+        nbit -= 32;
+        w++;
       }
       if (nbit) atomicOr(&s_pg[w], (uint32_t)acc);
     }
