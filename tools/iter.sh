@@ -1,12 +1,9 @@
 #!/bin/bash
-# r05 call 42: SQ counters of the C2 step with the reworked K6 (VALU, LDS, conflicts per kernel)
+# r05 call 43: K4m merge read-ahead A/B on the round-8 chain
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r05d42
+O=gpurun_out/r05d43
 mkdir -p $O
-BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e"
-SQ="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU"
-timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d $O/sq -o c2 -- python3 $BENCH > $O/sq.log 2>&1 || { echo "pmc sq failed"; exit 1; }
-python3 tools/sq_summary.py $O/sq/c2_counter_collection.csv > $O/sq_end.txt || exit 1
-cat $O/sq_end.txt
+AB_REPS=5 timeout -k 10 500 python3 tools/ab_chain.py tools/ab/librf_amd_base.so tools/ab/librf_amd_k4r.so > $O/chain.json 2> $O/chain.err || { echo "chain failed"; tail $O/chain.err; exit 1; }
+cat $O/chain.json | cut -c1-1500
