@@ -100,12 +100,19 @@ mono_ns(void)
    return (uint64)ts.tv_sec * 1000000000ull + (uint64)ts.tv_nsec;
 }
 
+static void shim_at_exit(void);
+
 static void
 engine_init(void)
 {
    const uint64 t0 = mono_ns();
    const char  *d  = getenv("RF_AMD_DEVICE");
    g_eng_rc        = rf_amd_engine_create(d ? atoi(d) : 0, &g_eng);
+   if (g_eng_rc == 0) {
+      /* registered after the engine library's own exit handler (rf_amd_engine_create), so it
+         runs first: the shim's threads stop before the engine is torn down */
+      (void)atexit(shim_at_exit);
+   }
    /* a storage engine links this: its pool keeps at most 2 GiB parked unless
       RF_AMD_POOL_MIB says otherwise (one add's batch is at most a few hundred MB) */
    if (g_eng_rc == 0 && !getenv("RF_AMD_POOL_MIB")) {
@@ -1652,6 +1659,12 @@ bq_complete(void)
 /* the batch thread: takes the whole stack whenever it is free -- what arrived during one GPU
  * round trip goes out in the next; a burst of submissions settles first (no arrival for a
  * microsecond, at most 4) */
+/* the shim's threads (completion, batch): joinable, stopped by shim_at_exit */
+#define SHIM_THREADS_MAX 9
+static pthread_t g_threads[SHIM_THREADS_MAX];
+static uint32    g_nthreads;
+static int       g_stopping; /* atomic: the threads leave their loops */
+
 static void *
 batch_main(void *arg)
 {
@@ -1665,11 +1678,14 @@ batch_main(void *arg)
          }
          pthread_mutex_lock(&g_bq_mu);
          __atomic_add_fetch(&g_bq_sleeping, 1, __ATOMIC_SEQ_CST);
-         while (!__atomic_load_n(&g_bq_head, __ATOMIC_SEQ_CST)) {
+         while (!__atomic_load_n(&g_bq_head, __ATOMIC_SEQ_CST) && !__atomic_load_n(&g_stopping, __ATOMIC_SEQ_CST)) {
             pthread_cond_wait(&g_bq_cv, &g_bq_mu);
          }
          __atomic_sub_fetch(&g_bq_sleeping, 1, __ATOMIC_SEQ_CST);
          pthread_mutex_unlock(&g_bq_mu);
+      }
+      if (__atomic_load_n(&g_stopping, __ATOMIC_SEQ_CST)) {
+         break;
       }
       uint64       c0 = __atomic_load_n(&g_bq_count, __ATOMIC_RELAXED);
       const uint64 t0 = now_ns();
@@ -1753,7 +1769,7 @@ completion_main(void *arg)
 {
    (void)arg;
    platform_ensure_thread_registered(); /* callbacks and cache_get (imports) run here */
-   for (;;) {
+   while (!__atomic_load_n(&g_stopping, __ATOMIC_SEQ_CST)) {
       if (async_reap_complete()) {
          continue;
       }
@@ -1763,7 +1779,7 @@ completion_main(void *arg)
       }
       pthread_mutex_lock(&g_aq_mu);
       __atomic_store_n(&g_aq_sleeping, 1, __ATOMIC_SEQ_CST);
-      while (!__atomic_load_n(&g_aq_outstanding, __ATOMIC_SEQ_CST)) {
+      while (!__atomic_load_n(&g_aq_outstanding, __ATOMIC_SEQ_CST) && !__atomic_load_n(&g_stopping, __ATOMIC_SEQ_CST)) {
          pthread_cond_wait(&g_aq_cv, &g_aq_mu);
       }
       __atomic_store_n(&g_aq_sleeping, 0, __ATOMIC_SEQ_CST);
@@ -1775,18 +1791,46 @@ completion_main(void *arg)
 static void
 aq_init(void)
 {
-   pthread_attr_t at;
-   pthread_attr_init(&at);
-   pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
-   pthread_t t;
-   platform_assert(pthread_create(&t, &at, completion_main, NULL) == 0);
+   platform_assert(pthread_create(&g_threads[g_nthreads++], NULL, completion_main, NULL) == 0);
    /* RF_SHIM_BATCH_THREADS batch threads (default 1; 2: a batch goes out while the previous
       one is on the GPU) */
    uint64 nb = env_u64("RF_SHIM_BATCH_THREADS", 1);
-   for (uint64 k = 0; k < (nb >= 1 && nb <= 8 ? nb : 1); k++) {
-      platform_assert(pthread_create(&t, &at, batch_main, NULL) == 0);
+   for (uint64 k = 0; k < (nb >= 1 && nb <= SHIM_THREADS_MAX - 1 ? nb : 1); k++) {
+      platform_assert(pthread_create(&g_threads[g_nthreads++], NULL, batch_main, NULL) == 0);
    }
-   pthread_attr_destroy(&at);
+}
+
+/* Process exit (atexit, registered when the engine was created): the completion and batch
+ * threads leave their loops and are joined, then the engine is destroyed -- its server wave
+ * stopped, streams drained, pinned rings freed, cache registrations dropped -- before HIP
+ * unregisters the engine library's kernels (the heap abort in
+ * __hipUnregisterFatBinary at the exit of a process running the shim). A thread that does not
+ * return within 2 s (stuck in a callback or a GPU wait) leaves the engine alone. States still
+ * queued at exit are not completed: their owners are gone. */
+static void
+shim_at_exit(void)
+{
+   __atomic_store_n(&g_stopping, 1, __ATOMIC_SEQ_CST);
+   pthread_mutex_lock(&g_aq_mu);
+   pthread_cond_broadcast(&g_aq_cv);
+   pthread_mutex_unlock(&g_aq_mu);
+   pthread_mutex_lock(&g_bq_mu);
+   pthread_cond_broadcast(&g_bq_cv);
+   pthread_mutex_unlock(&g_bq_mu);
+   int joined = 1;
+   for (uint32 i = 0; i < g_nthreads; i++) {
+      struct timespec dl;
+      clock_gettime(CLOCK_REALTIME, &dl);
+      dl.tv_sec += 2;
+      if (pthread_timedjoin_np(g_threads[i], NULL, &dl) != 0) {
+         joined = 0;
+      }
+   }
+   if (joined && g_eng) {
+      rf_amd_engine_destroy(g_eng);
+      g_eng    = NULL;
+      g_eng_rc = RF_AMD_ENODEV;
+   }
 }
 
 /* complete every state submitted so far, in the caller's thread (reaping with the

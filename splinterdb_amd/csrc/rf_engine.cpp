@@ -184,6 +184,10 @@ struct LookupServer {
   };
   Meta meta[SRV_RING];
   std::atomic<uint64_t> consumed[SRV_RING];  // per slot: 1 + the last ticket whose result was taken
+  // per slot: a ticket whose submitter gave up before publishing it (the server died while it
+  // waited for the slot): the reap and failure cursors step over it instead of waiting on it
+  std::atomic<uint64_t> abandoned[SRV_RING];
+  std::atomic<uint64_t> last_check_ns{0};  // the reaper's last look at the server stream
   std::atomic<uint64_t> tail{0};        // the next ticket
   std::atomic<uint64_t> state{0};       // generation << 1 | running
   std::mutex reap_mu;
@@ -303,6 +307,35 @@ struct rf_amd_batch {
 
 extern "C" const char* rf_amd_last_error(void) { return g_err.c_str(); }
 
+// ---- engines alive at process exit ---------------------------------------------------------
+// The compiler-generated constructor of this library registers its kernels with HIP when the
+// library loads and registers, with atexit, the destructor that unregisters them again. An
+// engine still alive at exit then has a lookup-server wave that may be running, pinned rings
+// the GPU writes, host registrations and streams -- and the process's other threads (a
+// drop-in's completion threads) may still be inside HIP calls -- while HIP tears the code
+// objects down (a free() of an invalid pointer in __hipUnregisterFatBinary at the
+// exit of the two-stack latency tool). Every engine alive at exit is therefore destroyed by a
+// handler registered at the first engine creation, i.e. after the library's own destructor,
+// so it runs before it (atexit order): server waves stopped, streams drained, pinned memory
+// freed, registrations dropped. A drop-in that owns threads stops them in its own handler,
+// registered after its engine's creation, so that one runs first (shim/routing_filter_amd.c).
+static std::mutex g_live_mu;
+static std::vector<rf_amd_engine*>* g_live = nullptr;  // never destroyed: read by the exit handler
+static bool engine_quiesce(rf_amd_engine* e, int budget_ms);
+static void engine_destroy_now(rf_amd_engine* e, bool device_sync);
+static void engines_at_exit() {
+  std::vector<rf_amd_engine*> v;
+  {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (g_live) v.swap(*g_live);
+  }
+  for (rf_amd_engine* e : v) {
+    // a stream that does not drain in time (a hung kernel) leaves the engine as it is: exit
+    // must not wait forever
+    if (engine_quiesce(e, 2000)) engine_destroy_now(e, false);
+  }
+}
+
 extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
@@ -326,6 +359,13 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
     delete e;
     return fail(RF_AMD_EINVAL, "hipStreamCreate failed");
   }
+  {
+    static std::once_flag at_exit_once;
+    std::call_once(at_exit_once, [] { (void)atexit(engines_at_exit); });
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (!g_live) g_live = new std::vector<rf_amd_engine*>();
+    g_live->push_back(e);
+  }
   *out = e;
   return 0;
 }
@@ -333,9 +373,18 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
 static void srv_stop(rf_amd_engine* e);
 extern "C" void rf_amd_engine_destroy(rf_amd_engine* e) {
   if (!e) return;
+  {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (g_live) g_live->erase(std::remove(g_live->begin(), g_live->end(), e), g_live->end());
+  }
+  engine_destroy_now(e, true);
+}
+
+// device_sync false: the engine's own streams are known drained (engines_at_exit)
+static void engine_destroy_now(rf_amd_engine* e, bool device_sync) {
   (void)hipSetDevice(e->device);
   srv_stop(e);
-  (void)hipDeviceSynchronize();
+  if (device_sync) (void)hipDeviceSynchronize();
   (void)hipStreamDestroy(e->stream);
   for (ProbeSlot* s : e->slots_all) {
     if (s->st) (void)hipStreamDestroy(s->st);
@@ -1298,6 +1347,7 @@ static int srv_init(rf_amd_engine* e) {
       v.ring[s].ticket = SRV_UNPUBLISHED;
       v.res[s].ticket = SRV_UNPUBLISHED;
       v.consumed[s].store(0, std::memory_order_relaxed);
+      v.abandoned[s].store(~0ull, std::memory_order_relaxed);
     }
     memset(v.ctl, 0, sizeof(SrvCtl));
     // a CU-masked stream is a queue of its own: the persistent wave never sits in front of
@@ -1359,6 +1409,35 @@ static void srv_stop(rf_amd_engine* e) {
   v.ctl = nullptr;
 }
 
+// stops the server wave and waits, at most budget_ms, for the engine's streams to drain (no
+// device-wide wait: other streams of the process are not the engine's)
+static bool stream_drained(hipStream_t st, uint64_t deadline_ns);
+static bool engine_quiesce(rf_amd_engine* e, int budget_ms) {
+  (void)hipSetDevice(e->device);
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  const uint64_t deadline = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec + (uint64_t)budget_ms * 1000000ull;
+  LookupServer& v = e->srv;
+  if (v.ctl) __atomic_store_n(&v.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  if (v.st && !stream_drained(v.st, deadline)) return false;
+  if (!stream_drained(e->stream, deadline)) return false;
+  std::lock_guard<std::mutex> g(e->slot_mu);
+  for (ProbeSlot* s : e->slots_all)
+    if (s->st && !stream_drained(s->st, deadline)) return false;
+  return true;
+}
+static bool stream_drained(hipStream_t st, uint64_t deadline_ns) {
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q != hipErrorNotReady) return true;  // idle, or faulted: nothing more will run on it
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    if ((uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec > deadline_ns) return false;
+    struct timespec nap = {0, 100000};
+    nanosleep(&nap, nullptr);
+  }
+}
+
 // the server stream's error, if its kernel faulted (checked while waiting)
 static int srv_check(rf_amd_engine* e) {
   const hipError_t q = hipStreamQuery(e->srv.st);
@@ -1391,9 +1470,13 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     for (uint32_t spin = 1; v.consumed[slot].load(std::memory_order_acquire) != t - SRV_RING + 1; spin++) {
       __builtin_ia32_pause();
       if ((spin & 1023) == 0) {  // ticket t stays unpublished only on a server that is dead
-        if (int rc = srv_ensure(e)) return rc;
-        if (int rc = srv_check(e)) return rc;
-        if (int rc = srv_dead(e)) return rc;
+        int rc = srv_ensure(e);
+        if (!rc) rc = srv_check(e);
+        if (!rc) rc = srv_dead(e);
+        if (rc) {  // ticket t is never published: the cursors step over it
+          v.abandoned[slot].store(t, std::memory_order_release);
+          return rc;
+        }
       }
     }
     // the slot is being rewritten: readers that see this do not trust its payload or tag
@@ -1453,6 +1536,10 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
       __builtin_prefetch(&v.meta[(t + 16) & (SRV_RING - 1)], 0, 0);
     }
     const uint64_t tk = v.meta[slot].ticket.load(std::memory_order_acquire);
+    if (tk != t && v.abandoned[slot].load(std::memory_order_acquire) == t) {  // never published
+      t++;
+      continue;
+    }
     if (tk == SRV_UNPUBLISHED || tk == SRV_BUSY || tk < t) break;  // not yet published
     if (tk > t) {  // a waiter already took ticket t and its slot was reused
       t++;
@@ -1474,7 +1561,17 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
   }
   v.reap_next = t;
   lk.unlock();
-  if (n == 0 && t < tail) (void)srv_ensure(e);
+  if (n == 0 && t < tail) {
+    (void)srv_ensure(e);
+    // a faulted server stream never answers and nothing else would notice with only tagged
+    // tickets outstanding: look at it about once a millisecond, so `dead` gets set and the
+    // caller's rf_amd_lookup_server_error / _failed path completes the waiting states
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    const uint64_t now = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+    uint64_t last = v.last_check_ns.load(std::memory_order_relaxed);
+    if (now - last > 1000000 && v.last_check_ns.compare_exchange_strong(last, now)) (void)srv_check(e);
+  }
   return n;
 }
 
@@ -1486,10 +1583,21 @@ extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, u
   std::lock_guard<std::mutex> lk(v.reap_mu);
   uint64_t n = 0, t = v.reap_next;
   const uint64_t tail = v.tail.load(std::memory_order_acquire);
+  // Stops at the first ticket not yet published: a submitter that passed the dead
+  // check before `dead` was set publishes it later, and the next call hands its tag back. A
+  // ticket its submitter abandoned is stepped over; a slot already holding a later ticket means
+  // a waiter took ticket t (waiters' tickets are not tagged).
   for (; n < max && t < tail; t++) {
     const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
-    if (v.meta[slot].ticket.load(std::memory_order_acquire) != t) continue;  // unpublished or reused
+    const uint64_t tk = v.meta[slot].ticket.load(std::memory_order_acquire);
+    if (tk != t) {
+      if (v.abandoned[slot].load(std::memory_order_acquire) == t) continue;
+      if (tk == SRV_UNPUBLISHED || tk == SRV_BUSY || tk < t) break;
+      continue;  // reused: a waiter's ticket, already taken
+    }
     void* tag = v.meta[slot].tag;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (v.meta[slot].ticket.load(std::memory_order_relaxed) != t) break;  // being rewritten: next call
     if (!tag) continue;
     if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) == t) break;  // answered: reap takes it
     tags[n++] = tag;
@@ -1497,6 +1605,15 @@ extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, u
   }
   v.reap_next = t;
   return n;
+}
+
+// diagnostics (rf_amd_diag.h): mark the lookup server dead as a failed launch would
+extern "C" int rf_amd_diag_lookup_server_kill(rf_amd_engine* e, int err) {
+  if (!e || !err) return fail(RF_AMD_EINVAL, "bad argument");
+  if (int rc = srv_init(e)) return rc;
+  int z = 0;
+  e->srv.dead.compare_exchange_strong(z, err);
+  return 0;
 }
 
 extern "C" int rf_amd_lookup_server_error(rf_amd_engine* e) { return e ? e->srv.dead.load() : RF_AMD_ENODEV; }

@@ -247,3 +247,78 @@ def test_device_sync_while_server_busy_is_short():
     assert n[0] > 100, n[0]
     assert ts[len(ts) // 2] < 1.0e-3 and ts[-1] < 3.0e-3, ts
     b.close(stream().cuda_stream)
+
+
+def test_dead_server_returns_every_tag():
+    """a server that dies (here marked dead by the diagnostics hook, as a failed
+    launch or a faulted stream marks it) while threads submit tagged lookups: every tag whose
+    submit succeeded comes back exactly once, answered (rf_amd_lookup_reap) or with the error
+    (rf_amd_lookup_server_failed) -- including tickets published after `dead` was set and the
+    tickets of submitters that gave up waiting for a slot -- and every later submit fails."""
+    eng = E.Engine(0)  # a server killed for good: an engine of its own
+    cfg = E.routing_config_init(log_index_size=8)
+    rng = np.random.default_rng(11)
+    h = rng.integers(0, 1 << 32, size=50_000, dtype=np.uint64).astype(np.uint32)
+    with torch.cuda.stream(stream()):
+        b = E.FilterBatch(cfg, [50_000], [0], engine=eng)
+        b.build_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"))
+    sync()
+    nth, per = 4, 3000
+    ok = [[] for _ in range(nth)]
+    refused = [0] * nth
+    submitted = [0]
+    done_submitting = threading.Event()
+    lock = threading.Lock()
+
+    def submitter(k):
+        for i in range(per):
+            tag = k * 100_000 + i + 1
+            t = ctypes.c_uint64()
+            rc = lib().rf_amd_lookup_submit(eng.h, b.h, 0, int(h[(k * per + i) % h.size]), tag, ctypes.byref(t))
+            if rc == 0:
+                ok[k].append(tag)
+            else:
+                refused[k] += 1
+            with lock:
+                submitted[0] += 1
+
+    def killer():
+        while submitted[0] < 2000:
+            time.sleep(0.0002)
+        E._check(lib().rf_amd_diag_lookup_server_kill(eng.h, 5))
+
+    got = {}
+    dup = []
+    tags = (ctypes.c_void_p * 256)()
+    found = (ctypes.c_uint64 * 256)()
+    ths = [threading.Thread(target=submitter, args=(k,)) for k in range(nth)] + [threading.Thread(target=killer)]
+    for t in ths:
+        t.start()
+    t0 = time.time()
+    while True:
+        k = lib().rf_amd_lookup_reap(eng.h, ctypes.addressof(tags), ctypes.addressof(found), 256)
+        for i in range(k):
+            if tags[i] in got:
+                dup.append(tags[i])
+            got[tags[i]] = "answered"
+        if lib().rf_amd_lookup_server_error(eng.h):
+            k = lib().rf_amd_lookup_server_failed(eng.h, ctypes.addressof(tags), 256)
+            for i in range(k):
+                if tags[i] in got:
+                    dup.append(tags[i])
+                got[tags[i]] = "failed"
+        if not any(t.is_alive() for t in ths) and len(got) >= sum(len(o) for o in ok):
+            break
+        assert time.time() - t0 < 60, (len(got), sum(len(o) for o in ok))
+    for t in ths:
+        t.join(10)
+    want = {t for o in ok for t in o}
+    assert not dup
+    assert set(got) == want
+    assert sum(refused) > 0 and "failed" in got.values()
+    assert lib().rf_amd_lookup_server_error(eng.h) == 5
+    t = ctypes.c_uint64()
+    assert lib().rf_amd_lookup_submit(eng.h, b.h, 0, 1, 1, ctypes.byref(t)) != 0
+    b.close(stream().cuda_stream)
+    sync()
+    eng.close()

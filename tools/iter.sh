@@ -1,12 +1,15 @@
 #!/bin/bash
-# r05 call 44: PMC HBM traffic (FETCH_SIZE, WRITE_SIZE passes) of the final round-5 code
+# r06 call 4: the lookup-server tests (ADVICE r5 dead-server test) and the two-stack latency tool
+# run to its natural exit (no --fast-exit)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r05d44
+O=gpurun_out/r06d
 mkdir -p $O
-BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pf -o c2 -- python3 $BENCH > $O/pf.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pw -o c2 -- python3 $BENCH > $O/pw.log 2>&1 || { echo "pmc write failed"; exit 1; }
-python3 profiles/pmc_summary.py $O/pf/c2_counter_collection.csv $O/pw/c2_counter_collection.csv $O/pmc_end.json || exit 1
-python3 -c "import json; d=json.load(open('$O/pmc_end.json')); print(json.dumps(d['per_launch_hbm_bytes']))"
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_server.py > $O/t_server.log 2>&1 || { echo "server tests failed"; tail -30 $O/t_server.log; exit 1; }
+tail -3 $O/t_server.log
+timeout -k 10 600 python3 tools/shim_latency.py > $O/shim_latency.json 2> $O/shim_latency.err
+rc=$?
+echo "shim_latency rc=$rc"
+tail -5 $O/shim_latency.err
+exit $rc

@@ -44,7 +44,7 @@ python3 tools/sq_summary.py $O/sq3/c3_counter_collection.csv > $O/sq_c3_$TAG.txt
 timeout -k 10 300 python3 bench.py --workload compaction --steps 5 --warmup 1 > $O/bench_compaction.json 2> $O/bench_compaction.err || { echo "bench compaction failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktc -o comp -- python3 bench.py --workload compaction --steps 2 --warmup 0 --no-cpu-baseline > $O/ktc.log 2>&1 || { echo "compaction kernel trace failed"; exit 1; }
 # the drop-in's per-call costs beside the reference's routing_filter.c (tools/shim_latency.py)
-timeout -k 10 600 python3 tools/shim_latency.py --fast-exit > $O/shim_latency_$TAG.json 2> $O/shim_latency.err || { echo "shim latency failed"; exit 1; }
+timeout -k 10 600 python3 tools/shim_latency.py > $O/shim_latency_$TAG.json 2> $O/shim_latency.err || { echo "shim latency failed"; exit 1; }
 timeout -k 10 300 python3 tools/trunk_latency.py > $O/trunk_latency_$TAG.json 2> $O/trunk_latency.err || { echo "trunk latency failed"; exit 1; }
 fi
 cat $O/bench_c2.json 2>/dev/null || true

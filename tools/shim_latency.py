@@ -119,5 +119,3 @@ for name, path in (("shim", R.SHIM_PATH), ("reference", R.LIB_PATH)):
             r["shim_stats"] = st
         out[name] = r
 print(json.dumps(out), flush=True)
-if "--fast-exit" in sys.argv:  # skip interpreter finalization (A/B runs; see DESIGN §2 on the exit abort)
-    os._exit(0)
