@@ -46,10 +46,12 @@ int rf_amd_diag_lookup_stats(uint64_t *out, int reset);
  * ticket the last exited server did not serve */
 int rf_amd_lookup_server_stats(rf_amd_engine *e, uint64_t *out);
 
-/* marks the engine's lookup server dead with error `err`, exactly as a failed launch or a
- * faulted server stream does (tests of the error path: every submitted tag must come back
- * through rf_amd_lookup_reap or rf_amd_lookup_server_failed) */
-int rf_amd_diag_lookup_server_kill(rf_amd_engine *e, int err);
+/* stops the engine's lookup server (its wave exits; relaunched waves exit at once) and, gap_us
+ * microseconds later, marks it dead with error `err`, exactly as a failed launch or a faulted
+ * server stream does: tickets published in the gap are never answered (tests of the error
+ * path: every submitted tag must come back through rf_amd_lookup_reap or
+ * rf_amd_lookup_server_failed) */
+int rf_amd_diag_lookup_server_kill(rf_amd_engine *e, int err, uint32_t gap_us);
 
 /* the source id the library was built from (16 hex digits of SHA-256 over the engine's
  * sources and headers, splinterdb_amd/build.py source_id): the Python loader refuses a

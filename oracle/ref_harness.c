@@ -685,12 +685,15 @@ routing_filter_amd_async_breakdown(uint64 *out);
 __attribute__((weak)) void
 routing_filter_amd_add_breakdown(uint64 *out);
 
-/* out[0..8]: the shim's routing_filter_add breakdown (calls, batches, create / stage / build /
- * infos / readback ns per batch, wait / place ns per add); 0 without a shim */
+/* out[0..10]: the shim's routing_filter_add breakdown (calls, batches, create / stage / build /
+ * infos / readback ns per batch, wait / place ns per add; ns creating the engine, registering
+ * cache buffers); 0 without a shim. (Round 5 declared out[0..8] here while the shim writes 11
+ * words: the Python caller's 9-word buffer was overrun by 16 bytes on every call -- the heap
+ * corruption behind the two-stack latency tool's aborts) */
 int
 rfr_add_breakdown(uint64 *out)
 {
-   memset(out, 0, 9 * sizeof(uint64));
+   memset(out, 0, 11 * sizeof(uint64));
    if (!routing_filter_amd_add_breakdown) {
       return 0;
    }

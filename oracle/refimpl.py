@@ -417,11 +417,11 @@ class Stack:
     def add_breakdown(self):
         """the shim's routing_filter_add so far: calls, combiner batches, ns per phase (None
         for the reference's library)"""
-        out = np.zeros(9, dtype=np.uint64)
+        out = np.zeros(11, dtype=np.uint64)  # routing_filter_amd_add_breakdown writes 11 words
         if not self.L.rfr_add_breakdown(_p(out)):
             return None
         keys = ("calls", "batches", "create_ns", "stage_ns", "build_ns", "infos_ns", "readback_ns", "wait_ns",
-                "place_ns")
+                "place_ns", "engine_create_ns", "register_ns")
         return dict(zip(keys, (int(x) for x in out)))
 
     def async_breakdown(self):

@@ -892,7 +892,9 @@ int
 routing_filter_amd_cache_attach(cache *cc)
 {
    rf_amd_engine *e = engine();
-   if (!e || !cc) {
+   if (!e || !cc || !direct_enabled()) {
+      /* RF_SHIM_DIRECT=0: nothing is registered (a caller that sees -1 need not release;
+         ADVICE r5: a registration here outlived the buffer's munmap) */
       return -1;
    }
    clockcache *ccc   = (clockcache *)cc;
@@ -916,7 +918,7 @@ routing_filter_amd_cache_attach(cache *cc)
    }
    ok = direct_register(e, i, base, bytes);
    pthread_mutex_unlock(&g_direct_mu);
-   return direct_enabled() && ok ? 0 : -1;
+   return ok ? 0 : -1;
 }
 
 /* out[0] = caches registered now, out[1] = registrations found stale by a placement */

@@ -1375,8 +1375,10 @@ static int srv_init(rf_amd_engine* e) {
 // make sure a server wave is running (or queued): the first submit launches one; a server that
 // exited (idle, lifetime, stop) while tickets wait is relaunched from the first ticket it did
 // not serve. The generation CAS makes exactly one caller launch.
+static int srv_dead(rf_amd_engine* e);
 static int srv_ensure(rf_amd_engine* e) {
   LookupServer& v = e->srv;
+  if (int rc = srv_dead(e)) return rc;  // a dead server is never relaunched
   uint64_t s = v.state.load(std::memory_order_acquire);
   const uint64_t gen = s >> 1;
   if (s & 1) {
@@ -1492,7 +1494,11 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
   v.meta[slot].ticket.store(t, std::memory_order_release);
   __atomic_store_n(&q.ticket, t, __ATOMIC_RELEASE);
   *ticket = t;
-  return srv_ensure(e);
+  // published: from here the ticket's tag comes back through rf_amd_lookup_reap or, if the
+  // server is (or now becomes) dead, rf_amd_lookup_server_failed -- so a launch failure here is
+  // not the submit's error (the caller would complete the state a second time)
+  (void)srv_ensure(e);
+  return 0;
 }
 
 extern "C" int rf_amd_lookup_wait(rf_amd_engine* e, uint64_t ticket, uint64_t* found_values) {
@@ -1607,10 +1613,17 @@ extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, u
   return n;
 }
 
-// diagnostics (rf_amd_diag.h): mark the lookup server dead as a failed launch would
-extern "C" int rf_amd_diag_lookup_server_kill(rf_amd_engine* e, int err) {
+// diagnostics (rf_amd_diag.h): the server stops answering (its wave told to exit; a relaunched
+// wave exits at once), then, after `gap_us`, is marked dead as a failed launch or a faulted
+// stream marks it: tickets published in the gap are never answered
+extern "C" int rf_amd_diag_lookup_server_kill(rf_amd_engine* e, int err, uint32_t gap_us) {
   if (!e || !err) return fail(RF_AMD_EINVAL, "bad argument");
   if (int rc = srv_init(e)) return rc;
+  __atomic_store_n(&e->srv.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  if (gap_us) {
+    struct timespec nap = {(time_t)(gap_us / 1000000), (long)(gap_us % 1000000) * 1000};
+    nanosleep(&nap, nullptr);
+  }
   int z = 0;
   e->srv.dead.compare_exchange_strong(z, err);
   return 0;

@@ -3709,6 +3709,10 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
     for (uint32_t m = 0; m < SRV_PER; m++)
       tk[m] = __hip_atomic_load(&ring[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))].ticket, __ATOMIC_RELAXED,
                                 __HIP_MEMORY_SCOPE_SYSTEM);
+    // the host's stop word, read beside the tickets (in flight with them: no extra round trip),
+    // so a busy wave stops too (engine shutdown, a server marked dead)
+    uint64_t stp = lane == 0 ? __hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    if (__shfl(stp, 0)) break;
     uint32_t k = 0;  // the ready prefix
 #pragma unroll
     for (uint32_t m = 0; m < SRV_PER; m++) {

@@ -155,7 +155,7 @@ def load_library(build_if_missing=True):
     L.rf_amd_lookup_server_failed.argtypes = [vp, vp, u64]
     L.rf_amd_lookup_server_failed.restype = u64
     L.rf_amd_lookup_server_set_times.argtypes = [vp, u64, u64]
-    L.rf_amd_diag_lookup_server_kill.argtypes = [vp, i32]
+    L.rf_amd_diag_lookup_server_kill.argtypes = [vp, i32, u32]
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
     L.rf_amd_filter_add.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),

@@ -147,10 +147,11 @@ def _all_gather_padded(dist, t, world):
     return [o[:k] for o, k in zip(outs, ns)]
 
 
-def replicate_images(batch, world, device, dist=None, coll_device=None, engine=None):
+def replicate_images(batch, world, device, dist=None, coll_device=None, engine=None, collective_at_one=False):
     """Every rank's filters (in rank = global filter order) as one probe-only batch on this
     rank: pack (rf_amd_batch_export), all-gather pages, slots and filter infos, import
-    (rf_amd_batch_import). Probes then use global filter ids locally."""
+    (rf_amd_batch_import). Probes then use global filter ids locally. collective_at_one: run
+    the all-gathers at world size 1 too (tests: the RCCL path on one GPU)."""
     import torch
     device = torch.device(device)
     coll = torch.device(coll_device) if coll_device is not None else device
@@ -162,7 +163,7 @@ def replicate_images(batch, world, device, dist=None, coll_device=None, engine=N
         torch.cuda.synchronize(device)
     d_pages, d_slots = d_pages[:pbytes], d_slots[:nslots]
     inf = torch.tensor([[getattr(i, k) for k in _INFO_FIELDS] for i in infos], dtype=torch.int64).reshape(-1)
-    if world == 1:
+    if world == 1 and not collective_at_one:
         parts = [(inf, d_pages, d_slots)]
     else:
         gi = _all_gather_padded(dist, inf.to(coll), world)

@@ -1,6 +1,7 @@
 """The multi-rank code path on one GPU: torch.distributed over RCCL ("nccl") with ONE rank,
 every collective run (not the one-rank shortcuts). ProbeRouter's all-to-alls (counts, probe
-pairs, found_values back) through RCCL must give the single-process probe's results, and
+pairs, found_values back) and replicate_images' all-gathers (filter infos, pages, slots, then
+an imported probe-only batch) through RCCL must give the single-process probe's results, and
 bench.py's multi-rank path (process group, barriers, max/sum over ranks, routed probes) must
 run and verify. Each check runs in a subprocess of its own (its process group, its port)."""
 import json
@@ -64,6 +65,55 @@ dist.barrier()
 dist.destroy_process_group()
 print("ROUTER_OK", P)
 """
+
+
+REPLICA = r"""
+import os, sys
+sys.path.insert(0, os.environ["RF_ROOT"])
+import numpy as np, torch, torch.distributed as dist
+from splinterdb_amd import engine as E, keys as K, route as R
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=dev)
+assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+cfg = E.routing_config_init(log_index_size=8)
+F, n = 5, 40_000
+kk = K.random_keys(F * n, seed=5)
+b = E.FilterBatch(cfg, [n] * F, [f % 8 for f in range(F)])
+b.build_keys(torch.from_numpy(kk).to(dev), 24)
+rep = R.replicate_images(b, 1, dev, dist=dist, coll_device=dev, collective_at_one=True)
+assert rep.F == F
+P = 80_000
+rng = np.random.default_rng(2)
+gfid = rng.integers(0, F, size=P).astype(np.int32)
+pk = K.random_keys(P, seed=17)
+own = rng.random(P) < 0.5
+idx = rng.integers(0, n, size=P)
+pk[own] = kk[gfid[own] * n + idx[own]]
+d_pk = torch.from_numpy(pk).to(dev)
+d_f = torch.from_numpy(gfid).to(dev)
+want = torch.zeros(P, dtype=torch.int64, device=dev)
+got = torch.zeros(P, dtype=torch.int64, device=dev)
+b.probe_keys(d_pk, 24, d_f, P, want)
+rep.probe_keys(d_pk, 24, d_f, P, got)
+torch.cuda.synchronize()
+assert torch.equal(got, want), int((got != want).sum())
+vals = torch.from_numpy((gfid % 8).astype(np.int64)).to(dev)
+assert bool(((want >> vals) & 1)[torch.from_numpy(own).to(dev)].all())
+for f in range(F):  # the imported images are the built ones, byte for byte
+    a, r = b.image(f), rep.image(f)
+    assert (a.pages == r.pages).all() and (a.slots == r.slots).all(), f
+dist.barrier()
+dist.destroy_process_group()
+print("REPLICA_OK", P)
+"""
+
+
+def test_replicated_images_all_gather_over_rccl_one_rank():
+    env = dict(os.environ, RF_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0",
+               WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", REPLICA], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "REPLICA_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
 
 
 def test_router_all_to_all_over_rccl_one_rank():

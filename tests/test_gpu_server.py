@@ -250,11 +250,12 @@ def test_device_sync_while_server_busy_is_short():
 
 
 def test_dead_server_returns_every_tag():
-    """a server that dies (here marked dead by the diagnostics hook, as a failed
-    launch or a faulted stream marks it) while threads submit tagged lookups: every tag whose
-    submit succeeded comes back exactly once, answered (rf_amd_lookup_reap) or with the error
-    (rf_amd_lookup_server_failed) -- including tickets published after `dead` was set and the
-    tickets of submitters that gave up waiting for a slot -- and every later submit fails."""
+    """a server that dies while threads submit tagged lookups (the diagnostics hook
+    stops its wave, then 2 ms later marks it dead, as a failed launch or a faulted stream marks
+    it): every tag whose submit succeeded comes back exactly once, answered (rf_amd_lookup_reap)
+    or with the error (rf_amd_lookup_server_failed) -- the tickets published in the gap, those
+    published after `dead` was set and those of submitters that gave up waiting for a slot --
+    and every later submit fails."""
     eng = E.Engine(0)  # a server killed for good: an engine of its own
     cfg = E.routing_config_init(log_index_size=8)
     rng = np.random.default_rng(11)
@@ -285,7 +286,7 @@ def test_dead_server_returns_every_tag():
     def killer():
         while submitted[0] < 2000:
             time.sleep(0.0002)
-        E._check(lib().rf_amd_diag_lookup_server_kill(eng.h, 5))
+        E._check(lib().rf_amd_diag_lookup_server_kill(eng.h, 5, 2000))
 
     got = {}
     dup = []
