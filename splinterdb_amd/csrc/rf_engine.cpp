@@ -1093,6 +1093,12 @@ static int do_build(rf_amd_batch* b, int kind, const void* in0, const uint64_t* 
   // after reading this count cannot miss a build it covers
   if (st == b->eng->stream) b->eng->builds_issued.fetch_add(1, std::memory_order_acq_rel);
   if (rc) return fail(RF_AMD_EINVAL, std::string("build launch: ") + hipGetErrorString((hipError_t)rc));
+  if (getenv("RF_AMD_DIAG_OVERFLOW") && b->d_overflow.p) {  // diagnostics: coarse buckets handed back by K4/K4m
+    uint32_t nov = 0;
+    if (hipMemcpyAsync(&nov, b->d_overflow.p, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        hipStreamSynchronize(st) == hipSuccess)
+      fprintf(stderr, "rf_amd: %u of %u coarse buckets handed back (K4b / list mode)\n", nov, b->CB);
+  }
   if (int erc = note_built(b, st)) return erc;
   b->built = true;
   b->has_entries = true;

@@ -1,14 +1,10 @@
 #!/bin/bash
-# r06 call 6: the two-stack latency tool to its natural exit after the harness buffer fix, and
-# the drop-in's GPU tests
+# r06 call 10: K4m2 diagnostics -- coarse buckets handed back per round
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r06f
+O=gpurun_out/r06j
 mkdir -p $O
-RFR_ABORT_BT=1 timeout -k 10 600 python3 tools/shim_latency.py > $O/shim_latency.json 2> $O/shim_latency.err
-rc=$?
-echo "shim_latency rc=$rc"
-grep -v UserWarning $O/shim_latency.err | grep -v "setattr\|return self" | tail -30
-[ $rc -eq 0 ] || exit 1
-timeout -k 10 900 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_shim.py tests/test_gpu_trunk.py > $O/t_shim.log 2>&1; echo "shim tests rc=$?"; tail -5 $O/t_shim.log
+cp splinterdb_amd/librf_amd.so /tmp/k4m1.so
+RF_AMD_DIAG_OVERFLOW=1 AB_R=8 AB_REPS=1 timeout -k 10 300 python3 tools/ab_chain.py /tmp/k4m1.so:RF_AMD_K4M=1 splinterdb_amd/librf_amd.so > $O/ab_r8.json 2> $O/ab_r8.err || { echo "ab failed"; tail -5 $O/ab_r8.err; exit 1; }
+cat $O/ab_r8.json; grep "handed back" $O/ab_r8.err
