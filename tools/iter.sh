@@ -1,10 +1,12 @@
 #!/bin/bash
-# r06 call 10: K4m2 diagnostics -- coarse buckets handed back per round
+# r06 call 15: probe lines v2 at the old table sizes (RF_AMD_LINE_SIGMA=5: 8 lines per index at
+# C2 and C3, no overflow walks) -- the decode's own cost
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r06j
+O=gpurun_out/r06o
 mkdir -p $O
-cp splinterdb_amd/librf_amd.so /tmp/k4m1.so
-RF_AMD_DIAG_OVERFLOW=1 AB_R=8 AB_REPS=1 timeout -k 10 300 python3 tools/ab_chain.py /tmp/k4m1.so:RF_AMD_K4M=1 splinterdb_amd/librf_amd.so > $O/ab_r8.json 2> $O/ab_r8.err || { echo "ab failed"; tail -5 $O/ab_r8.err; exit 1; }
-cat $O/ab_r8.json; grep "handed back" $O/ab_r8.err
+for W in c2 c3; do
+  RF_AMD_LINE_SIGMA=5 timeout -k 10 300 python3 bench.py --workload $W --no-cpu-baseline --no-e2e --pmc none > $O/bench_${W}_s5.json 2> $O/bench_${W}_s5.err || { echo "bench $W failed"; tail -5 $O/bench_${W}_s5.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench_${W}_s5.json')); print('$W sigma5', d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('probe_floor'))"
+done
