@@ -59,11 +59,26 @@ static int fail(int rc, const std::string& msg) {
 // its ~25 work buffers here instead of calling hipMalloc. Sizes are rounded up to classes
 // of 1/8 of a power of two (at most 12.5 % slack); a block returns to the pool when its
 // batch is destroyed unless the pool already holds RF_AMD_POOL_MIB MiB (default: a quarter
-// of the device memory free at engine creation, at most 16 GiB; rf_amd_engine_pool_trim
+// of the device memory free at engine creation; rf_amd_engine_pool_trim
 // hands blocks back).
 // rf_amd_batch_destroy synchronises the device first; rf_amd_batch_destroy_on instead
 // parks the blocks behind an event on the caller's stream (stream-ordered release, as
 // hipFreeAsync): they become reusable once that event has completed.
+// RF_AMD_POOL_TRACE=<ms>: diagnostics, every pool hipMalloc / hipFree slower than that
+static uint64_t pool_trace_ns() {
+  static const char* v = getenv("RF_AMD_POOL_TRACE");
+  if (!v) return 0;
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+static void pool_trace(const char* what, size_t bytes, uint64_t t0) {
+  if (!t0) return;
+  static const double lim = atof(getenv("RF_AMD_POOL_TRACE"));
+  const double ms = (pool_trace_ns() - t0) * 1e-6;
+  fprintf(stderr, "rf_amd pool: %s %zu B %.3f ms%s\n", what, bytes, ms, ms >= lim ? " SLOW" : "");
+}
+
 struct DevPool {
   std::mutex mu;
   std::multimap<size_t, void*> free_blocks;
@@ -82,7 +97,9 @@ struct DevPool {
   }
   void give_locked(void* p, size_t cls) {
     if (cls == 0 || pooled + cls > limit) {
+      const uint64_t t0 = pool_trace_ns();
       (void)hipFree(p);
+      pool_trace("hipFree", cls, t0);
       return;
     }
     free_blocks.emplace(cls, p);
@@ -240,7 +257,9 @@ struct DevBuf {
     pool = from;
     n = from ? DevPool::size_class(bytes ? bytes : 16) : (bytes ? bytes : 16);
     if (from && (p = from->take(&n)) != nullptr) return 0;
+    const uint64_t t0 = pool_trace_ns();
     hipError_t e = hipMalloc(&p, n);
+    pool_trace("hipMalloc", n, t0);
     if (e != hipSuccess && from) {  // the pool may hold what this needs: give it back, retry
       from->drain();
       e = hipMalloc(&p, n);
@@ -345,13 +364,16 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
   auto* e = new rf_amd_engine();
   e->device = device;
   {
-    // default: a quarter of the memory free at engine creation, at most 16 GiB (one
-    // compaction round of 64 x 8M-fingerprint filters parks ~9 GB); other allocators of the
-    // process can reclaim it with rf_amd_engine_pool_trim
+    // default: a quarter of the memory free at engine creation (~62 GB on an idle MI355X);
+    // other allocators of the process can reclaim it with rf_amd_engine_pool_trim. The
+    // compaction chain of 64 x 8M-fingerprint filters keeps 7.4 GB pooled beside the ~10 GB
+    // its last round parks; a cap below that (round 5 had 16 GiB) makes every chain free and
+    // re-allocate blocks of up to 2.7 GB, and hipFree of those costs ~28 ms per GB once the
+    // driver clears released memory (profiles/r06_pool_churn.txt)
     const char* lim = getenv("RF_AMD_POOL_MIB");
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
-    const size_t dflt = std::min<size_t>((size_t)16384 << 20, free_b / 4);
+    const size_t dflt = free_b / 4;
     e->pool.limit = lim ? (size_t)atoll(lim) << 20 : dflt;
   }
   // a BLOCKING stream: ordered with the legacy null stream that torch and most callers use
@@ -595,10 +617,18 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       const FilterPlan* op = olds[f].second;
       if (!op) continue;
       FilterPlan& p = b->plans[f];
-      if (direct_ok && ob->has_entries && op->lnb == p.lnb && op->cbits == p.cbits &&
-          ob->cfg.fingerprint_size == fps && ob->cfg.log_index_size == lis) {
+      // in place also across a geometry change (lnb grew: rounds 2, 3 and 5 of the compaction
+      // chain), as long as each new coarse bucket lies inside one old one (cbits did not shrink)
+      // (RF_AMD_OLD_RESPLIT_OFF: decode those, for A/B)
+      const bool same_cfg = direct_ok && ob->has_entries && ob->cfg.fingerprint_size == fps &&
+                            ob->cfg.log_index_size == lis;
+      const bool same_geo = op->lnb == p.lnb && op->cbits == p.cbits;
+      const bool resplit = p.cbits >= op->cbits && p.lnb >= op->lnb && getenv("RF_AMD_OLD_RESPLIT_OFF") == nullptr;
+      if (same_cfg && (same_geo || resplit)) {
         const uint32_t* es = ob->wide ? ob->d_sorted.as<uint32_t>() : ob->d_part.as<uint32_t>();
         p.old_direct = 1;
+        p.old_cbits = op->cbits;
+        p.old_bbits = op->bbits;
         p.old_entries = es + op->e_first;
         p.old_idx_start = ob->d_idx_start.as<uint32_t>() + op->idx_base;
         p.old_idx_cnt = ob->d_idx_cnt.as<uint32_t>() + op->idx_base;
@@ -632,6 +662,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
   const size_t esz = (b->wide && !b->flag32) ? 8 : 4;
   int rc = 0;
   DevPool* pool = &e->pool;
+  const uint64_t ta0 = pool_trace_ns();
   rc |= b->d_plans.alloc(sizeof(FilterPlan) * num_filters, pool);
   rc |= b->d_pplans.alloc(16ull * num_filters, pool);
   rc |= b->d_outs.alloc(sizeof(FilterOut) * num_filters, pool);
@@ -672,6 +703,7 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       rc |= b->d_ob_n.alloc(4 * b->CB, pool);
     }
   }
+  pool_trace("create allocs", 0, ta0);
   if (rc) {
     delete b;
     return fail(RF_AMD_ENOMEM, "device allocation failed");
@@ -725,7 +757,9 @@ extern "C" int rf_amd_batch_create(rf_amd_engine* e, const rf_amd_config* cfg, u
       }
     }
   }
+  const uint64_t ts0 = pool_trace_ns();
   HIPCHK(hipStreamSynchronize(st));
+  pool_trace("create sync", 0, ts0);
   *out = b;
   return 0;
 }

@@ -2368,11 +2368,29 @@ __global__ __launch_bounds__(256) void k_old_cb_bounds(const FilterPlan* __restr
   const FilterPlan& P = plans[f];
   const uint32_t cl = cb - P.cb_base, ncb = 1u << P.cbits;
   if (P.old_direct) {
-    // the old filter has this geometry: new coarse bucket cl is its coarse bucket cl, whose
-    // entries are those of its indices [cl * ipc, (cl + 1) * ipc), consecutive in its entry
-    // array (K4 compacts a coarse bucket's indices in order)
-    const uint32_t ipc = 1u << (P.bbits - lis), i0 = cl * ipc, i1 = i0 + ipc - 1;
-    const uint32_t lo = P.old_idx_start[i0], hi = P.old_idx_start[i1] + P.old_idx_cnt[i1];
+    // new coarse bucket cl lies in the old filter's coarse bucket cl >> (cbits - old_cbits), whose
+    // entries are those of its indices [c_old * ipc, (c_old + 1) * ipc), consecutive in its entry
+    // array (K4 compacts a coarse bucket's indices in order); with the same geometry that is the
+    // run, else the run is the sub-range of entries in cl (binary searches: the entries are sorted
+    // by fingerprint, and re-widening the value bits keeps their order)
+    const uint32_t c_old = cl >> (P.cbits - P.old_cbits);
+    const uint32_t ipc = 1u << (P.old_bbits - lis), i0 = c_old * ipc, i1 = i0 + ipc - 1;
+    uint32_t lo = P.old_idx_start[i0], hi = P.old_idx_start[i1] + P.old_idx_cnt[i1];
+    if (P.cbits != P.old_cbits) {
+      const uint32_t* o = P.old_entries;
+      const uint32_t ovs = P.old_vs, vs = P.vs, esh = fp_size + vs - P.cbits;
+      auto key = [&](uint32_t raw) -> uint32_t { return (((raw >> ovs) << vs) | (raw & ((1u << ovs) - 1u))) >> esh; };
+      auto lb = [&](uint32_t c, uint32_t a, uint32_t b) -> uint32_t {  // first entry in [a, b) of coarse bucket >= c
+        while (a < b) {
+          const uint32_t mid = (a + b) >> 1;
+          if (key(o[mid]) < c) a = mid + 1; else b = mid;
+        }
+        return a;
+      };
+      const uint32_t nlo = lb(cl, lo, hi);
+      hi = lb(cl + 1, nlo, hi);
+      lo = nlo;
+    }
     ob_lo[cb] = lo;
     ob_n[cb] = hi - lo;
     cb_count[cb] += hi - lo;

@@ -64,11 +64,15 @@ struct FilterPlan {
                           // are flagged in pg_noline and k_plines cuts their indices' lines
   const uint8_t* old_pages;
   const uint64_t* old_slots;
-  // 32-bit incremental builds whose old filter was built by this engine with the same
-  // geometry (lnb, coarse buckets): its entries are read in place from the old batch's
-  // sorted entry array (old_entries, old_idx_start / old_idx_cnt relative to it) -- no
-  // decode of its image. Value bits are re-widened (old_vs -> vs) as K4 loads them.
+  // 32-bit incremental builds whose old filter was built by this engine: its entries are read
+  // in place from the old batch's sorted entry array (old_entries, old_idx_start / old_idx_cnt
+  // relative to it) -- no decode of its image. Value bits are re-widened (old_vs -> vs) as K4
+  // loads them. The old filter may have fewer coarse buckets (old_cbits <= cbits: a chain round
+  // whose num_fingerprints crossed a power of two): each new coarse bucket's run is then a
+  // sub-range of one old coarse bucket's, found by binary search (entries are sorted by
+  // fingerprint in either geometry).
   uint32_t old_direct;
+  uint32_t old_cbits, old_bbits;
   const uint32_t* old_entries;
   const uint32_t* old_idx_start;
   const uint32_t* old_idx_cnt;
