@@ -142,17 +142,20 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
-def e2e_duplex(eng, cfg, stream, keys, found, batch, h_keys, counts, infos, n, F, N, P, reps=6):
+def e2e_duplex(eng, cfg, stream, ins, h_ins, compute, found, batch, infos, n, F, N, P, found_ok, reps=6):
     """PCIe-inclusive rate of a stream of `reps` batches with two in flight (full duplex):
-    keys H2D on a copy-in stream, build + probe on `stream`, found_values + page images +
-    index slots D2H on a copy-out stream, every buffer double-buffered. Returns (Mkeys/s of
-    this rank, every key found in the last results)."""
-    dev = keys.device
+    inputs H2D on a copy-in stream, build + probe on `stream`, found_values + page images +
+    index slots D2H on a copy-out stream, every buffer double-buffered. `ins` are the device
+    input tensors (keys; or C5's key bytes, offsets, probe bytes, offsets and filter ids),
+    `h_ins` their pinned host sources, compute(batch, ins, found) issues one build + probe on
+    `stream`, found_ok(host found) checks the results. Returns (Mkeys/s of this rank, the
+    results checked and both batches' images equal)."""
+    dev = found.device
     s_in, s_out = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
-    keys2 = torch.empty_like(keys)
-    found2 = torch.empty_like(found)
+    ib = [list(ins), [torch.empty_like(x) for x in ins]]
+    fb = [found, torch.empty_like(found)]
     batch2 = E.FilterBatch(cfg, [n] * F, engine=eng)
-    kb, fb, bb = [keys, keys2], [found, found2], [batch, batch2]
+    bb = [batch, batch2]
     hf = [torch.empty(P, dtype=torch.int64).pin_memory() for _ in range(2)]
     hp = [[torch.empty(i.num_pages * cfg.page_size, dtype=torch.uint8).pin_memory() for i in infos] for _ in range(2)]
     hs = [[torch.empty(i.num_indices, dtype=torch.int64).pin_memory() for i in infos] for _ in range(2)]
@@ -163,15 +166,15 @@ def e2e_duplex(eng, cfg, stream, keys, found, batch, h_keys, counts, infos, n, F
     def one(r):
         s = r % 2
         if r >= 2:
-            s_in.wait_event(ev_comp[s])  # batch r-2 read keys[s]
+            s_in.wait_event(ev_comp[s])  # batch r-2 read these inputs
         with torch.cuda.stream(s_in):
-            kb[s].view(-1).copy_(h_keys, non_blocking=True)
+            for d, h in zip(ib[s], h_ins):
+                d.view(-1).copy_(h.view(-1), non_blocking=True)
         ev_in[s].record(s_in)
         stream.wait_event(ev_in[s])
         if r >= 2:
             stream.wait_event(ev_out[s])  # batch r-2's results and images have left
-        bb[s].build_keys(kb[s], 24, stream=stream.cuda_stream)
-        bb[s].probe_keys_runs(kb[s], 24, counts, fb[s], stream=stream.cuda_stream)
+        compute(bb[s], ib[s], fb[s])
         ev_comp[s].record(stream)
         s_out.wait_event(ev_comp[s])
         with torch.cuda.stream(s_out):
@@ -188,7 +191,7 @@ def e2e_duplex(eng, cfg, stream, keys, found, batch, h_keys, counts, infos, n, F
         one(r)
     torch.cuda.synchronize()
     rate = N * reps / (time.perf_counter() - te) / 1e6
-    ok = all(bool(((hf[s] & 1) == 1).all().item()) for s in range(2))
+    ok = all(found_ok(hf[s]) for s in range(2))
     # both batches' images equal (the same keys)
     ok = ok and all(torch.equal(hp[0][f], hp[1][f]) and torch.equal(hs[0][f], hs[1][f]) for f in range(F))
     batch2.close()
@@ -398,14 +401,30 @@ def main():
             ok_e2e = bool(((hfound & 1) == 1).all().item())
         verified = verified and ok_e2e
         e2e = e2e_serial
-        if not var:
-            # full duplex: a stream of batches, two in flight -- batch r+1's keys cross PCIe
-            # host->device (copy-in stream) while batch r's results and images cross
-            # device->host (copy-out stream) and the GPU builds and probes in between; keys,
-            # results, images and the filter batch are double-buffered
-            e2e, ok_dup = e2e_duplex(eng, cfg, stream, keys, found, batch, h_in[0][1], counts, infos, n, F, N, P)
-            e2e = S.sum_over_ranks(e2e, dist, coll_dev)
-            verified = verified and ok_dup
+        # full duplex: a stream of batches, two in flight -- batch r+1's keys cross PCIe
+        # host->device (copy-in stream) while batch r's results and images cross
+        # device->host (copy-out stream) and the GPU builds and probes in between; inputs,
+        # results, images and the filter batch are double-buffered
+        if var:
+            pos = torch.from_numpy(w["positive"])
+
+            def compute(b, ins, fo):
+                b.build_var_keys(ins[0], ins[1], stream=stream.cuda_stream)
+                b.probe_var_keys(ins[2], ins[3], ins[4], P, fo, stream=stream.cuda_stream)
+
+            def found_ok(hf):
+                return bool(((hf[pos] & 1) == 1).all().item())
+        else:
+            def compute(b, ins, fo):
+                b.build_keys(ins[0], 24, stream=stream.cuda_stream)
+                b.probe_keys_runs(ins[0], 24, counts, fo, stream=stream.cuda_stream)
+
+            def found_ok(hf):
+                return bool(((hf & 1) == 1).all().item())
+        e2e, ok_dup = e2e_duplex(eng, cfg, stream, [d for d, _ in h_in], [h for _, h in h_in], compute, found,
+                                 batch, infos, n, F, N, P, found_ok)
+        e2e = S.sum_over_ranks(e2e, dist, coll_dev)
+        verified = verified and ok_dup
         if not var:
             # the drop-in interface itself takes fingerprints, not keys (routing_filter_add's
             # new_fp_arr; btree_pack hashes on the host): 4 B/key H2D instead of 24

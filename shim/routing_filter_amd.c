@@ -77,6 +77,8 @@
 #include "platform_typed_alloc.h"
 
 #include <pthread.h>
+#include <sched.h>
+#include <x86intrin.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1561,14 +1563,20 @@ static char g_queued_marker;
 #define ASYNC_STATE_QUEUED ((async_state)&g_queued_marker)
 typedef routing_filter_lookup_async_state rf_state;
 
-static uint64          g_aq_outstanding; /* submitted, not yet completed (atomic) */
-static int             g_aq_sleeping;    /* the completion thread waits on g_aq_cv (atomic) */
-static pthread_mutex_t g_aq_mu = PTHREAD_MUTEX_INITIALIZER;
+/* The submitting threads and the completion thread run on different cores: what each side
+ * writes sits on 128-byte blocks of its own (a written line moving between the host's CCDs
+ * costs ~300 ns; profiles/r06_async_submit.txt) */
+#define SHIM_LINE __attribute__((aligned(128)))
+/* submitted, not yet completed (atomic; the completion thread subtracts once per reap) */
+static uint64 g_aq_outstanding SHIM_LINE;
+static uint64 g_async_submit_ns; /* ns spent submitting: hash, pin, ring (submitters) */
+static int    g_aq_sleeping SHIM_LINE; /* the completion thread waits on g_aq_cv (atomic) */
+static pthread_mutex_t g_aq_mu SHIM_LINE = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t  g_aq_cv = PTHREAD_COND_INITIALIZER;
 static pthread_once_t  g_aq_once = PTHREAD_ONCE_INIT;
-/* reaps that returned states, states completed, and ns spent submitting (hash, pin, ring),
- * reaping and firing callbacks (routing_filter_amd_async_breakdown) */
-static uint64          g_async_batches, g_async_probes, g_async_submit_ns, g_async_reap_ns, g_async_cb_ns;
+/* reaps that returned states, states completed, ns spent reaping and firing callbacks
+ * (routing_filter_amd_async_breakdown; the completion thread's) */
+static uint64 g_async_batches SHIM_LINE, g_async_probes, g_async_reap_ns, g_async_cb_ns;
 
 #define AQ_PIN(st) (*(shim_batch **)&(st)->filter_page)
 
@@ -1665,7 +1673,7 @@ bq_complete(void)
 #define SHIM_THREADS_MAX 9
 static pthread_t g_threads[SHIM_THREADS_MAX];
 static uint32    g_nthreads;
-static int       g_stopping; /* atomic: the threads leave their loops */
+static int       g_stopping SHIM_LINE; /* atomic: the threads leave their loops */
 
 static void *
 batch_main(void *arg)
@@ -1717,9 +1725,13 @@ async_reap_complete(void)
    uint64       n  = rf_amd_lookup_reap(engine(), tags, found, REAP);
    if (n == 0) {
       /* a dead lookup server (a launch failed, its stream faulted) never answers: complete
-         its states with the error instead of leaving their owners waiting */
-      const int err = __atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE) ? rf_amd_lookup_server_error(engine()) : 0;
-      uint64    k   = err ? rf_amd_lookup_server_failed(engine(), tags, REAP) : 0;
+         its states with the error instead of leaving their owners waiting. The
+         server's sticky error word is read first: it is read-mostly, the outstanding count is
+         written by every submit */
+      const int err = rf_amd_lookup_server_error(engine());
+      uint64    k   = err && __atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE)
+                         ? rf_amd_lookup_server_failed(engine(), tags, REAP)
+                         : 0;
       for (uint64 i = 0; i < k; i++) {
          rf_state         *st  = tags[i];
          async_callback_fn cb  = st->callback;
@@ -1737,7 +1749,9 @@ async_reap_complete(void)
       return k;
    }
    const uint64 t1 = now_ns();
-   shim_batch  *pins[REAP];
+   shim_batch       *pins[REAP];
+   async_callback_fn cbs[REAP];
+   void             *args[REAP];
    for (uint64 i = 0; i < n && i < 4; i++) {
       __builtin_prefetch(tags[i], 1, 3);
    }
@@ -1745,17 +1759,21 @@ async_reap_complete(void)
       if (i + 4 < n) {
          __builtin_prefetch(tags[i + 4], 1, 3); /* the owners' states: misses overlapped */
       }
-      rf_state         *st  = tags[i];
-      async_callback_fn cb  = st->callback;
-      void             *arg = st->callback_arg;
-      pins[i]               = AQ_PIN(st);
-      *st->found_values     = found[i];
-      st->__async_result    = STATUS_OK;
+      rf_state *st       = tags[i];
+      cbs[i]             = st->callback;
+      args[i]            = st->callback_arg;
+      pins[i]            = AQ_PIN(st);
+      *st->found_values  = found[i];
+      st->__async_result = STATUS_OK;
       /* from here the owner may resume (and reuse) the state: it is not touched again */
       __atomic_store_n(&st->__async_state_stack[0], ASYNC_STATE_DONE, __ATOMIC_RELEASE);
-      __atomic_sub_fetch(&g_aq_outstanding, 1, __ATOMIC_RELAXED);
-      if (cb) {
-         cb(arg);
+   }
+   /* one update of the shared count per reap, before the callbacks (a callback that submits
+      and finds the ring nearly full reaps in place: the count must not hold these) */
+   __atomic_sub_fetch(&g_aq_outstanding, n, __ATOMIC_RELEASE);
+   for (uint64 i = 0; i < n; i++) {
+      if (cbs[i]) {
+         cbs[i](args[i]);
       }
    }
    registry_unpin_many(pins, n); /* the batches stay pinned until their answers are stored */
@@ -1771,12 +1789,16 @@ completion_main(void *arg)
 {
    (void)arg;
    platform_ensure_thread_registered(); /* callbacks and cache_get (imports) run here */
+   uint32 idle = 0;
    while (!__atomic_load_n(&g_stopping, __ATOMIC_SEQ_CST)) {
       if (async_reap_complete()) {
+         idle = 0;
          continue;
       }
-      if (__atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE)) {
-         __builtin_ia32_pause(); /* answers arrive within microseconds */
+      /* answers arrive within microseconds: spin on the reap (it reads only the GPU-written
+         answer line while idle) and look at the submitters' count only every 64 spins */
+      if ((++idle & 63) != 0 || __atomic_load_n(&g_aq_outstanding, __ATOMIC_ACQUIRE)) {
+         __builtin_ia32_pause();
          continue;
       }
       pthread_mutex_lock(&g_aq_mu);
@@ -1790,9 +1812,79 @@ completion_main(void *arg)
    return NULL;
 }
 
+/* RF_SHIM_PIN_THREADS (default 1): the completion and batch threads run on the cores that
+ * share the last-level cache with the thread that made the first async call. Every answered
+ * state moves cache lines between that thread and the completion thread (the state, its
+ * callback's context, the ring bookkeeping); between the host's CCDs such a move costs ~300 ns,
+ * within one a fraction of it. Nothing is pinned when the process's allowed cores do not
+ * include two of that cache's cores. */
+static void
+pin_near_caller(const pthread_t *th, uint32 n)
+{
+   if (!env_u64("RF_SHIM_PIN_THREADS", 1)) {
+      return;
+   }
+   const int cpu = sched_getcpu();
+   if (cpu < 0) {
+      return;
+   }
+   char path[160], buf[1024];
+   int  lvl = 0;
+   snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/level", cpu);
+   FILE *f = fopen(path, "r");
+   if (!f) {
+      return;
+   }
+   if (fscanf(f, "%d", &lvl) != 1) {
+      lvl = 0;
+   }
+   fclose(f);
+   if (lvl != 3) {
+      return;
+   }
+   snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+   f = fopen(path, "r");
+   if (!f) {
+      return;
+   }
+   const char *ok = fgets(buf, sizeof(buf), f);
+   fclose(f);
+   if (!ok) {
+      return;
+   }
+   cpu_set_t llc, allowed;
+   CPU_ZERO(&llc);
+   for (char *p = buf; *p && *p != '\n';) { /* "a-b,c,..." */
+      char *e;
+      long  a = strtol(p, &e, 10), b = a;
+      if (e == p) {
+         break;
+      }
+      if (*e == '-') {
+         p = e + 1;
+         b = strtol(p, &e, 10);
+      }
+      for (long c = a; c <= b && c < CPU_SETSIZE; c++) {
+         CPU_SET(c, &llc);
+      }
+      p = (*e == ',') ? e + 1 : e;
+   }
+   if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) {
+      return;
+   }
+   CPU_AND(&llc, &llc, &allowed);
+   if (CPU_COUNT(&llc) < 2) {
+      return;
+   }
+   for (uint32 i = 0; i < n; i++) {
+      (void)pthread_setaffinity_np(th[i], sizeof(llc), &llc);
+   }
+}
+
 static void
 aq_init(void)
 {
+   const uint32 first = g_nthreads;
    platform_assert(pthread_create(&g_threads[g_nthreads++], NULL, completion_main, NULL) == 0);
    /* RF_SHIM_BATCH_THREADS batch threads (default 1; 2: a batch goes out while the previous
       one is on the GPU) */
@@ -1800,6 +1892,7 @@ aq_init(void)
    for (uint64 k = 0; k < (nb >= 1 && nb <= SHIM_THREADS_MAX - 1 ? nb : 1); k++) {
       platform_assert(pthread_create(&g_threads[g_nthreads++], NULL, batch_main, NULL) == 0);
    }
+   pin_near_caller(&g_threads[first], g_nthreads - first);
 }
 
 /* Process exit (atexit, registered when the engine was created): the completion and batch
@@ -1875,9 +1968,48 @@ routing_filter_amd_async_probe_ns(void)
    return __atomic_load_n(&g_async_reap_ns, __ATOMIC_RELAXED) + __atomic_load_n(&g_bq_ns, __ATOMIC_RELAXED);
 }
 
+/* RF_SHIM_SUBMIT_PROFILE=1 (diagnostics): TSC cycles of each step of a server submission --
+   hash, registry pin, ring-space wait and bookkeeping, rf_amd_lookup_submit, wake-up -- summed
+   and printed to stderr at exit */
+static int    g_subprof = -1;
+static uint64 g_subprof_cyc[5], g_subprof_n;
+#define SUBPROF_MARK(i)                                                                            \
+   uint64 sp_##i = 0;                                                                              \
+   if (g_subprof > 0) {                                                                            \
+      sp_##i = __rdtsc();                                                                          \
+   }
+#define SUBPROF_DONE()                                                                             \
+   if (g_subprof > 0) {                                                                            \
+      g_subprof_cyc[0] += sp_1 - sp_0;                                                             \
+      g_subprof_cyc[1] += sp_2 - sp_1;                                                             \
+      g_subprof_cyc[2] += sp_3 - sp_2;                                                             \
+      g_subprof_cyc[3] += sp_4 - sp_3;                                                             \
+      g_subprof_cyc[4] += sp_5 - sp_4;                                                             \
+      g_subprof_n++;                                                                               \
+   }
+static void
+subprof_print(void)
+{
+   if (g_subprof > 0 && g_subprof_n) {
+      fprintf(stderr,
+              "rf_shim submit profile: %lu submissions, TSC cycles each: hash %.0f pin %.0f "
+              "wait+book %.0f submit %.0f wake %.0f\n",
+              (unsigned long)g_subprof_n, (double)g_subprof_cyc[0] / g_subprof_n,
+              (double)g_subprof_cyc[1] / g_subprof_n, (double)g_subprof_cyc[2] / g_subprof_n,
+              (double)g_subprof_cyc[3] / g_subprof_n, (double)g_subprof_cyc[4] / g_subprof_n);
+   }
+}
+
 async_status
 routing_filter_lookup_async(routing_filter_lookup_async_state *state)
 {
+   if (g_subprof < 0) {
+      const char *v = getenv("RF_SHIM_SUBMIT_PROFILE");
+      g_subprof     = v && atoi(v) > 0;
+      if (g_subprof) {
+         atexit(subprof_print);
+      }
+   }
    async_state at = __atomic_load_n(&state->__async_state_stack[0], __ATOMIC_ACQUIRE);
    if (at == ASYNC_STATE_DONE) {
       return ASYNC_STATUS_DONE;
@@ -1901,7 +2033,9 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    }
    pthread_once(&g_aq_once, aq_init);
    const uint64 t0 = now_ns();
+   SUBPROF_MARK(0);
    state->fp       = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
+   SUBPROF_MARK(1);
    if (__atomic_load_n(&g_aq_outstanding, __ATOMIC_RELAXED) >= AQ_SERVER_MAX
        || __atomic_load_n(&g_bq_pending, __ATOMIC_RELAXED))
    {
@@ -1925,6 +2059,7 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    shim_batch     *sb;
    uint32          fi;
    platform_status rc = resident_pin(state->cc, state->cfg, &state->filter, &sb, &fi);
+   SUBPROF_MARK(2);
    if (!SUCCESS(rc)) {
       *state->found_values          = 0;
       state->__async_result         = rc;
@@ -1942,7 +2077,9 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    state->__async_state_stack[0] = ASYNC_STATE_QUEUED;
    __atomic_add_fetch(&g_aq_outstanding, 1, __ATOMIC_SEQ_CST);
    uint64 ticket;
+   SUBPROF_MARK(3);
    int    r = rf_amd_lookup_submit(engine(), sb->b, fi, state->fp, state, &ticket);
+   SUBPROF_MARK(4);
    if (r) { /* not queued: nobody else saw the state */
       __atomic_sub_fetch(&g_aq_outstanding, 1, __ATOMIC_SEQ_CST);
       registry_unpin(sb);
@@ -1958,6 +2095,8 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
       pthread_cond_signal(&g_aq_cv);
       pthread_mutex_unlock(&g_aq_mu);
    }
+   SUBPROF_MARK(5);
+   SUBPROF_DONE();
    return ASYNC_STATUS_RUNNING;
 }
 

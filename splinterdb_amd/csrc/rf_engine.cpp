@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <x86intrin.h>
 
 #include <map>
 #include <atomic>
@@ -186,6 +187,12 @@ struct ProbeSlot {
 
 // The engine's lookup server (k_lookup_server): rings in pinned coherent host memory, the
 // persistent kernel's generation and state, and the host-side bookkeeping of tickets.
+// Submitting threads and the reaping thread run on different cores (often different CCDs of
+// the host, where moving a written cache line costs ~300 ns), so the words each side writes
+// sit on lines of their own: the submitters' ticket counter, the reaper's lock and cursor, and
+// the read-mostly server state each get a 128-byte block (round 5 had them on one line, and a
+// reaper spinning on its lock cost each submit several such transfers: 0.7 us per submit,
+// profiles/r06_async_submit.txt).
 struct LookupServer {
   std::once_flag once;
   int init_rc = 0;
@@ -193,28 +200,34 @@ struct LookupServer {
   SrvRes* res = nullptr;
   SrvCtl* ctl = nullptr;
   hipStream_t st = nullptr;             // its own HSA queue (CU-masked), so it never blocks other work
-  // per slot, host-only (the reaper never reads the request ring, whose lines the GPU polls):
-  // the slot's ticket (published after the tag) and the submitter's tag (NULL: a waiter's)
-  struct Meta {
-    std::atomic<uint64_t> ticket{~0ull};
-    void* tag = nullptr;
-  };
-  Meta meta[SRV_RING];
-  std::atomic<uint64_t> consumed[SRV_RING];  // per slot: 1 + the last ticket whose result was taken
-  // per slot: a ticket whose submitter gave up before publishing it (the server died while it
-  // waited for the slot): the reap and failure cursors step over it instead of waiting on it
-  std::atomic<uint64_t> abandoned[SRV_RING];
-  std::atomic<uint64_t> last_check_ns{0};  // the reaper's last look at the server stream
-  std::atomic<uint64_t> tail{0};        // the next ticket
-  std::atomic<uint64_t> state{0};       // generation << 1 | running
-  std::mutex reap_mu;
-  uint64_t reap_next = 0;               // the next ticket reap() looks at (under reap_mu)
-  std::atomic<uint64_t> launches{0};
   std::atomic<uint64_t> idle_ticks{0}, life_ticks{0};  // of the next launch (rf_amd_lookup_server_set_times)
+  std::atomic<bool> ready{false};  // rings allocated and initialised (srv_init done)
+  // read-mostly: written when a server is launched or fails
+  alignas(128) std::atomic<uint64_t> state{0};  // generation << 1 | running
+  std::atomic<uint64_t> launches{0};
   // sticky: the first error of the server (a launch that failed, a faulted stream). Every
   // waiter then returns it, submits fail at once, and rf_amd_lookup_server_failed hands the
   // unanswered tickets' tags back, so no caller spins on an answer that cannot come
   std::atomic<int> dead{0};
+  // the submitters'
+  alignas(128) std::atomic<uint64_t> tail{0};  // the next ticket
+  // the reaper's
+  alignas(128) std::mutex reap_mu;
+  uint64_t reap_next = 0;                      // the next ticket reap() looks at (under reap_mu)
+  std::atomic<uint64_t> reap_hint{0};          // reap_next, for the lock-free look of an idle reap
+  std::atomic<uint64_t> last_check_ns{0};      // the reaper's last look at the server stream
+  // per slot, host-only: the slot's ticket (published after the tag) and the submitter's tag
+  // (NULL: a waiter's) -- read by rf_amd_lookup_server_failed (tags of tickets a dead server
+  // never answered) and by the next submitter of the slot; the reaper reads answer lines only
+  struct Meta {
+    std::atomic<uint64_t> ticket{~0ull};
+    void* tag = nullptr;
+  };
+  alignas(128) Meta meta[SRV_RING];
+  std::atomic<uint64_t> consumed[SRV_RING];  // per slot: 1 + the last ticket whose result was taken
+  // per slot: a ticket whose submitter gave up before publishing it (the server died while it
+  // waited for the slot): the reap and failure cursors step over it instead of waiting on it
+  std::atomic<uint64_t> abandoned[SRV_RING];
 };
 
 struct rf_amd_engine {
@@ -1375,6 +1388,9 @@ static_assert(SRV_RING == RF_AMD_SERVER_RING, "rf_amd.h and the kernels agree on
 
 static int srv_init(rf_amd_engine* e) {
   LookupServer& v = e->srv;
+  // once initialised, one load (std::call_once's own fast path measured ~900 TSC cycles per
+  // submit, profiles/r06_async_submit.txt)
+  if (v.ready.load(std::memory_order_acquire)) return 0;
   std::call_once(v.once, [&] {
     if (hipSetDevice(e->device) != hipSuccess ||
         hipHostMalloc((void**)&v.ring, sizeof(SrvReq) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
@@ -1408,6 +1424,7 @@ static int srv_init(rf_amd_engine* e) {
     const char* life = getenv("RF_AMD_SERVER_LIFE_US");
     if (!v.idle_ticks.load()) v.idle_ticks = (idle ? strtoull(idle, nullptr, 10) : 400) * 100;
     if (!v.life_ticks.load()) v.life_ticks = (life ? strtoull(life, nullptr, 10) : 800) * 100;
+    v.ready.store(true, std::memory_order_release);  // reapers on other threads may look now
   });
   return v.init_rc ? fail(v.init_rc, "lookup server allocation failed") : 0;
 }
@@ -1441,6 +1458,7 @@ static int srv_ensure(rf_amd_engine* e) {
 static void srv_stop(rf_amd_engine* e) {
   LookupServer& v = e->srv;
   if (!v.ctl || !v.st) return;
+  v.ready.store(false, std::memory_order_release);
   __atomic_store_n(&v.ctl->stop, 1ull, __ATOMIC_RELEASE);
   (void)hipStreamSynchronize(v.st);
   (void)hipStreamDestroy(v.st);
@@ -1496,20 +1514,54 @@ static int srv_dead(rf_amd_engine* e) {
 static ProbeGroup probe_group_of(const rf_amd_batch* b, uint32_t f);
 static int batch_errors(rf_amd_batch* b);
 
+// RF_AMD_SUBMIT_PROFILE=1 (diagnostics): TSC cycles of the steps of rf_amd_lookup_submit --
+// checks, ticket + slot wait, request write, server check -- printed to stderr at exit
+static int g_subprof = -1;
+static uint64_t g_subprof_cyc[7], g_subprof_n;
+static void subprof_print() {
+  if (g_subprof_n)
+    fprintf(stderr, "rf_amd submit profile: %llu submissions, TSC cycles each: checks %.0f (args %.0f init %.0f "
+            "errors %.0f) ticket %.0f write %.0f ensure %.0f\n",
+            (unsigned long long)g_subprof_n, (double)g_subprof_cyc[0] / g_subprof_n, (double)g_subprof_cyc[4] / g_subprof_n,
+            (double)g_subprof_cyc[5] / g_subprof_n, (double)g_subprof_cyc[6] / g_subprof_n,
+            (double)g_subprof_cyc[1] / g_subprof_n, (double)g_subprof_cyc[2] / g_subprof_n,
+            (double)g_subprof_cyc[3] / g_subprof_n);
+}
+
 extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t filter_index, uint32_t hash,
                                     void* tag, uint64_t* ticket) {
+  if (g_subprof < 0) {
+    const char* pv = getenv("RF_AMD_SUBMIT_PROFILE");
+    g_subprof = pv && atoi(pv) > 0;
+    if (g_subprof) atexit(subprof_print);
+  }
+  const uint64_t c0 = g_subprof > 0 ? __rdtsc() : 0;
   if (!e) return fail(RF_AMD_ENODEV, "no engine");
   if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "lookup on an unbuilt or foreign batch");
   if (filter_index >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
   if (!ticket) return fail(RF_AMD_EINVAL, "null ticket");
+  const uint64_t c0a = g_subprof > 0 ? __rdtsc() : 0;
   if (int rc = srv_init(e)) return rc;
+  const uint64_t c0b = g_subprof > 0 ? __rdtsc() : 0;
   if (int rc = batch_errors(b)) return rc;
+  const uint64_t c0c = g_subprof > 0 ? __rdtsc() : 0;
   if (int rc = srv_dead(e)) return rc;
   LookupServer& v = e->srv;
+  const uint64_t c1 = g_subprof > 0 ? __rdtsc() : 0;
   const uint64_t t = v.tail.fetch_add(1, std::memory_order_acq_rel);
   const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
-  if (t >= SRV_RING) {  // the slot's previous ticket must have been taken
-    for (uint32_t spin = 1; v.consumed[slot].load(std::memory_order_acquire) != t - SRV_RING + 1; spin++) {
+  if (t >= SRV_RING) {
+    // the slot's previous ticket p must have been taken: by the reaper (a tagged ticket: the
+    // reap cursor passed it, having copied its answer out), by its waiter (consumed), or never
+    // published (abandoned)
+    const uint64_t p = t - SRV_RING;
+    auto taken = [&] {
+      if (v.consumed[slot].load(std::memory_order_acquire) == p + 1) return true;
+      if (v.reap_hint.load(std::memory_order_acquire) <= p) return false;
+      if (v.abandoned[slot].load(std::memory_order_acquire) == p) return true;
+      return v.meta[slot].ticket.load(std::memory_order_acquire) == p && v.meta[slot].tag != nullptr;
+    };
+    for (uint32_t spin = 1; !taken(); spin++) {
       __builtin_ia32_pause();
       if ((spin & 1023) == 0) {  // ticket t stays unpublished only on a server that is dead
         int rc = srv_ensure(e);
@@ -1526,23 +1578,37 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     v.meta[slot].ticket.store(SRV_BUSY, std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_release);  // BUSY before the new tag (a seqlock)
   }
+  const uint64_t c2 = g_subprof > 0 ? __rdtsc() : 0;
   SrvReq& q = v.ring[slot];
   q.g = probe_group_of(b, filter_index);
   q.h = hash;
   q.pad = tag ? 0u : 1u;  // 1: a waiter's ticket (rf_amd_lookup_wait takes its result)
+  q.tag = (uint64_t)(uintptr_t)tag;
   v.meta[slot].tag = tag;
   v.meta[slot].ticket.store(t, std::memory_order_release);
   __atomic_store_n(&q.ticket, t, __ATOMIC_RELEASE);
   *ticket = t;
+  const uint64_t c3 = g_subprof > 0 ? __rdtsc() : 0;
   // published: from here the ticket's tag comes back through rf_amd_lookup_reap or, if the
   // server is (or now becomes) dead, rf_amd_lookup_server_failed -- so a launch failure here is
   // not the submit's error (the caller would complete the state a second time)
   (void)srv_ensure(e);
+  if (g_subprof > 0) {  // one submitting thread in the profiled runs: plain sums
+    const uint64_t c4 = __rdtsc();
+    g_subprof_cyc[0] += c1 - c0;
+    g_subprof_cyc[4] += c0a - c0;
+    g_subprof_cyc[5] += c0b - c0a;
+    g_subprof_cyc[6] += c0c - c0b;
+    g_subprof_cyc[1] += c2 - c1;
+    g_subprof_cyc[2] += c3 - c2;
+    g_subprof_cyc[3] += c4 - c3;
+    g_subprof_n++;
+  }
   return 0;
 }
 
 extern "C" int rf_amd_lookup_wait(rf_amd_engine* e, uint64_t ticket, uint64_t* found_values) {
-  if (!e || !e->srv.ring) return fail(RF_AMD_EINVAL, "no lookup server");
+  if (!e || !e->srv.ready.load(std::memory_order_acquire)) return fail(RF_AMD_EINVAL, "no lookup server");
   LookupServer& v = e->srv;
   const uint32_t slot = (uint32_t)(ticket & (SRV_RING - 1));
   for (uint32_t spin = 1;; spin++) {
@@ -1562,50 +1628,57 @@ extern "C" int rf_amd_lookup_wait(rf_amd_engine* e, uint64_t ticket, uint64_t* f
 }
 
 extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* found_values, uint64_t max) {
-  if (!e || !e->srv.ring || !tags || !found_values) return 0;
+  // (ready, not ring: another thread's srv_init may have allocated the request ring only)
+  if (!e || !e->srv.ready.load(std::memory_order_acquire) || !tags || !found_values) return 0;
   LookupServer& v = e->srv;
+  {
+    // an idle reap (callers spin on this) looks only at the next ticket's answer line, which
+    // only the GPU writes: no lock taken, no line the submitters write read. The full pass
+    // below runs once that ticket is answered (or its slot moved on: answered later tickets
+    // mean a waiter took it), when it was abandoned, and every few microseconds regardless --
+    // it relaunches a server that exited with tickets waiting and notices a faulted one.
+    const uint64_t t = v.reap_hint.load(std::memory_order_relaxed);
+    const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
+    const uint64_t rt = __atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE);
+    if ((rt < t || rt == SRV_UNPUBLISHED) && v.abandoned[slot].load(std::memory_order_relaxed) != t) {
+      static thread_local uint64_t last_full = 0;
+      const uint64_t now = __rdtsc();
+      if (now - last_full < 8192) return 0;  // a few microseconds at the hosts' TSC rates
+      last_full = now;
+    }
+  }
   std::unique_lock<std::mutex> lk(v.reap_mu, std::try_to_lock);
   if (!lk.owns_lock()) return 0;  // another thread is reaping
   uint64_t n = 0, t = v.reap_next;
   const uint64_t tail = v.tail.load(std::memory_order_acquire);
-  // the result lines (written by the GPU over PCIe: a miss each) and the request metadata
-  // (written by the submitting threads) of the next tickets are fetched ahead, so the misses
-  // of consecutive tickets overlap instead of costing one round trip per state
-  for (uint64_t q = t; q < tail && q < t + 16; q += 4) {
-    __builtin_prefetch(&v.res[q & (SRV_RING - 1)], 0, 0);
-    __builtin_prefetch(&v.meta[q & (SRV_RING - 1)], 0, 0);
-  }
+  // Only the answer lines are read: written by the GPU over PCIe (a miss each, fetched ahead so
+  // the misses of consecutive tickets overlap), they carry the request's tag -- no line of the
+  // submitting threads is touched per state. Ticket t is done when its answer is there (a
+  // waiter's, tag 0, is left to its waiter), when its slot already holds a later answer (a
+  // waiter took t and the slot was reused), or when it was abandoned unpublished.
+  for (uint64_t q = t; q < tail && q < t + 16; q += 2) __builtin_prefetch(&v.res[q & (SRV_RING - 1)], 0, 0);
   while (n < max && t < tail) {
     const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
-    if ((t & 3) == 0 && t + 16 < tail) {
-      __builtin_prefetch(&v.res[(t + 16) & (SRV_RING - 1)], 0, 0);
-      __builtin_prefetch(&v.meta[(t + 16) & (SRV_RING - 1)], 0, 0);
-    }
-    const uint64_t tk = v.meta[slot].ticket.load(std::memory_order_acquire);
-    if (tk != t && v.abandoned[slot].load(std::memory_order_acquire) == t) {  // never published
+    if ((t & 1) == 0 && t + 16 < tail) __builtin_prefetch(&v.res[(t + 16) & (SRV_RING - 1)], 0, 0);
+    const uint64_t rt = __atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE);
+    if (rt == t) {
+      const uint64_t tag = __atomic_load_n(&v.res[slot].tag, __ATOMIC_RELAXED);
+      if (tag) {
+        tags[n] = (void*)(uintptr_t)tag;
+        found_values[n] = __atomic_load_n(&v.res[slot].found, __ATOMIC_RELAXED);
+        n++;
+      }
       t++;
       continue;
     }
-    if (tk == SRV_UNPUBLISHED || tk == SRV_BUSY || tk < t) break;  // not yet published
-    if (tk > t) {  // a waiter already took ticket t and its slot was reused
+    if ((rt != SRV_UNPUBLISHED && rt > t) || v.abandoned[slot].load(std::memory_order_acquire) == t) {
       t++;
       continue;
     }
-    void* tag = v.meta[slot].tag;
-    std::atomic_thread_fence(std::memory_order_acquire);  // the tag read before the re-check
-    if (v.meta[slot].ticket.load(std::memory_order_relaxed) != t) continue;  // rewritten meanwhile: re-read
-    if (!tag) {  // a waiter's ticket: its waiter takes the result
-      t++;
-      continue;
-    }
-    if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) != t) break;  // not answered yet
-    tags[n] = tag;
-    found_values[n] = __atomic_load_n(&v.res[slot].found, __ATOMIC_RELAXED);
-    v.consumed[slot].store(t + 1, std::memory_order_release);
-    n++;
-    t++;
+    break;  // not answered yet
   }
   v.reap_next = t;
+  v.reap_hint.store(t, std::memory_order_release);  // the answers before t are copied out
   lk.unlock();
   if (n == 0 && t < tail) {
     (void)srv_ensure(e);
@@ -1624,7 +1697,7 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
 // a dead server's unanswered tickets: the tags of the published ones from the reap cursor on
 // (waiters' tickets skipped: rf_amd_lookup_wait returns the error to them), consumed here
 extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, uint64_t max) {
-  if (!e || !e->srv.ring || !tags || !e->srv.dead.load(std::memory_order_acquire)) return 0;
+  if (!e || !e->srv.ready.load(std::memory_order_acquire) || !tags || !e->srv.dead.load(std::memory_order_acquire)) return 0;
   LookupServer& v = e->srv;
   std::lock_guard<std::mutex> lk(v.reap_mu);
   uint64_t n = 0, t = v.reap_next;
@@ -1650,6 +1723,7 @@ extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, u
     v.consumed[slot].store(t + 1, std::memory_order_release);
   }
   v.reap_next = t;
+  v.reap_hint.store(t, std::memory_order_release);
   return n;
 }
 

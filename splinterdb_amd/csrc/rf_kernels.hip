@@ -3743,21 +3743,26 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       ProbeGroup G[SRV_PER];
       uint32_t h[SRV_PER];
+      uint64_t tg[SRV_PER];
 #pragma unroll
       for (uint32_t m = 0; m < SRV_PER; m++) {  // every payload load first
         const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
         if (i < k) {
           G[m] = ring[slot].g;
           h[m] = ring[slot].h;
+          tg[m] = ring[slot].tag;
         }
       }
 #pragma unroll
       for (uint32_t m = 0; m < SRV_PER; m++) {
         const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
-        if (i < k) __hip_atomic_store(&res[slot].found, probe_group(G[m], h[m]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (i < k) {
+          __hip_atomic_store(&res[slot].found, probe_group(G[m], h[m]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&res[slot].tag, tg[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
-      // the found words (system-coherent stores to host memory, no cached copy to write back)
-      // have completed before any ticket is stored
+      // the found and tag words (system-coherent stores to host memory, no cached copy to
+      // write back) have completed before any ticket is stored
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (uint32_t m = 0; m < SRV_PER; m++) {

@@ -110,14 +110,19 @@ struct SrvReq {
   ProbeGroup g;     // the filter (its own routing config)
   uint32_t h;       // the key's 32-bit hash
   uint32_t pad;
-  uint64_t pad2;
+  uint64_t tag;     // the submitter's tag (0: a waiter's ticket), handed back with the answer
   uint64_t ticket;  // written last
 };
 static_assert(sizeof(SrvReq) == 64, "one request per 64-byte line");
+// an answer carries its request's tag, so the reaping thread reads only answer lines (written
+// by the GPU) and no line a submitting thread wrote
 struct SrvRes {
   uint64_t found;
   uint64_t ticket;  // written last
+  uint64_t tag;
+  uint64_t pad;
 };
+static_assert(sizeof(SrvRes) == 32, "two answers per 64-byte line");
 // control block (pinned coherent host memory): stop is set by the host; the server writes the
 // first ticket it did not serve, then its generation, when it exits
 struct SrvCtl {
