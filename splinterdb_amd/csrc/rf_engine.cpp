@@ -1386,6 +1386,12 @@ extern "C" int rf_launch_lookup_server(void* stream, const SrvReq* ring, SrvRes*
 static const uint64_t SRV_UNPUBLISHED = ~0ull, SRV_BUSY = ~0ull - 1;
 static_assert(SRV_RING == RF_AMD_SERVER_RING, "rf_amd.h and the kernels agree on the ring size");
 
+// the published tickets, dense after the request ring (eight to a 64-byte line): the server
+// polls these, one line per eight requests, and reads a request's own line only once its
+// ticket is there (polling the tickets inside the 64-byte requests read one line per request:
+// 7.6 us per 256-ticket pass, profiles/r06_async_submit.txt)
+static inline uint64_t* srv_pub(SrvReq* ring) { return reinterpret_cast<uint64_t*>(ring + SRV_RING); }
+
 static int srv_init(rf_amd_engine* e) {
   LookupServer& v = e->srv;
   // once initialised, one load (std::call_once's own fast path measured ~900 TSC cycles per
@@ -1393,7 +1399,7 @@ static int srv_init(rf_amd_engine* e) {
   if (v.ready.load(std::memory_order_acquire)) return 0;
   std::call_once(v.once, [&] {
     if (hipSetDevice(e->device) != hipSuccess ||
-        hipHostMalloc((void**)&v.ring, sizeof(SrvReq) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc((void**)&v.ring, (sizeof(SrvReq) + 8) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
         hipHostMalloc((void**)&v.res, sizeof(SrvRes) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
         hipHostMalloc((void**)&v.ctl, sizeof(SrvCtl), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
       v.init_rc = RF_AMD_ENOMEM;
@@ -1401,6 +1407,7 @@ static int srv_init(rf_amd_engine* e) {
     }
     for (uint32_t s = 0; s < SRV_RING; s++) {
       v.ring[s].ticket = SRV_UNPUBLISHED;
+      srv_pub(v.ring)[s] = SRV_UNPUBLISHED;
       v.res[s].ticket = SRV_UNPUBLISHED;
       v.consumed[s].store(0, std::memory_order_relaxed);
       v.abandoned[s].store(~0ull, std::memory_order_relaxed);
@@ -1518,7 +1525,15 @@ static int batch_errors(rf_amd_batch* b);
 // checks, ticket + slot wait, request write, server check -- printed to stderr at exit
 static int g_subprof = -1;
 static uint64_t g_subprof_cyc[7], g_subprof_n;
+static rf_amd_engine* g_subprof_eng = nullptr;
 static void subprof_print() {
+  if (g_subprof_eng && g_subprof_eng->srv.ctl && g_subprof_eng->srv.ctl->prof[5]) {
+    const uint64_t* q = g_subprof_eng->srv.ctl->prof;
+    const double np = (double)q[5];
+    fprintf(stderr, "rf_amd server passes (RF_SRV_PROF build): %llu served, us each: tickets %.2f payloads %.2f "
+            "probe+store %.2f store wait %.2f ticket stores %.2f\n", (unsigned long long)q[5], q[0] / np / 100,
+            q[1] / np / 100, q[2] / np / 100, q[3] / np / 100, q[4] / np / 100);
+  }
   if (g_subprof_n)
     fprintf(stderr, "rf_amd submit profile: %llu submissions, TSC cycles each: checks %.0f (args %.0f init %.0f "
             "errors %.0f) ticket %.0f write %.0f ensure %.0f\n",
@@ -1537,6 +1552,7 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
   }
   const uint64_t c0 = g_subprof > 0 ? __rdtsc() : 0;
   if (!e) return fail(RF_AMD_ENODEV, "no engine");
+  if (g_subprof > 0) g_subprof_eng = e;
   if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "lookup on an unbuilt or foreign batch");
   if (filter_index >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
   if (!ticket) return fail(RF_AMD_EINVAL, "null ticket");
@@ -1573,8 +1589,8 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
         }
       }
     }
-    // the slot is being rewritten: readers that see this do not trust its payload or tag
-    __atomic_store_n(&v.ring[slot].ticket, SRV_BUSY, __ATOMIC_RELEASE);
+    // the slot is being rewritten: readers that see this do not trust its tag (the server
+    // reads the request only after its new ticket is published)
     v.meta[slot].ticket.store(SRV_BUSY, std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_release);  // BUSY before the new tag (a seqlock)
   }
@@ -1586,7 +1602,8 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
   q.tag = (uint64_t)(uintptr_t)tag;
   v.meta[slot].tag = tag;
   v.meta[slot].ticket.store(t, std::memory_order_release);
-  __atomic_store_n(&q.ticket, t, __ATOMIC_RELEASE);
+  q.ticket = t;
+  __atomic_store_n(&srv_pub(v.ring)[slot], t, __ATOMIC_RELEASE);  // after the payload (x86: in order)
   *ticket = t;
   const uint64_t c3 = g_subprof > 0 ? __rdtsc() : 0;
   // published: from here the ticket's tag comes back through rf_amd_lookup_reap or, if the

@@ -3711,33 +3711,61 @@ __global__ __launch_bounds__(WAVE) void k_probe_small(SmallProbe a) {
 // `life_ticks` in total (s_memrealtime, 100 MHz) or when the host sets ctl->stop -- every
 // loop iteration checks the clock, so the kernel always ends -- and reports the first ticket
 // it did not serve; the host relaunches it from there when more requests come.
+#ifndef RF_SRV_PROF
+#define RF_SRV_PROF 0
+#endif
 __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict__ ring, SrvRes* __restrict__ res,
                                                         SrvCtl* __restrict__ ctl, uint64_t head, uint64_t gen,
                                                         uint64_t idle_ticks, uint64_t life_ticks) {
   const uint32_t lane = threadIdx.x;
+  // the published tickets: SRV_RING words after the requests (rf_engine.cpp srv_pub)
+  const uint64_t* pub = reinterpret_cast<const uint64_t*>(ring + SRV_RING);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t t_busy = t0, served = 0;
-  // a pass looks at the next SRV_PER x 64 tickets (one load per lane and group, all in flight
-  // together) and serves their ready prefix, SRV_PER requests per lane: a backlog of
-  // submitted requests goes out SRV_PER times faster than one request per lane and pass
+  // a pass looks at the next 64 tickets (one load per lane) and, when all of them are ready
+  // (a backlog), at the next (SRV_PER - 1) x 64 too, all in flight together; it serves their
+  // ready prefix, up to SRV_PER requests per lane. Reads of host memory go out at ~30 ns each
+  // per wave (throughput, not latency, bound: polling 256 tickets took 7.6 us a pass, 64 take
+  // a quarter of that -- profiles/r06_async_submit.txt), so only a backlog pays for more.
   constexpr uint32_t SRV_PER = 4;
+#if RF_SRV_PROF
+  uint64_t pf[6] = {0, 0, 0, 0, 0, 0};
+  auto stamp = [] {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return __builtin_amdgcn_s_memrealtime();
+  };
+#endif
   for (;;) {
+#if RF_SRV_PROF
+    const uint64_t pa = stamp();
+#endif
     uint64_t tk[SRV_PER];
-#pragma unroll
-    for (uint32_t m = 0; m < SRV_PER; m++)
-      tk[m] = __hip_atomic_load(&ring[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))].ticket, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_SYSTEM);
+    tk[0] = __hip_atomic_load(&pub[(uint32_t)((head + lane) & (SRV_RING - 1))], __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_SYSTEM);
     // the host's stop word, read beside the tickets (in flight with them: no extra round trip),
     // so a busy wave stops too (engine shutdown, a server marked dead)
     uint64_t stp = lane == 0 ? __hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     if (__shfl(stp, 0)) break;
-    uint32_t k = 0;  // the ready prefix
+    uint32_t k;  // the ready prefix
+    {
+      const uint64_t ready = __builtin_amdgcn_ballot_w64(tk[0] == head + lane);
+      k = ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
+    }
+    if (k == WAVE) {
 #pragma unroll
-    for (uint32_t m = 0; m < SRV_PER; m++) {
-      const uint64_t ready = __builtin_amdgcn_ballot_w64(tk[m] == head + lane + WAVE * m);
-      if (k == WAVE * m) k += ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
+      for (uint32_t m = 1; m < SRV_PER; m++)
+        tk[m] = __hip_atomic_load(&pub[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (uint32_t m = 1; m < SRV_PER; m++) {
+        const uint64_t ready = __builtin_amdgcn_ballot_w64(tk[m] == head + lane + WAVE * m);
+        if (k == WAVE * m) k += ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
+      }
     }
     if (k) {
+#if RF_SRV_PROF
+      const uint64_t pb = stamp();
+#endif
       // acquire (system scope) once per served pass, not per poll: the payloads after the
       // tickets, and no stale cached device data (it invalidates this CU's L1 and the L2)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -3753,6 +3781,9 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
           tg[m] = ring[slot].tag;
         }
       }
+#if RF_SRV_PROF
+      const uint64_t pc = stamp();
+#endif
 #pragma unroll
       for (uint32_t m = 0; m < SRV_PER; m++) {
         const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
@@ -3763,12 +3794,27 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
       }
       // the found and tag words (system-coherent stores to host memory, no cached copy to
       // write back) have completed before any ticket is stored
+#if RF_SRV_PROF
+      const uint64_t pd = __builtin_amdgcn_s_memrealtime();
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if RF_SRV_PROF
+      const uint64_t pe = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
       for (uint32_t m = 0; m < SRV_PER; m++) {
         const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
         if (i < k) __hip_atomic_store(&res[slot].ticket, head + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
+#if RF_SRV_PROF
+      const uint64_t pg = stamp();
+      pf[0] += pb - pa;
+      pf[1] += pc - pb;
+      pf[2] += pd - pc;
+      pf[3] += pe - pd;
+      pf[4] += pg - pe;
+      pf[5] += 1;
+#endif
       head += k;
       served += k;
       t_busy = __builtin_amdgcn_s_memrealtime();
@@ -3785,7 +3831,7 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
       }
       uint64_t t1 = 0, st = 0;
       if (lane == 0) {
-        t1 = __hip_atomic_load(&ring[head & (SRV_RING - 1)].ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        t1 = __hip_atomic_load(&pub[head & (SRV_RING - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         st = __hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       t1 = __shfl(t1, 0);
@@ -3800,6 +3846,11 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
     if (stop) break;
   }
   if (lane == 0) {
+#if RF_SRV_PROF
+    for (int q = 0; q < 6; q++)  // one server wave at a time: a plain read-add-write
+      __hip_atomic_store(&ctl->prof[q], __hip_atomic_load(&ctl->prof[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + pf[q],
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     __hip_atomic_store(&ctl->exit_head, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&ctl->served, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&ctl->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -103,8 +103,9 @@ struct ProbeGroup {
 
 // The lookup server (k_lookup_server): single lookups travel through a ring of requests in
 // pinned coherent host memory that a persistent wave polls, instead of one kernel launch per
-// call. Request t sits in slot t % SRV_RING; the host writes the payload, then `ticket` = t
-// (release); the server answers in slot t of the result ring (found, then ticket = t).
+// call. Request t sits in slot t % SRV_RING; the host writes the payload, then publishes t in
+// word t % SRV_RING of the dense ticket array after the ring (release); the server answers in
+// slot t of the result ring (found and tag, then ticket = t).
 constexpr uint32_t SRV_RING = 4096;
 struct SrvReq {
   ProbeGroup g;     // the filter (its own routing config)
@@ -130,6 +131,10 @@ struct SrvCtl {
   uint64_t exit_head;
   uint64_t exit_gen;
   uint64_t served;
+  // diagnostics builds (RF_SRV_PROF): over every served pass of every launch, 10-ns ticks
+  // polling the tickets, loading the payloads, probing + storing the answers, waiting for those
+  // stores, storing the tickets; then the served passes
+  uint64_t prof[6];
 };
 
 // a lookup call small enough to travel in the kernel arguments (k_probe_small)

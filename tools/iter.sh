@@ -1,14 +1,16 @@
 #!/bin/bash
-# r06 call 29: completion threads pinned to the caller's LLC (RF_SHIM_PIN_THREADS 0 vs 1)
+# r06 call 32: dense published-ticket array (8 tickets per polled line)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r06zc
+O=gpurun_out/r06zf
 mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_server.py tests/test_gpu_shim.py > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
 for i in 1 2; do
-for P in 0 1; do
-  RF_SHIM_PIN_THREADS=$P AD_REPS=9 timeout -k 10 300 python3 -u tools/async_driven.py > $O/ad_p${P}_$i.json 2> $O/ad_p${P}_$i.err || { echo ad failed; tail -40 $O/ad_p${P}_$i.err; exit 1; }
-  echo "pin=$P"; cat $O/ad_p${P}_$i.json
+AD_REPS=9 timeout -k 10 300 python3 -u tools/async_driven.py > $O/ad_$i.json 2> $O/ad_$i.err || { echo ad failed; tail -40 $O/ad_$i.err; exit 1; }
+cat $O/ad_$i.json
 done
-done
-cat /sys/devices/system/cpu/cpu0/cache/index3/shared_cpu_list; taskset -p $$
+cp tools/ab/librf_amd_srvprof.so splinterdb_amd/librf_amd.so
+RF_AMD_SUBMIT_PROFILE=1 AD_ONLY=shim timeout -k 10 300 python3 -u tools/async_driven.py > $O/ad_prof.json 2> $O/ad_prof.err || { echo ad failed; tail -40 $O/ad_prof.err; exit 1; }
+cat $O/ad_prof.json; grep "profile\|passes" $O/ad_prof.err
