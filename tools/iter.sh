@@ -1,9 +1,9 @@
 #!/bin/bash
-# r06 call 32: dense published-ticket array (8 tickets per polled line)
+# r06 call 33: the idle poll hands its window to the next pass
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r06zf
+O=gpurun_out/r06zg
 mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_server.py tests/test_gpu_shim.py > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
