@@ -55,8 +55,9 @@
  * reaches zero.
  *
  * Lookups. routing_filter_lookup and routing_filter_lookup_async go to the engine's lookup
- * server (rf_amd_lookup_submit): a ring of requests in pinned host memory that a persistent
- * GPU wave polls, so a single lookup costs no kernel launch and needs no batching.
+ * server (rf_amd_lookup_submit): a ring of requests in device memory, written by the host
+ * through the BAR, that a persistent GPU wave polls, so a single lookup costs no kernel
+ * launch and needs no batching.
  * routing_filter_lookup waits for its answer. routing_filter_lookup_async's first call on a
  * state hashes the key, submits it and returns ASYNC_STATUS_RUNNING without touching the
  * state again (async.h:115-125: it may be completed on another thread at once). A completion
@@ -1546,7 +1547,7 @@ lookup_many(cache *const          *ccs,
 /*
  * routing_filter_lookup_async hashes the key and, while fewer than AQ_SERVER_MAX states wait
  * on the engine's lookup server, pins the filter's device batch and submits ONE request to it
- * (rf_amd_lookup_submit: a ring in pinned host memory that a persistent GPU wave polls -- no
+ * (rf_amd_lookup_submit: a ring in device memory that a persistent GPU wave polls -- no
  * kernel launch, no batching delay: the latency path of callers that keep a few lookups in
  * flight). Beyond that the state goes onto a lock-free stack instead (one compare-and-swap):
  * the batch thread takes the whole stack whenever it is free and answers it with ONE launch
@@ -1577,6 +1578,10 @@ static pthread_once_t  g_aq_once = PTHREAD_ONCE_INIT;
 /* reaps that returned states, states completed, ns spent reaping and firing callbacks
  * (routing_filter_amd_async_breakdown; the completion thread's) */
 static uint64 g_async_batches SHIM_LINE, g_async_probes, g_async_reap_ns, g_async_cb_ns;
+/* RF_SHIM_SUBMIT_PROFILE=1 (diagnostics; set at the first async call): submit steps, and the
+ * server states outstanding whenever a reap finds answers (completion thread only) */
+static int    g_subprof = -1;
+static uint64 g_reap_outstanding_sum, g_reap_outstanding_n;
 
 #define AQ_PIN(st) (*(shim_batch **)&(st)->filter_page)
 
@@ -1770,7 +1775,11 @@ async_reap_complete(void)
    }
    /* one update of the shared count per reap, before the callbacks (a callback that submits
       and finds the ring nearly full reaps in place: the count must not hold these) */
-   __atomic_sub_fetch(&g_aq_outstanding, n, __ATOMIC_RELEASE);
+   const uint64 outstanding = __atomic_fetch_sub(&g_aq_outstanding, n, __ATOMIC_RELEASE);
+   if (g_subprof > 0) { /* diagnostics: server states outstanding when a reap finds answers */
+      g_reap_outstanding_sum += outstanding;
+      g_reap_outstanding_n++;
+   }
    for (uint64 i = 0; i < n; i++) {
       if (cbs[i]) {
          cbs[i](args[i]);
@@ -1971,7 +1980,6 @@ routing_filter_amd_async_probe_ns(void)
 /* RF_SHIM_SUBMIT_PROFILE=1 (diagnostics): TSC cycles of each step of a server submission --
    hash, registry pin, ring-space wait and bookkeeping, rf_amd_lookup_submit, wake-up -- summed
    and printed to stderr at exit */
-static int    g_subprof = -1;
 static uint64 g_subprof_cyc[5], g_subprof_n;
 #define SUBPROF_MARK(i)                                                                            \
    uint64 sp_##i = 0;                                                                              \
@@ -1990,6 +1998,10 @@ static uint64 g_subprof_cyc[5], g_subprof_n;
 static void
 subprof_print(void)
 {
+   if (g_subprof > 0 && g_reap_outstanding_n) {
+      fprintf(stderr, "rf_shim reaps: %lu with answers, %.1f server states outstanding at each\n",
+              (unsigned long)g_reap_outstanding_n, (double)g_reap_outstanding_sum / g_reap_outstanding_n);
+   }
    if (g_subprof > 0 && g_subprof_n) {
       fprintf(stderr,
               "rf_shim submit profile: %lu submissions, TSC cycles each: hash %.0f pin %.0f "

@@ -196,8 +196,9 @@ struct ProbeSlot {
 struct LookupServer {
   std::once_flag once;
   int init_rc = 0;
-  SrvReq* ring = nullptr;  // pinned coherent host memory
-  SrvRes* res = nullptr;
+  SrvReq* ring = nullptr;  // device memory the host writes through the BAR (or pinned host memory)
+  bool ring_dev = false;
+  SrvRes* res = nullptr;   // pinned coherent host memory
   SrvCtl* ctl = nullptr;
   hipStream_t st = nullptr;             // its own HSA queue (CU-masked), so it never blocks other work
   std::atomic<uint64_t> idle_ticks{0}, life_ticks{0};  // of the next launch (rf_amd_lookup_server_set_times)
@@ -1386,11 +1387,33 @@ extern "C" int rf_launch_lookup_server(void* stream, const SrvReq* ring, SrvRes*
 static const uint64_t SRV_UNPUBLISHED = ~0ull, SRV_BUSY = ~0ull - 1;
 static_assert(SRV_RING == RF_AMD_SERVER_RING, "rf_amd.h and the kernels agree on the ring size");
 
-// the published tickets, dense after the request ring (eight to a 64-byte line): the server
-// polls these, one line per eight requests, and reads a request's own line only once its
-// ticket is there (polling the tickets inside the 64-byte requests read one line per request:
-// 7.6 us per 256-ticket pass, profiles/r06_async_submit.txt)
-static inline uint64_t* srv_pub(SrvReq* ring) { return reinterpret_cast<uint64_t*>(ring + SRV_RING); }
+// the host's stop word, after the request ring (the wave polls it with the requests)
+static inline volatile uint64_t* srv_stop_word(SrvReq* ring) { return reinterpret_cast<volatile uint64_t*>(ring + SRV_RING); }
+static void srv_set_stop(LookupServer& v) {
+  if (!v.ring) return;
+  *srv_stop_word(v.ring) = 1;
+  _mm_sfence();  // out of the write-combining buffer now
+}
+// answer of ticket t in its slot: 1 = all four words carry t's check (found/tag filled in),
+// -1 = the slot holds a later ticket's answer (a waiter took t and the slot moved on), 0 = not yet
+static inline int srv_answer(const SrvRes* r, uint64_t t, uint64_t* found, uint64_t* tag) {
+  const uint32_t c = srv_check(t);
+  uint64_t w[4];
+  for (int k = 0; k < 4; k++) w[k] = __atomic_load_n(&r->w[k], __ATOMIC_ACQUIRE);
+  const uint32_t c0 = (uint32_t)(w[0] >> 32);
+  if (c0 != c) return (c0 != 0 && (int32_t)(c0 - c) > 0) ? -1 : 0;
+  for (int k = 1; k < 4; k++)
+    if ((uint32_t)(w[k] >> 32) != c) return 0;  // still arriving
+  if (found) *found = (w[0] & 0xffffffffull) | (w[1] << 32);
+  if (tag) *tag = (w[2] & 0xffffffffull) | (w[3] << 32);
+  return 1;
+}
+// RF_AMD_SRV_RING=host puts the request ring in pinned host memory (the round-6 layout's
+// placement); default: fine-grained device memory, written by the host through the BAR
+static bool srv_ring_on_device() {
+  const char* s = getenv("RF_AMD_SRV_RING");
+  return !(s && !strcmp(s, "host"));
+}
 
 static int srv_init(rf_amd_engine* e) {
   LookupServer& v = e->srv;
@@ -1398,17 +1421,50 @@ static int srv_init(rf_amd_engine* e) {
   // submit, profiles/r06_async_submit.txt)
   if (v.ready.load(std::memory_order_acquire)) return 0;
   std::call_once(v.once, [&] {
-    if (hipSetDevice(e->device) != hipSuccess ||
-        hipHostMalloc((void**)&v.ring, (sizeof(SrvReq) + 8) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
-        hipHostMalloc((void**)&v.res, sizeof(SrvRes) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+    const size_t ring_bytes = sizeof(SrvReq) * SRV_RING + 128;  // + the stop word's line
+    if (hipSetDevice(e->device) != hipSuccess) {
+      v.init_rc = RF_AMD_ENOMEM;
+      return;
+    }
+    v.ring_dev = srv_ring_on_device() &&
+                 hipExtMallocWithFlags((void**)&v.ring, ring_bytes, hipDeviceMallocFinegrained) == hipSuccess;
+    if (v.ring_dev) {
+      // the host writes it through its mapping of device memory: zero it there, then check on
+      // the device that a host store landed (a box whose BAR does not reach it falls back)
+      if (hipMemset(v.ring, 0, ring_bytes) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) {
+        (void)hipFree(v.ring);
+        v.ring = nullptr;
+        v.ring_dev = false;
+      } else {
+        volatile uint64_t* w = &v.ring[SRV_RING - 1].w[SRV_REQ_WORDS - 1];
+        *w = 0x5EEDF00Dull;
+        _mm_sfence();
+        uint64_t back = 0;
+        const bool ok = hipMemcpy(&back, (const void*)w, 8, hipMemcpyDeviceToHost) == hipSuccess && back == 0x5EEDF00Dull;
+        *w = 0;
+        _mm_sfence();
+        if (!ok) {
+          (void)hipFree(v.ring);
+          v.ring = nullptr;
+          v.ring_dev = false;
+        }
+      }
+    }
+    if (!v.ring_dev) {
+      if (hipHostMalloc((void**)&v.ring, ring_bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        v.ring = nullptr;
+        v.init_rc = RF_AMD_ENOMEM;
+        return;
+      }
+      memset((void*)v.ring, 0, ring_bytes);
+    }
+    if (hipHostMalloc((void**)&v.res, sizeof(SrvRes) * SRV_RING, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
         hipHostMalloc((void**)&v.ctl, sizeof(SrvCtl), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
       v.init_rc = RF_AMD_ENOMEM;
       return;
     }
+    memset(v.res, 0, sizeof(SrvRes) * SRV_RING);  // check 0: no answer yet
     for (uint32_t s = 0; s < SRV_RING; s++) {
-      v.ring[s].ticket = SRV_UNPUBLISHED;
-      srv_pub(v.ring)[s] = SRV_UNPUBLISHED;
-      v.res[s].ticket = SRV_UNPUBLISHED;
       v.consumed[s].store(0, std::memory_order_relaxed);
       v.abandoned[s].store(~0ull, std::memory_order_relaxed);
     }
@@ -1466,10 +1522,14 @@ static void srv_stop(rf_amd_engine* e) {
   LookupServer& v = e->srv;
   if (!v.ctl || !v.st) return;
   v.ready.store(false, std::memory_order_release);
-  __atomic_store_n(&v.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  srv_set_stop(v);
   (void)hipStreamSynchronize(v.st);
   (void)hipStreamDestroy(v.st);
-  (void)hipHostFree(v.ring);
+  if (v.ring_dev)
+    (void)hipFree(v.ring);
+  else
+    (void)hipHostFree(v.ring);
+  v.ring = nullptr;
   (void)hipHostFree(v.res);
   (void)hipHostFree(v.ctl);
   v.st = nullptr;
@@ -1485,7 +1545,7 @@ static bool engine_quiesce(rf_amd_engine* e, int budget_ms) {
   clock_gettime(CLOCK_MONOTONIC, &ts);
   const uint64_t deadline = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec + (uint64_t)budget_ms * 1000000ull;
   LookupServer& v = e->srv;
-  if (v.ctl) __atomic_store_n(&v.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  if (v.ctl) srv_set_stop(v);
   if (v.st && !stream_drained(v.st, deadline)) return false;
   if (!stream_drained(e->stream, deadline)) return false;
   std::lock_guard<std::mutex> g(e->slot_mu);
@@ -1521,19 +1581,48 @@ static int srv_dead(rf_amd_engine* e) {
 static ProbeGroup probe_group_of(const rf_amd_batch* b, uint32_t f);
 static int batch_errors(rf_amd_batch* b);
 
+// RF_AMD_REAP_TAIL=1: the reap loop bounded by the ticket counter (A/B switch; by default the
+// answers' checks bound it and the submitters' counter line is not read)
+static bool srv_reap_tail() {
+  static const bool on = [] {
+    const char* s = getenv("RF_AMD_REAP_TAIL");
+    return s && atoi(s) > 0;
+  }();
+  return on;
+}
+// RF_AMD_SRV_SFENCE=1: an sfence after each request (A/B switch: whole lines leave the
+// write-combining buffers without one)
+static bool srv_sfence() {
+  static const bool on = [] {
+    const char* s = getenv("RF_AMD_SRV_SFENCE");
+    return s && atoi(s) > 0;
+  }();
+  return on;
+}
+
 // RF_AMD_SUBMIT_PROFILE=1 (diagnostics): TSC cycles of the steps of rf_amd_lookup_submit --
 // checks, ticket + slot wait, request write, server check -- printed to stderr at exit
 static int g_subprof = -1;
 static uint64_t g_subprof_cyc[7], g_subprof_n;
+// the reaper's side (one completion thread in the profiled runs): TSC cycles of reaps that
+// returned states -- the idle look at the next answer, lock + cursor, the answer loop -- and
+// the states they returned
+static uint64_t g_reapprof_cyc[3], g_reapprof_n, g_reapprof_states;
 static rf_amd_engine* g_subprof_eng = nullptr;
 static void subprof_print() {
   if (g_subprof_eng && g_subprof_eng->srv.ctl && g_subprof_eng->srv.ctl->prof[5]) {
     const uint64_t* q = g_subprof_eng->srv.ctl->prof;
     const double np = (double)q[5];
-    fprintf(stderr, "rf_amd server passes (RF_SRV_PROF build): %llu served, us each: tickets %.2f payloads %.2f "
-            "probe+store %.2f store wait %.2f ticket stores %.2f\n", (unsigned long long)q[5], q[0] / np / 100,
-            q[1] / np / 100, q[2] / np / 100, q[3] / np / 100, q[4] / np / 100);
+    fprintf(stderr, "rf_amd server passes (RF_SRV_PROF build): %llu served, us each: poll %.2f payloads %.2f "
+            "probe+answers %.2f; %.1f requests per pass, %llu passes cut by a request still arriving\n",
+            (unsigned long long)q[5], q[0] / np / 100, q[1] / np / 100, q[2] / np / 100, q[4] / np,
+            (unsigned long long)q[3]);
   }
+  if (g_reapprof_n)
+    fprintf(stderr, "rf_amd reap profile: %llu reaps with answers, %.1f states each, TSC cycles each: idle look %.0f "
+            "lock+cursor %.0f answers %.0f\n", (unsigned long long)g_reapprof_n, (double)g_reapprof_states / g_reapprof_n,
+            (double)g_reapprof_cyc[0] / g_reapprof_n, (double)g_reapprof_cyc[1] / g_reapprof_n,
+            (double)g_reapprof_cyc[2] / g_reapprof_n);
   if (g_subprof_n)
     fprintf(stderr, "rf_amd submit profile: %llu submissions, TSC cycles each: checks %.0f (args %.0f init %.0f "
             "errors %.0f) ticket %.0f write %.0f ensure %.0f\n",
@@ -1595,15 +1684,21 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     std::atomic_thread_fence(std::memory_order_release);  // BUSY before the new tag (a seqlock)
   }
   const uint64_t c2 = g_subprof > 0 ? __rdtsc() : 0;
-  SrvReq& q = v.ring[slot];
-  q.g = probe_group_of(b, filter_index);
-  q.h = hash;
-  q.pad = tag ? 0u : 1u;  // 1: a waiter's ticket (rf_amd_lookup_wait takes its result)
-  q.tag = (uint64_t)(uintptr_t)tag;
-  v.meta[slot].tag = tag;
-  v.meta[slot].ticket.store(t, std::memory_order_release);
-  q.ticket = t;
-  __atomic_store_n(&srv_pub(v.ring)[slot], t, __ATOMIC_RELEASE);  // after the payload (x86: in order)
+  {
+    // 16 words, each with t's check in its high half; plain 8-byte stores in any order (two
+    // whole 64-byte lines: through the write-combining BAR mapping they leave as two bursts)
+    const ProbeGroup g = probe_group_of(b, filter_index);
+    const uint64_t tg = (uint64_t)(uintptr_t)tag;
+    const uint64_t lp = (uint64_t)(uintptr_t)g.lines, pp = (uint64_t)(uintptr_t)g.pages, sp = (uint64_t)(uintptr_t)g.slots;
+    const uint32_t p[SRV_REQ_WORDS] = {g.x, g.err, g.fpl, hash, (uint32_t)lp, (uint32_t)(lp >> 32), (uint32_t)pp, (uint32_t)(pp >> 32),
+                                       (uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)tg, (uint32_t)(tg >> 32), 0u, 0u, 0u, 0u};
+    v.meta[slot].tag = tag;
+    v.meta[slot].ticket.store(t, std::memory_order_release);
+    const uint64_t ck = (uint64_t)srv_check(t) << 32;
+    volatile uint64_t* w = v.ring[slot].w;
+    for (uint32_t k = 0; k < SRV_REQ_WORDS; k++) w[k] = (uint64_t)p[k] | ck;
+    if (srv_sfence()) _mm_sfence();
+  }
   *ticket = t;
   const uint64_t c3 = g_subprof > 0 ? __rdtsc() : 0;
   // published: from here the ticket's tag comes back through rf_amd_lookup_reap or, if the
@@ -1629,8 +1724,7 @@ extern "C" int rf_amd_lookup_wait(rf_amd_engine* e, uint64_t ticket, uint64_t* f
   LookupServer& v = e->srv;
   const uint32_t slot = (uint32_t)(ticket & (SRV_RING - 1));
   for (uint32_t spin = 1;; spin++) {
-    if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) == ticket) {
-      if (found_values) *found_values = __atomic_load_n(&v.res[slot].found, __ATOMIC_RELAXED);
+    if (srv_answer(&v.res[slot], ticket, found_values, nullptr) == 1) {
       v.consumed[slot].store(ticket + 1, std::memory_order_release);
       return 0;
     }
@@ -1648,6 +1742,8 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
   // (ready, not ring: another thread's srv_init may have allocated the request ring only)
   if (!e || !e->srv.ready.load(std::memory_order_acquire) || !tags || !found_values) return 0;
   LookupServer& v = e->srv;
+  const bool prof = g_subprof > 0;
+  const uint64_t r0 = prof ? __rdtsc() : 0;
   {
     // an idle reap (callers spin on this) looks only at the next ticket's answer line, which
     // only the GPU writes: no lock taken, no line the submitters write read. The full pass
@@ -1656,48 +1752,59 @@ extern "C" uint64_t rf_amd_lookup_reap(rf_amd_engine* e, void** tags, uint64_t* 
     // it relaunches a server that exited with tickets waiting and notices a faulted one.
     const uint64_t t = v.reap_hint.load(std::memory_order_relaxed);
     const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
-    const uint64_t rt = __atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE);
-    if ((rt < t || rt == SRV_UNPUBLISHED) && v.abandoned[slot].load(std::memory_order_relaxed) != t) {
+    if (srv_answer(&v.res[slot], t, nullptr, nullptr) == 0 && v.abandoned[slot].load(std::memory_order_relaxed) != t) {
       static thread_local uint64_t last_full = 0;
       const uint64_t now = __rdtsc();
       if (now - last_full < 8192) return 0;  // a few microseconds at the hosts' TSC rates
       last_full = now;
     }
   }
+  const uint64_t r1 = prof ? __rdtsc() : 0;
   std::unique_lock<std::mutex> lk(v.reap_mu, std::try_to_lock);
   if (!lk.owns_lock()) return 0;  // another thread is reaping
   uint64_t n = 0, t = v.reap_next;
-  const uint64_t tail = v.tail.load(std::memory_order_acquire);
   // Only the answer lines are read: written by the GPU over PCIe (a miss each, fetched ahead so
-  // the misses of consecutive tickets overlap), they carry the request's tag -- no line of the
-  // submitting threads is touched per state. Ticket t is done when its answer is there (a
-  // waiter's, tag 0, is left to its waiter), when its slot already holds a later answer (a
-  // waiter took t and the slot was reused), or when it was abandoned unpublished.
+  // the misses of consecutive tickets overlap), they carry the request's tag and check -- no line
+  // of the submitting threads is touched per state, not even the ticket counter: a slot past
+  // the last ticket holds an older check and stops the loop like an unanswered one. Ticket t is
+  // done when its answer is there (a waiter's, tag 0, is left to its waiter), when its slot
+  // already holds a later answer (a waiter took t and the slot was reused), or when it was
+  // abandoned unpublished.
+  const uint64_t tail = srv_reap_tail() ? v.tail.load(std::memory_order_acquire) : ~0ull;
+  const uint64_t r2 = prof ? __rdtsc() : 0;
   for (uint64_t q = t; q < tail && q < t + 16; q += 2) __builtin_prefetch(&v.res[q & (SRV_RING - 1)], 0, 0);
   while (n < max && t < tail) {
     const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
-    if ((t & 1) == 0 && t + 16 < tail) __builtin_prefetch(&v.res[(t + 16) & (SRV_RING - 1)], 0, 0);
-    const uint64_t rt = __atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE);
-    if (rt == t) {
-      const uint64_t tag = __atomic_load_n(&v.res[slot].tag, __ATOMIC_RELAXED);
+    if ((t & 1) == 0) __builtin_prefetch(&v.res[(t + 16) & (SRV_RING - 1)], 0, 0);
+    uint64_t found = 0, tag = 0;
+    const int a = srv_answer(&v.res[slot], t, &found, &tag);
+    if (a == 1) {
       if (tag) {
         tags[n] = (void*)(uintptr_t)tag;
-        found_values[n] = __atomic_load_n(&v.res[slot].found, __ATOMIC_RELAXED);
+        found_values[n] = found;
         n++;
       }
       t++;
       continue;
     }
-    if ((rt != SRV_UNPUBLISHED && rt > t) || v.abandoned[slot].load(std::memory_order_acquire) == t) {
+    if (a < 0 || v.abandoned[slot].load(std::memory_order_acquire) == t) {
       t++;
       continue;
     }
-    break;  // not answered yet
+    break;  // not answered yet (or past the last ticket)
   }
   v.reap_next = t;
   v.reap_hint.store(t, std::memory_order_release);  // the answers before t are copied out
   lk.unlock();
-  if (n == 0 && t < tail) {
+  if (prof && n) {
+    const uint64_t r3 = __rdtsc();
+    g_reapprof_cyc[0] += r1 - r0;
+    g_reapprof_cyc[1] += r2 - r1;
+    g_reapprof_cyc[2] += r3 - r2;
+    g_reapprof_n++;
+    g_reapprof_states += n;
+  }
+  if (n == 0 && t < v.tail.load(std::memory_order_acquire)) {
     (void)srv_ensure(e);
     // a faulted server stream never answers and nothing else would notice with only tagged
     // tickets outstanding: look at it about once a millisecond, so `dead` gets set and the
@@ -1735,7 +1842,7 @@ extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, u
     std::atomic_thread_fence(std::memory_order_acquire);
     if (v.meta[slot].ticket.load(std::memory_order_relaxed) != t) break;  // being rewritten: next call
     if (!tag) continue;
-    if (__atomic_load_n(&v.res[slot].ticket, __ATOMIC_ACQUIRE) == t) break;  // answered: reap takes it
+    if (srv_answer(&v.res[slot], t, nullptr, nullptr) == 1) break;  // answered: reap takes it
     tags[n++] = tag;
     v.consumed[slot].store(t + 1, std::memory_order_release);
   }
@@ -1750,7 +1857,7 @@ extern "C" uint64_t rf_amd_lookup_server_failed(rf_amd_engine* e, void** tags, u
 extern "C" int rf_amd_diag_lookup_server_kill(rf_amd_engine* e, int err, uint32_t gap_us) {
   if (!e || !err) return fail(RF_AMD_EINVAL, "bad argument");
   if (int rc = srv_init(e)) return rc;
-  __atomic_store_n(&e->srv.ctl->stop, 1ull, __ATOMIC_RELEASE);
+  srv_set_stop(e->srv);
   if (gap_us) {
     struct timespec nap = {(time_t)(gap_us / 1000000), (long)(gap_us % 1000000) * 1000};
     nanosleep(&nap, nullptr);

@@ -3698,35 +3698,38 @@ __global__ __launch_bounds__(WAVE) void k_probe_small(SmallProbe a) {
 
 // ---- the lookup server ---------------------------------------------------------------------
 // One persistent wave answers single lookups (routing_filter_lookup, routing_filter_lookup_async
-// states) that the host writes into a ring of SrvReq in pinned coherent host memory: no
-// kernel launch per call (a launch round trip is ~6.5 us on MI355X, a round trip through the
-// ring ~3.8 us, profiles/r04_pingpong.txt). Each pass reads the ticket words of the next 64
-// slots; when some are ready, a system-scope acquire orders the payload reads after them (the
-// host stores the payload before the ticket) and drops stale cached device data (batches are
-// built by other kernels into pooled memory while this one runs); the lanes of the ready prefix
-// probe their filter
-// (probe_group, as k_probe_groups does) and answer in the result ring, found first, then the
-// ticket (system-scope release). When nothing is ready, lane 0 polls the next ticket with
-// s_sleep between polls. The wave exits after `idle_ticks` without requests, after
-// `life_ticks` in total (s_memrealtime, 100 MHz) or when the host sets ctl->stop -- every
-// loop iteration checks the clock, so the kernel always ends -- and reports the first ticket
-// it did not serve; the host relaunches it from there when more requests come.
+// states) that the host writes into a ring of SrvReq (rf_plan.h: device memory written through
+// the BAR, or pinned host memory): no kernel launch per call (a launch round trip is ~6.5 us on
+// MI355X). Each pass reads word 0 of the next 64 slots; the lanes whose word carries their
+// ticket's check read the rest of their request, and the prefix whose 16 words all carry it
+// (the host's stores arrive in any order) is served: a system-scope acquire drops stale cached
+// device data (batches are built by other kernels into pooled memory while this one runs), the
+// lanes probe their filter (probe_group, as k_probe_groups does) and store the answer words,
+// each carrying the check, so nothing waits for those stores. When nothing is ready, lane 0
+// polls the next slot with s_sleep between polls. The wave exits after `idle_ticks` without
+// requests, after `life_ticks` in total (s_memrealtime, 100 MHz) or when the host sets the stop
+// word after the ring -- every loop iteration checks the clock, so the kernel always ends -- and
+// reports the first ticket it did not serve; the host relaunches it from there when more
+// requests come.
 #ifndef RF_SRV_PROF
 #define RF_SRV_PROF 0
 #endif
+#ifndef RF_SRV_PAIRSTORE
+#define RF_SRV_PAIRSTORE 1
+#endif
+__device__ __forceinline__ uint64_t srv_ld(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict__ ring, SrvRes* __restrict__ res,
                                                         SrvCtl* __restrict__ ctl, uint64_t head, uint64_t gen,
                                                         uint64_t idle_ticks, uint64_t life_ticks) {
   const uint32_t lane = threadIdx.x;
-  // the published tickets: SRV_RING words after the requests (rf_engine.cpp srv_pub)
-  const uint64_t* pub = reinterpret_cast<const uint64_t*>(ring + SRV_RING);
+  const uint64_t* stop_word = reinterpret_cast<const uint64_t*>(ring + SRV_RING);  // rf_engine.cpp srv_stop_word
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t t_busy = t0, served = 0;
-  // a pass looks at the next 64 tickets (one load per lane) and, when all of them are ready
-  // (a backlog), at the next (SRV_PER - 1) x 64 too, all in flight together; it serves their
-  // ready prefix, up to SRV_PER requests per lane. Reads of host memory go out at ~30 ns each
-  // per wave (throughput, not latency, bound: polling 256 tickets took 7.6 us a pass, 64 take
-  // a quarter of that -- profiles/r06_async_submit.txt), so only a backlog pays for more.
+  // a pass looks at the next 64 slots (one word per lane) and, when all of them are ready (a
+  // backlog), at the next (SRV_PER - 1) x 64 too; it serves their ready prefix, up to SRV_PER
+  // requests per lane
   constexpr uint32_t SRV_PER = 4;
 #if RF_SRV_PROF
   uint64_t pf[6] = {0, 0, 0, 0, 0, 0};
@@ -3739,26 +3742,23 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
 #if RF_SRV_PROF
     const uint64_t pa = stamp();
 #endif
-    uint64_t tk[SRV_PER];
-    tk[0] = __hip_atomic_load(&pub[(uint32_t)((head + lane) & (SRV_RING - 1))], __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_SYSTEM);
-    // the host's stop word, read beside the tickets (in flight with them: no extra round trip),
-    // so a busy wave stops too (engine shutdown, a server marked dead)
-    uint64_t stp = lane == 0 ? __hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    uint64_t w0[SRV_PER];
+    w0[0] = srv_ld(&ring[(uint32_t)((head + lane) & (SRV_RING - 1))].w[0]);
+    // the host's stop word, read beside the requests (no extra round trip), so a busy wave
+    // stops too (engine shutdown, a server marked dead)
+    const uint64_t stp = lane == 0 ? srv_ld(stop_word) : 0ull;
     if (__shfl(stp, 0)) break;
-    uint32_t k;  // the ready prefix
+    uint32_t k;  // the ready prefix (word 0)
     {
-      const uint64_t ready = __builtin_amdgcn_ballot_w64(tk[0] == head + lane);
+      const uint64_t ready = __builtin_amdgcn_ballot_w64((uint32_t)(w0[0] >> 32) == srv_check(head + lane));
       k = ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
     }
     if (k == WAVE) {
 #pragma unroll
-      for (uint32_t m = 1; m < SRV_PER; m++)
-        tk[m] = __hip_atomic_load(&pub[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_SYSTEM);
+      for (uint32_t m = 1; m < SRV_PER; m++) w0[m] = srv_ld(&ring[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))].w[0]);
 #pragma unroll
       for (uint32_t m = 1; m < SRV_PER; m++) {
-        const uint64_t ready = __builtin_amdgcn_ballot_w64(tk[m] == head + lane + WAVE * m);
+        const uint64_t ready = __builtin_amdgcn_ballot_w64((uint32_t)(w0[m] >> 32) == srv_check(head + lane + WAVE * m));
         if (k == WAVE * m) k += ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
       }
     }
@@ -3766,62 +3766,112 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
 #if RF_SRV_PROF
       const uint64_t pb = stamp();
 #endif
-      // acquire (system scope) once per served pass, not per poll: the payloads after the
-      // tickets, and no stale cached device data (it invalidates this CU's L1 and the L2)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      ProbeGroup G[SRV_PER];
-      uint32_t h[SRV_PER];
-      uint64_t tg[SRV_PER];
+      // the rest of each ready request: every load in flight at once, then the prefix whose
+      // words all carry their check
+      uint64_t w[SRV_PER][SRV_REQ_WORDS];
 #pragma unroll
-      for (uint32_t m = 0; m < SRV_PER; m++) {  // every payload load first
+      for (uint32_t m = 0; m < SRV_PER; m++) {
         const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
+        w[m][0] = w0[m];
         if (i < k) {
-          G[m] = ring[slot].g;
-          h[m] = ring[slot].h;
-          tg[m] = ring[slot].tag;
+#pragma unroll
+          for (uint32_t q = 1; q < SRV_REQ_WORDS; q++) w[m][q] = srv_ld(&ring[slot].w[q]);
         }
       }
+      uint32_t k2 = k;
+#pragma unroll
+      for (uint32_t m = 0; m < SRV_PER; m++) {
+        const uint32_t i = lane + WAVE * m;
+        const uint32_t ck = srv_check(head + i);
+        bool ok = i < k;
+#pragma unroll
+        for (uint32_t q = 1; q < SRV_REQ_WORDS; q++) ok = ok && (uint32_t)(w[m][q] >> 32) == ck;
+        const uint64_t good = __builtin_amdgcn_ballot_w64(ok);
+        if (k2 == k && k > WAVE * m && good != ~0ull) k2 = WAVE * m + (uint32_t)__builtin_ctzll(~good);
+      }
+#if RF_SRV_PROF
+      if (k2 < k) pf[3] += 1;  // passes cut short by a request still arriving
+#endif
+      k = min(k, k2);
 #if RF_SRV_PROF
       const uint64_t pc = stamp();
 #endif
+      if (k) {
+        // acquire (system scope) once per served pass: no stale cached device data (it
+        // invalidates this CU's L1 and the L2)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        uint64_t found[SRV_PER];
 #pragma unroll
-      for (uint32_t m = 0; m < SRV_PER; m++) {
-        const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
-        if (i < k) {
-          __hip_atomic_store(&res[slot].found, probe_group(G[m], h[m]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(&res[slot].tag, tg[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (uint32_t m = 0; m < SRV_PER; m++) {
+          const uint32_t i = lane + WAVE * m;
+          found[m] = 0;
+          if (i < k) {
+            ProbeGroup G;
+            G.x = (uint32_t)w[m][0];
+            G.err = (uint32_t)w[m][1];
+            G.fpl = (uint32_t)w[m][2];
+            G.pad = 0;
+            const uint32_t h = (uint32_t)w[m][3];
+            G.lines = reinterpret_cast<const uint4*>((uint64_t)(uint32_t)w[m][4] | ((uint64_t)(uint32_t)w[m][5] << 32));
+            G.pages = reinterpret_cast<const uint8_t*>((uint64_t)(uint32_t)w[m][6] | ((uint64_t)(uint32_t)w[m][7] << 32));
+            G.slots = reinterpret_cast<const uint64_t*>((uint64_t)(uint32_t)w[m][8] | ((uint64_t)(uint32_t)w[m][9] << 32));
+            found[m] = probe_group(G, h);
+          }
         }
-      }
-      // the found and tag words (system-coherent stores to host memory, no cached copy to
-      // write back) have completed before any ticket is stored
-#if RF_SRV_PROF
-      const uint64_t pd = __builtin_amdgcn_s_memrealtime();
-#endif
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if RF_SRV_PROF
-      const uint64_t pe = __builtin_amdgcn_s_memrealtime();
-#endif
+#if RF_SRV_PAIRSTORE
+        // answers: lanes 2j and 2j+1 store the two 16-byte halves of answer j of a group of 32
+        // (found, then tag, each word with its check), so one store instruction writes 1 KB of
+        // consecutive answers -- whole 64-byte lines over PCIe instead of 8-byte partial writes
+        // (each of which the host's copy of the line would see arrive separately)
 #pragma unroll
-      for (uint32_t m = 0; m < SRV_PER; m++) {
-        const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
-        if (i < k) __hip_atomic_store(&res[slot].ticket, head + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-#if RF_SRV_PROF
-      const uint64_t pg = stamp();
-      pf[0] += pb - pa;
-      pf[1] += pc - pb;
-      pf[2] += pd - pc;
-      pf[3] += pe - pd;
-      pf[4] += pg - pe;
-      pf[5] += 1;
+        for (uint32_t r = 0; r < 2 * SRV_PER; r++) {
+          if (k > 32 * r) {  // wave-uniform
+            const uint32_t m = r >> 1, src = (r & 1) * 32 + (lane >> 1), a = 32 * r + (lane >> 1);
+            const uint32_t f0 = __shfl((uint32_t)found[m], src), f1 = __shfl((uint32_t)(found[m] >> 32), src);
+            const uint32_t g0 = __shfl((uint32_t)w[m][10], src), g1 = __shfl((uint32_t)w[m][11], src);
+            if (a < k) {
+              const uint64_t ck = (uint64_t)srv_check(head + a) << 32;
+              const uint64_t x = (uint64_t)((lane & 1) ? g0 : f0) | ck, y = (uint64_t)((lane & 1) ? g1 : f1) | ck;
+              uint64_t* dst = res[(uint32_t)((head + a) & (SRV_RING - 1))].w + (lane & 1) * 2;
+              typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+              const u64x2 v = {x, y};
+              // a system-scope store (sc0 sc1, as __hip_atomic_store emits for 8 bytes) of 16 bytes
+              asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+            }
+          }
+        }
+#else
+        // (A/B: each lane stores its own answer as four 8-byte words)
+#pragma unroll
+        for (uint32_t m = 0; m < SRV_PER; m++) {
+          const uint32_t i = lane + WAVE * m;
+          if (i < k) {
+            const uint64_t ck = (uint64_t)srv_check(head + i) << 32;
+            uint64_t* r = res[(uint32_t)((head + i) & (SRV_RING - 1))].w;
+            __hip_atomic_store(r + 0, (found[m] & 0xffffffffull) | ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(r + 1, (found[m] >> 32) | ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(r + 2, (uint64_t)(uint32_t)w[m][10] | ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(r + 3, (uint64_t)(uint32_t)w[m][11] | ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
 #endif
-      head += k;
-      served += k;
-      t_busy = __builtin_amdgcn_s_memrealtime();
-      if (t_busy - t0 > life_ticks) break;  // the lifetime bounds a busy wave too (waiters relaunch it)
-      continue;
+#if RF_SRV_PROF
+        const uint64_t pd = stamp();
+        pf[0] += pb - pa;
+        pf[1] += pc - pb;
+        pf[2] += pd - pc;
+        pf[4] += k;
+        pf[5] += 1;
+#endif
+        head += k;
+        served += k;
+        t_busy = __builtin_amdgcn_s_memrealtime();
+        if (t_busy - t0 > life_ticks) break;  // the lifetime bounds a busy wave too (waiters relaunch it)
+        continue;
+      }
+      // word 0 there, the rest still on its way: poll again
     }
-    // idle: poll the next ticket alone (one 8-byte PCIe read per poll), bounded by the clock
+    // idle: poll the next slot's word 0 alone, bounded by the clock
     bool stop = false;
     for (;;) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -3831,8 +3881,8 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
       }
       uint64_t t1 = 0, st = 0;
       if (lane == 0) {
-        t1 = __hip_atomic_load(&pub[head & (SRV_RING - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        st = __hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        t1 = srv_ld(&ring[head & (SRV_RING - 1)].w[0]);
+        st = srv_ld(stop_word);
       }
       t1 = __shfl(t1, 0);
       st = __shfl(st, 0);
@@ -3840,7 +3890,7 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
         stop = true;
         break;
       }
-      if (t1 == head) break;
+      if ((uint32_t)(t1 >> 32) == srv_check(head)) break;
       __builtin_amdgcn_s_sleep(2);
     }
     if (stop) break;

@@ -101,33 +101,37 @@ struct ProbeGroup {
   const uint64_t* slots;  // the filter's (relocatable) index slots
 };
 
-// The lookup server (k_lookup_server): single lookups travel through a ring of requests in
-// pinned coherent host memory that a persistent wave polls, instead of one kernel launch per
-// call. Request t sits in slot t % SRV_RING; the host writes the payload, then publishes t in
-// word t % SRV_RING of the dense ticket array after the ring (release); the server answers in
-// slot t of the result ring (found and tag, then ticket = t).
+// The lookup server (k_lookup_server): single lookups travel through a ring of requests that a
+// persistent wave polls, instead of one kernel launch per call. The ring lives in fine-grained
+// device memory that the host writes through its BAR mapping (posted writes; the wave polls its
+// own HBM: 0.09 us per 64-slot poll against 1.1-4.3 us for pinned host memory,
+// profiles/r06_ring_placement.txt), or in pinned host memory (RF_AMD_SRV_RING=host). The
+// host's stores reach the device in no particular order (a write-combining mapping), so every
+// 8-byte word of a request carries the request's check value in its high half and the server
+// serves a request only when all of its words do; answers are written the same way, so
+// neither side waits for the other's stores to complete before publishing.
+// Request t sits in slot t % SRV_RING; its check is t / SRV_RING + 1 (0: never written).
 constexpr uint32_t SRV_RING = 4096;
+constexpr uint32_t SRV_REQ_WORDS = 16;
+// payload u32 of word i: 0 x, 1 err, 2 fpl (ProbeGroup), 3 the key's hash, 4-5 lines, 6-7 pages,
+// 8-9 slots, 10-11 the submitter's tag (0: a waiter's ticket), 12-15 zero (two whole 64-byte
+// lines: a full write-combining buffer leaves the host at once)
 struct SrvReq {
-  ProbeGroup g;     // the filter (its own routing config)
-  uint32_t h;       // the key's 32-bit hash
-  uint32_t pad;
-  uint64_t tag;     // the submitter's tag (0: a waiter's ticket), handed back with the answer
-  uint64_t ticket;  // written last
+  uint64_t w[SRV_REQ_WORDS];
 };
-static_assert(sizeof(SrvReq) == 64, "one request per 64-byte line");
-// an answer carries its request's tag, so the reaping thread reads only answer lines (written
-// by the GPU) and no line a submitting thread wrote
+static_assert(sizeof(SrvReq) == 128, "one request per two 64-byte lines");
+// found lo, found hi, tag lo, tag hi (each | check << 32): an answer carries its request's tag,
+// so the reaping thread reads only answer lines (written by the GPU)
 struct SrvRes {
-  uint64_t found;
-  uint64_t ticket;  // written last
-  uint64_t tag;
-  uint64_t pad;
+  uint64_t w[4];
 };
 static_assert(sizeof(SrvRes) == 32, "two answers per 64-byte line");
-// control block (pinned coherent host memory): stop is set by the host; the server writes the
-// first ticket it did not serve, then its generation, when it exits
+__host__ __device__ inline uint32_t srv_check(uint64_t t) { return (uint32_t)(t / SRV_RING) + 1u; }
+// control block (pinned coherent host memory): the server writes the first ticket it did not
+// serve, then its generation, when it exits. (The host's stop word sits after the request ring,
+// where the wave polls it with the requests.)
 struct SrvCtl {
-  uint64_t stop;
+  uint64_t unused;
   uint64_t exit_head;
   uint64_t exit_gen;
   uint64_t served;
