@@ -149,7 +149,8 @@ int rf_amd_probe_many_hashes_host(rf_amd_engine *e, rf_amd_batch *const *batches
  * call. A persistent wave (started on demand on a queue of its own, exiting after 400 us
  * without requests and after an 800 us lifetime -- so a device-wide synchronisation waits at
  * most that long for it; relaunched while lookups continue) polls a ring of requests in
- * pinned host memory and
+ * device memory that the host writes through its BAR mapping (RF_AMD_SRV_RING=host: pinned
+ * host memory) and
  * answers each with filter filter_index of batch b, in submission order. submit queues the
  * lookup of `hash` and returns its ticket; the batch must stay alive until the result is
  * taken. A NULL tag: the caller takes the result with rf_amd_lookup_wait (blocking). A

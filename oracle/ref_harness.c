@@ -37,6 +37,7 @@
 #include <stdlib.h>
 #include <unistd.h>
 #include <pthread.h>
+#include <x86intrin.h>
 #include <sched.h>
 #include <signal.h>
 #include <stdatomic.h>
@@ -1276,6 +1277,10 @@ rfr_lookup_keys_async_driven(rfr_stack      *s,
    uint64 next = 0, done = 0, running = 0;
    double last = now_s();
    int    ret  = 0;
+   /* RFR_DRIVE_PROF=1 (diagnostics): TSC cycles of the driving loop's parts -- first calls,
+      the ready list's second calls, cleanup -- and iterations, printed to stderr */
+   const int prof = getenv("RFR_DRIVE_PROF") && atoi(getenv("RFR_DRIVE_PROF")) > 0;
+   uint64    pc[3] = {0, 0, 0}, iters = 0, firsts = 0, seconds = 0;
 #define FINISH(c)                                                                              \
    do {                                                                                        \
       found[(c)->i] = SUCCESS((c)->st.__async_result) ? found[(c)->i] : UINT64_MAX;            \
@@ -1286,7 +1291,10 @@ rfr_lookup_keys_async_driven(rfr_stack      *s,
       last = now_s();                                                                          \
    } while (0)
    while (done < n) {
+      const uint64 q0 = prof ? __rdtsc() : 0;
+      iters++;
       while (avail && next < n) {
+         firsts++;
          rfr_actx *c = avail;
          avail       = c->next;
          c->i        = next++;
@@ -1306,6 +1314,7 @@ rfr_lookup_keys_async_driven(rfr_stack      *s,
             running++;
          }
       }
+      const uint64 q1 = prof ? __rdtsc() : 0;
       pthread_mutex_lock(&d.mu);
       rfr_actx *r = d.ready;
       d.ready     = NULL;
@@ -1313,19 +1322,34 @@ rfr_lookup_keys_async_driven(rfr_stack      *s,
       while (r) {
          rfr_actx *c = r;
          r           = r->next;
+         seconds++;
          if (routing_filter_lookup_async(&c->st) == ASYNC_STATUS_DONE) {
             FINISH(c);
          } else {
             atomic_fetch_add(&d.violations, 1); /* called back, yet not resumable */
          }
       }
+      const uint64 q2 = prof ? __rdtsc() : 0;
       if (done < n && now_s() - last > timeout_s) {
          ret = -1;
          break;
       }
       cache_cleanup((cache *)&s->cc);
+      if (prof) {
+         const uint64 q3 = __rdtsc();
+         pc[0] += q1 - q0;
+         pc[1] += q2 - q1;
+         pc[2] += q3 - q2;
+      }
    }
 #undef FINISH
+   if (prof) {
+      fprintf(stderr,
+              "rfr drive profile: %lu iterations, %.2f first calls and %.2f second calls each; TSC cycles: "
+              "%.0f per first call, %.0f per second call (incl. ready list), %.0f cleanup per iteration\n",
+              (unsigned long)iters, (double)firsts / iters, (double)seconds / iters,
+              firsts ? (double)pc[0] / firsts : 0.0, seconds ? (double)pc[1] / seconds : 0.0, (double)pc[2] / iters);
+   }
    /* every callback owed has fired before the contexts go away */
    double t0 = now_s();
    while (atomic_load(&d.callbacks) < running && now_s() - t0 < timeout_s) {

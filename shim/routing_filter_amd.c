@@ -1586,6 +1586,8 @@ static uint64 g_reap_outstanding_sum, g_reap_outstanding_n;
 #define AQ_PIN(st) (*(shim_batch **)&(st)->filter_page)
 
 #define AQ_SERVER_MAX 64 /* server requests outstanding beyond which states are batched */
+/* first calls of this thread since one of its calls last returned DONE */
+static __thread uint32 g_tl_first_calls;
 static rf_state *g_bq_head;     /* the stack of batched states (atomic) */
 static uint64    g_bq_count;    /* states on it (atomic) */
 static uint64    g_bq_pending;  /* batched states not yet completed (atomic) */
@@ -1984,7 +1986,9 @@ static uint64 g_subprof_cyc[5], g_subprof_n;
 #define SUBPROF_MARK(i)                                                                            \
    uint64 sp_##i = 0;                                                                              \
    if (g_subprof > 0) {                                                                            \
+      _mm_lfence();                                                                                \
       sp_##i = __rdtsc();                                                                          \
+      _mm_lfence();                                                                                \
    }
 #define SUBPROF_DONE()                                                                             \
    if (g_subprof > 0) {                                                                            \
@@ -2024,6 +2028,7 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    }
    async_state at = __atomic_load_n(&state->__async_state_stack[0], __ATOMIC_ACQUIRE);
    if (at == ASYNC_STATE_DONE) {
+      g_tl_first_calls = 0;
       return ASYNC_STATUS_DONE;
    }
    if (at == ASYNC_STATE_QUEUED) {
@@ -2048,7 +2053,13 @@ routing_filter_lookup_async(routing_filter_lookup_async_state *state)
    SUBPROF_MARK(0);
    state->fp       = data_key_hash(state->cfg->data_cfg, state->target, state->cfg->seed);
    SUBPROF_MARK(1);
-   if (__atomic_load_n(&g_aq_outstanding, __ATOMIC_RELAXED) >= AQ_SERVER_MAX
+   /* a burst: more than AQ_SERVER_MAX first calls from this thread with no state of its
+      finished in between (a caller that keeps a bounded number in flight sees DONE between
+      its submissions; one that submits thousands and polls later does not). With the server
+      answering in a few microseconds the outstanding count alone stays low through such a
+      burst, and every state would pay a ring submission instead of a stack push */
+   const int burst = ++g_tl_first_calls > AQ_SERVER_MAX;
+   if (burst || __atomic_load_n(&g_aq_outstanding, __ATOMIC_RELAXED) >= AQ_SERVER_MAX
        || __atomic_load_n(&g_bq_pending, __ATOMIC_RELAXED))
    {
       /* a burst (the server's share is full, or batched states are still in flight: the

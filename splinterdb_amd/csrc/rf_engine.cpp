@@ -233,6 +233,7 @@ struct LookupServer {
 
 struct rf_amd_engine {
   int device;
+  uint64_t uid = 0;  // unique per engine created in this process (per-thread caches key on it)
   LookupServer srv;
   // completion points on the engine stream (rf_amd_engine_fence): recycled events
   std::mutex fence_mu;
@@ -376,6 +377,8 @@ extern "C" int rf_amd_engine_create(int device, rf_amd_engine** out) {
   if (device < 0 || device >= n) return fail(RF_AMD_EINVAL, "bad device ordinal");
   HIPCHK(hipSetDevice(device));
   auto* e = new rf_amd_engine();
+  static std::atomic<uint64_t> next_uid{1};
+  e->uid = next_uid.fetch_add(1);
   e->device = device;
   {
     // default: a quarter of the memory free at engine creation (~62 GB on an idle MI355X);
@@ -1590,6 +1593,35 @@ static bool srv_reap_tail() {
   }();
   return on;
 }
+// the request's 16 words (payload | check << 32) into its slot. Each 8-byte word is valid on
+// its own, so wider stores are as safe as 8-byte ones: RF_AMD_SRV_STORE = 8 (eight-byte
+// stores), 16 (SSE, the default) or 32 (AVX) -- an A/B switch
+static int srv_store_width() {
+  static const int w = [] {
+    const char* s = getenv("RF_AMD_SRV_STORE");
+    const int v = s ? atoi(s) : 16;
+    return v == 8 || v == 32 ? v : 16;
+  }();
+  return w;
+}
+__attribute__((target("avx2"))) static void srv_write_request_avx(uint64_t* dst, const uint64_t* src) {
+  for (uint32_t k = 0; k < SRV_REQ_WORDS; k += 4)
+    _mm256_store_si256(reinterpret_cast<__m256i*>(dst + k), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + k)));
+}
+static inline void srv_write_request(uint64_t* dst, const uint32_t* p, uint64_t ck) {
+  alignas(32) uint64_t w[SRV_REQ_WORDS];
+  for (uint32_t k = 0; k < SRV_REQ_WORDS; k++) w[k] = (uint64_t)p[k] | ck;
+  const int width = srv_store_width();
+  if (width == 8) {
+    volatile uint64_t* d = dst;
+    for (uint32_t k = 0; k < SRV_REQ_WORDS; k++) d[k] = w[k];
+  } else if (width == 16) {
+    for (uint32_t k = 0; k < SRV_REQ_WORDS; k += 2)
+      _mm_store_si128(reinterpret_cast<__m128i*>(dst + k), _mm_load_si128(reinterpret_cast<const __m128i*>(w + k)));
+  } else {
+    srv_write_request_avx(dst, w);
+  }
+}
 // RF_AMD_SRV_SFENCE=1: an sfence after each request (A/B switch: whole lines leave the
 // write-combining buffers without one)
 static bool srv_sfence() {
@@ -1604,6 +1636,14 @@ static bool srv_sfence() {
 // checks, ticket + slot wait, request write, server check -- printed to stderr at exit
 static int g_subprof = -1;
 static uint64_t g_subprof_cyc[7], g_subprof_n;
+// a TSC stamp that waits for the loads before it (lfence on both sides): each step's misses
+// land in its own interval
+static inline uint64_t tsc_ser() {
+  _mm_lfence();
+  const uint64_t t = __rdtsc();
+  _mm_lfence();
+  return t;
+}
 // the reaper's side (one completion thread in the profiled runs): TSC cycles of reaps that
 // returned states -- the idle look at the next answer, lock + cursor, the answer loop -- and
 // the states they returned
@@ -1639,20 +1679,21 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     g_subprof = pv && atoi(pv) > 0;
     if (g_subprof) atexit(subprof_print);
   }
-  const uint64_t c0 = g_subprof > 0 ? __rdtsc() : 0;
+  const uint64_t c0 = g_subprof > 0 ? tsc_ser() : 0;
   if (!e) return fail(RF_AMD_ENODEV, "no engine");
   if (g_subprof > 0) g_subprof_eng = e;
   if (!b || !b->built || b->eng != e) return fail(RF_AMD_EINVAL, "lookup on an unbuilt or foreign batch");
   if (filter_index >= b->F) return fail(RF_AMD_EINVAL, "bad filter index");
   if (!ticket) return fail(RF_AMD_EINVAL, "null ticket");
-  const uint64_t c0a = g_subprof > 0 ? __rdtsc() : 0;
-  if (int rc = srv_init(e)) return rc;
-  const uint64_t c0b = g_subprof > 0 ? __rdtsc() : 0;
+  const uint64_t c0a = g_subprof > 0 ? tsc_ser() : 0;
+  if (__builtin_expect(!e->srv.ready.load(std::memory_order_acquire), 0))
+    if (int rc = srv_init(e)) return rc;
+  const uint64_t c0b = g_subprof > 0 ? tsc_ser() : 0;
   if (int rc = batch_errors(b)) return rc;
-  const uint64_t c0c = g_subprof > 0 ? __rdtsc() : 0;
+  const uint64_t c0c = g_subprof > 0 ? tsc_ser() : 0;
   if (int rc = srv_dead(e)) return rc;
   LookupServer& v = e->srv;
-  const uint64_t c1 = g_subprof > 0 ? __rdtsc() : 0;
+  const uint64_t c1 = g_subprof > 0 ? tsc_ser() : 0;
   const uint64_t t = v.tail.fetch_add(1, std::memory_order_acq_rel);
   const uint32_t slot = (uint32_t)(t & (SRV_RING - 1));
   if (t >= SRV_RING) {
@@ -1660,9 +1701,22 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     // reap cursor passed it, having copied its answer out), by its waiter (consumed), or never
     // published (abandoned)
     const uint64_t p = t - SRV_RING;
+    // the reap cursor only moves forward, and it is usually ~64 tickets behind the tail, far
+    // past p = t - SRV_RING: a submitting thread re-reads it (a line the reaper writes on every
+    // reap) only when its last look does not already show p reaped
+    static thread_local uint64_t hint_uid = 0, hint_seen = 0;
+    if (hint_uid != e->uid) {
+      hint_uid = e->uid;
+      hint_seen = 0;
+    }
+    auto reaped = [&] {
+      if (hint_seen > p) return true;
+      hint_seen = v.reap_hint.load(std::memory_order_acquire);
+      return hint_seen > p;
+    };
     auto taken = [&] {
       if (v.consumed[slot].load(std::memory_order_acquire) == p + 1) return true;
-      if (v.reap_hint.load(std::memory_order_acquire) <= p) return false;
+      if (!reaped()) return false;
       if (v.abandoned[slot].load(std::memory_order_acquire) == p) return true;
       return v.meta[slot].ticket.load(std::memory_order_acquire) == p && v.meta[slot].tag != nullptr;
     };
@@ -1683,7 +1737,7 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     v.meta[slot].ticket.store(SRV_BUSY, std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_release);  // BUSY before the new tag (a seqlock)
   }
-  const uint64_t c2 = g_subprof > 0 ? __rdtsc() : 0;
+  const uint64_t c2 = g_subprof > 0 ? tsc_ser() : 0;
   {
     // 16 words, each with t's check in its high half; plain 8-byte stores in any order (two
     // whole 64-byte lines: through the write-combining BAR mapping they leave as two bursts)
@@ -1695,18 +1749,17 @@ extern "C" int rf_amd_lookup_submit(rf_amd_engine* e, rf_amd_batch* b, uint32_t 
     v.meta[slot].tag = tag;
     v.meta[slot].ticket.store(t, std::memory_order_release);
     const uint64_t ck = (uint64_t)srv_check(t) << 32;
-    volatile uint64_t* w = v.ring[slot].w;
-    for (uint32_t k = 0; k < SRV_REQ_WORDS; k++) w[k] = (uint64_t)p[k] | ck;
+    srv_write_request(v.ring[slot].w, p, ck);
     if (srv_sfence()) _mm_sfence();
   }
   *ticket = t;
-  const uint64_t c3 = g_subprof > 0 ? __rdtsc() : 0;
+  const uint64_t c3 = g_subprof > 0 ? tsc_ser() : 0;
   // published: from here the ticket's tag comes back through rf_amd_lookup_reap or, if the
   // server is (or now becomes) dead, rf_amd_lookup_server_failed -- so a launch failure here is
   // not the submit's error (the caller would complete the state a second time)
   (void)srv_ensure(e);
   if (g_subprof > 0) {  // one submitting thread in the profiled runs: plain sums
-    const uint64_t c4 = __rdtsc();
+    const uint64_t c4 = tsc_ser();
     g_subprof_cyc[0] += c1 - c0;
     g_subprof_cyc[4] += c0a - c0;
     g_subprof_cyc[5] += c0b - c0a;

@@ -3731,6 +3731,7 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
   // backlog), at the next (SRV_PER - 1) x 64 too; it serves their ready prefix, up to SRV_PER
   // requests per lane
   constexpr uint32_t SRV_PER = 4;
+  constexpr uint32_t SRV_USED = 12;  // request words 12-15 are padding
 #if RF_SRV_PROF
   uint64_t pf[6] = {0, 0, 0, 0, 0, 0};
   auto stamp = [] {
@@ -3742,61 +3743,46 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
 #if RF_SRV_PROF
     const uint64_t pa = stamp();
 #endif
-    uint64_t w0[SRV_PER];
-    w0[0] = srv_ld(&ring[(uint32_t)((head + lane) & (SRV_RING - 1))].w[0]);
+    // every used word of the next 64 slots in one round trip (device memory: ~0.1-0.3 us);
+    // a slot is ready when all of its words carry its ticket's check
+    uint64_t w[SRV_PER][SRV_USED];
+#pragma unroll
+    for (uint32_t q = 0; q < SRV_USED; q++) w[0][q] = srv_ld(&ring[(uint32_t)((head + lane) & (SRV_RING - 1))].w[q]);
     // the host's stop word, read beside the requests (no extra round trip), so a busy wave
     // stops too (engine shutdown, a server marked dead)
     const uint64_t stp = lane == 0 ? srv_ld(stop_word) : 0ull;
     if (__shfl(stp, 0)) break;
-    uint32_t k;  // the ready prefix (word 0)
+    uint32_t k;  // the ready prefix
     {
-      const uint64_t ready = __builtin_amdgcn_ballot_w64((uint32_t)(w0[0] >> 32) == srv_check(head + lane));
+      const uint32_t ck = srv_check(head + lane);
+      bool ok = true;
+#pragma unroll
+      for (uint32_t q = 0; q < SRV_USED; q++) ok = ok && (uint32_t)(w[0][q] >> 32) == ck;
+      const uint64_t ready = __builtin_amdgcn_ballot_w64(ok);
       k = ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
     }
-    if (k == WAVE) {
+    if (k == WAVE) {  // a backlog: the next (SRV_PER - 1) x 64 slots too, all in flight together
 #pragma unroll
-      for (uint32_t m = 1; m < SRV_PER; m++) w0[m] = srv_ld(&ring[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))].w[0]);
+      for (uint32_t m = 1; m < SRV_PER; m++)
+#pragma unroll
+        for (uint32_t q = 0; q < SRV_USED; q++)
+          w[m][q] = srv_ld(&ring[(uint32_t)((head + lane + WAVE * m) & (SRV_RING - 1))].w[q]);
 #pragma unroll
       for (uint32_t m = 1; m < SRV_PER; m++) {
-        const uint64_t ready = __builtin_amdgcn_ballot_w64((uint32_t)(w0[m] >> 32) == srv_check(head + lane + WAVE * m));
+        const uint32_t ck = srv_check(head + lane + WAVE * m);
+        bool ok = true;
+#pragma unroll
+        for (uint32_t q = 0; q < SRV_USED; q++) ok = ok && (uint32_t)(w[m][q] >> 32) == ck;
+        const uint64_t ready = __builtin_amdgcn_ballot_w64(ok);
         if (k == WAVE * m) k += ready == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~ready);
       }
     }
     if (k) {
 #if RF_SRV_PROF
       const uint64_t pb = stamp();
+      const uint64_t pc = pb;
 #endif
-      // the rest of each ready request: every load in flight at once, then the prefix whose
-      // words all carry their check
-      uint64_t w[SRV_PER][SRV_REQ_WORDS];
-#pragma unroll
-      for (uint32_t m = 0; m < SRV_PER; m++) {
-        const uint32_t i = lane + WAVE * m, slot = (uint32_t)((head + i) & (SRV_RING - 1));
-        w[m][0] = w0[m];
-        if (i < k) {
-#pragma unroll
-          for (uint32_t q = 1; q < SRV_REQ_WORDS; q++) w[m][q] = srv_ld(&ring[slot].w[q]);
-        }
-      }
-      uint32_t k2 = k;
-#pragma unroll
-      for (uint32_t m = 0; m < SRV_PER; m++) {
-        const uint32_t i = lane + WAVE * m;
-        const uint32_t ck = srv_check(head + i);
-        bool ok = i < k;
-#pragma unroll
-        for (uint32_t q = 1; q < SRV_REQ_WORDS; q++) ok = ok && (uint32_t)(w[m][q] >> 32) == ck;
-        const uint64_t good = __builtin_amdgcn_ballot_w64(ok);
-        if (k2 == k && k > WAVE * m && good != ~0ull) k2 = WAVE * m + (uint32_t)__builtin_ctzll(~good);
-      }
-#if RF_SRV_PROF
-      if (k2 < k) pf[3] += 1;  // passes cut short by a request still arriving
-#endif
-      k = min(k, k2);
-#if RF_SRV_PROF
-      const uint64_t pc = stamp();
-#endif
-      if (k) {
+      {
         // acquire (system scope) once per served pass: no stale cached device data (it
         // invalidates this CU's L1 and the L2)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -3869,7 +3855,6 @@ __global__ __launch_bounds__(WAVE) void k_lookup_server(const SrvReq* __restrict
         if (t_busy - t0 > life_ticks) break;  // the lifetime bounds a busy wave too (waiters relaunch it)
         continue;
       }
-      // word 0 there, the rest still on its way: poll again
     }
     // idle: poll the next slot's word 0 alone, bounded by the clock
     bool stop = false;
