@@ -46,6 +46,11 @@ int rf_amd_diag_lookup_stats(uint64_t *out, int reset);
  * ticket the last exited server did not serve */
 int rf_amd_lookup_server_stats(rf_amd_engine *e, uint64_t *out);
 
+/* where the engine's lookup server keeps its request ring: 1 device memory written through the
+ * BAR, 0 pinned host memory (RF_AMD_SRV_RING=host, or a box whose BAR mapping failed the
+ * check), -1 no server yet */
+int rf_amd_diag_lookup_ring(rf_amd_engine *e);
+
 /* stops the engine's lookup server (its wave exits; relaunched waves exit at once) and, gap_us
  * microseconds later, marks it dead with error `err`, exactly as a failed launch or a faulted
  * server stream does: tickets published in the gap are never answered (tests of the error

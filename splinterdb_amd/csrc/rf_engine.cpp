@@ -1931,6 +1931,11 @@ extern "C" int rf_amd_lookup_server_set_times(rf_amd_engine* e, uint64_t idle_us
   return 0;
 }
 
+extern "C" int rf_amd_diag_lookup_ring(rf_amd_engine* e) {
+  if (!e || !e->srv.ready.load(std::memory_order_acquire)) return -1;
+  return e->srv.ring_dev ? 1 : 0;
+}
+
 extern "C" int rf_amd_lookup_server_stats(rf_amd_engine* e, uint64_t* out) {
   if (!e || !out) return fail(RF_AMD_EINVAL, "null argument");
   out[0] = e->srv.tail.load();

@@ -55,7 +55,7 @@ EXPORTED = [
     "rf_amd_probe_filters_host", "rf_amd_engine_pool_trim", "rf_amd_engine_stream", "rf_amd_engine_sync",
     "rf_amd_batch_device_bytes", "rf_amd_batch_trim", "rf_amd_batch_stage_begin", "rf_amd_batch_stage_build",
     "rf_amd_batch_stage_abort", "rf_amd_lookup_server_error", "rf_amd_lookup_server_failed",
-    "rf_amd_lookup_server_set_times", "rf_amd_diag_lookup_server_kill",
+    "rf_amd_lookup_server_set_times", "rf_amd_diag_lookup_server_kill", "rf_amd_diag_lookup_ring",
 ]
 ROUTE_MAX_WORLD = 16
 ASYNC_STATUS_RUNNING = 0  # src/platform_linux/async.h:137-140
@@ -156,6 +156,7 @@ def load_library(build_if_missing=True):
     L.rf_amd_lookup_server_failed.restype = u64
     L.rf_amd_lookup_server_set_times.argtypes = [vp, u64, u64]
     L.rf_amd_diag_lookup_server_kill.argtypes = [vp, i32, u32]
+    L.rf_amd_diag_lookup_ring.argtypes = [vp]
     L.rf_amd_batch_num_filters.argtypes = [vp]
     L.rf_amd_batch_num_filters.restype = u32
     L.rf_amd_filter_add.argtypes = [vp, ctypes.POINTER(RfConfig), ctypes.POINTER(RfImage),

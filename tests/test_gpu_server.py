@@ -1,5 +1,6 @@
 """The engine's lookup server (rf_amd_lookup_submit / _wait / _reap, k_lookup_server): single
-lookups answered by a persistent wave that polls a ring in pinned host memory. Every answer
+lookups answered by a persistent wave that polls a ring of requests in device memory written
+by the host through the BAR (or in pinned host memory, RF_AMD_SRV_RING=host). Every answer
 must equal the batch probe's (k_probe) for the same filter and hash, through the waiting and
 the reaping forms, from several threads at once, across the wave's idle exit and relaunch,
 and after the batch's device memory was reused by another build while the wave kept running
@@ -324,4 +325,47 @@ def test_dead_server_returns_every_tag():
     assert lib().rf_amd_lookup_submit(eng.h, b.h, 0, 1, 1, ctypes.byref(t)) != 0
     b.close(stream().cuda_stream)
     sync()
+    eng.close()
+
+
+@pytest.mark.parametrize("placement", ["device", "host"])
+def test_ring_placements_equal_batch_probe(placement, monkeypatch):
+    """both request-ring placements (device memory written through the BAR: the default; pinned
+    host memory: RF_AMD_SRV_RING=host) answer every lookup as the batch probe does, through the
+    waiting and the reaping forms, on an engine of their own"""
+    if placement == "host":
+        monkeypatch.setenv("RF_AMD_SRV_RING", "host")
+    else:
+        monkeypatch.delenv("RF_AMD_SRV_RING", raising=False)
+    eng = E.Engine(0)
+    cfg = E.routing_config_init(log_index_size=8)
+    sizes, values = [50_000, 20_000], [2, 7]
+    rng = np.random.default_rng(11)
+    h = rng.integers(0, 1 << 32, size=sum(sizes), dtype=np.uint64).astype(np.uint32)
+    with torch.cuda.stream(stream()):
+        b = E.FilterBatch(cfg, sizes, values, engine=eng)
+        b.build_hashes(torch.from_numpy(h.view(np.int32)).to("cuda:0"))
+    sync()
+    fid, ph = probes(h, sizes, 3000, seed=12)
+    want = batch_probe(b, ph, fid)
+    got = np.array([wait(b, submit(b, fid[i], ph[i], None)) for i in range(500)], dtype=np.uint64)
+    assert (got == want[:500]).all()
+    lib().rf_amd_diag_lookup_ring.argtypes = [ctypes.c_void_p]
+    assert lib().rf_amd_diag_lookup_ring(eng.h) == (1 if placement == "device" else 0)
+    res = {}
+    done = threading.Event()
+
+    def reaper():
+        res.update(reap_all(eng, 2500))
+        done.set()
+
+    th = threading.Thread(target=reaper)
+    th.start()
+    for i in range(500, 3000):
+        submit(b, fid[i], ph[i], i + 1)
+    th.join(60)
+    assert done.is_set()
+    got = np.array([res[i + 1] for i in range(500, 3000)], dtype=np.uint64)
+    assert (got == want[500:]).all()
+    b.close(stream().cuda_stream)
     eng.close()
