@@ -1,10 +1,10 @@
 #!/bin/bash
-# r06 session 2, call 14: final validation -- full GPU suite (incl. both ring placements), smoke,
+# r06 session 3, call 1: final validation -- full GPU suite (incl. both ring placements), smoke,
 # the default bench
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r06s2n
+O=gpurun_out/r06s3a
 mkdir -p $O
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log; grep "ring_placements" $O/tests.log
