@@ -226,6 +226,59 @@ __global__ __launch_bounds__(NT) void k_floor(const uint8_t* __restrict__ keys, 
   for (int t = 0; t < ILP; t++) __builtin_nontemporal_store((uint64_t)acc[t], out + wf + t * WAVE + lane);
 }
 
+// Table-part split (round 6, priced in DESIGN §12 first): the probes of each filter gathered in
+// NPART passes, pass p gathering only the lines of the p-th part of the table (top bits of the
+// hash), so each XCD's L2 holds 1/NPART of its table at a time. Pass 0 stages and hashes the
+// keys and writes the 4-B hashes; passes p > 0 read them back. Lanes outside the pass's part
+// issue no gather and store nothing (masked 8-B stores).
+template <int NPART>
+__global__ __launch_bounds__(NT) void k_split(const uint8_t* __restrict__ keys, const uint8_t* __restrict__ table,
+                                              uint64_t tbytes, uint64_t ppf, uint64_t n, uint64_t* __restrict__ out,
+                                              uint32_t* __restrict__ hbuf, uint32_t pass) {
+  __shared__ v4u s[NT / WAVE][(KSTRIDE * 3 + 1024) / 16 + 1];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x) / WAVE;
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t wf = ((uint64_t)xcd_chunk(blockIdx.x, gridDim.x) * (NT / WAVE) + wv) * WAVE;
+  if (wf >= n) return;
+  const uint8_t* fb = table + (wf / ppf) * tbytes;
+  const uint32_t nlines = (uint32_t)(tbytes / 64);
+  uint32_t h;
+  if (pass == 0) {
+    const uint8_t* kb = keys + wf * 24;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + lane * 16),
+                                     (__attribute__((address_space(3))) void*)&s[wv][0], 16, 0, 2);
+    if (lane < 32)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void*)&s[wv][WAVE], 16, 0, 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync_lds();
+    const uint2* k2 = reinterpret_cast<const uint2*>(&s[wv][0]) + 3 * lane;
+    const uint2 a = k2[0], b = k2[1], c = k2[2];
+    const uint32_t w[6] = {a.x, a.y, b.x, b.y, c.x, c.y};
+    h = hash6<0>(w);
+    if (NPART > 1) __builtin_nontemporal_store(h, hbuf + wf + lane);
+    wave_sync_lds();  // every lane's key read before the lines land over them
+  } else {
+    h = __builtin_nontemporal_load(hbuf + wf + lane);
+  }
+  const uint32_t lo = __umulhi(h, nlines) * 64, q = lane & 3;
+  const uint32_t act = (NPART == 1 || __umulhi(h, NPART) == pass) ? 1u : 0u;
+  uint8_t* sb = reinterpret_cast<uint8_t*>(&s[wv][0]);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t lk = bcast<4>(lo, k), ak = bcast<4>(act, k);
+    if (ak)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(fb + lk + q * 16),
+                                       (__attribute__((address_space(3))) void*)(sb + k * KSTRIDE), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wave_sync_lds();
+  if (act) {
+    const v4u E = *reinterpret_cast<const v4u*>(sb + (lane & 3) * KSTRIDE + (lane >> 2) * 64);
+    __builtin_nontemporal_store((uint64_t)(h ^ E[0] ^ E[1] ^ E[2] ^ E[3]), out + wf + lane);
+  }
+}
+
 __global__ void k_fill(uint32_t* p, uint64_t nw, uint64_t salt) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t x = (i + salt) * 0x9e3779b97f4a7c15ull;
@@ -241,6 +294,26 @@ float run(const Ctx& c, int reps) {
   const uint64_t per_blk = (uint64_t)NT * ILP;
   dim3 g((unsigned)((c.n + per_blk - 1) / per_blk));
   auto L = [&]() { hipLaunchKernelGGL((k_floor<LW, GM, ILP, KM, HS>), g, dim3(NT), 0, 0, c.keys, c.table, c.T, c.ppf, c.n, c.out); };
+  L(); L();
+  CK(hipGetLastError());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; r++) L();
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipEventDestroy(e0)); CK(hipEventDestroy(e1));
+  return ms / reps;
+}
+
+template <int NPART>
+float run_split(const Ctx& c, uint32_t* hbuf, int reps) {
+  dim3 g((unsigned)((c.n + NT - 1) / NT));
+  auto L = [&]() {
+    for (uint32_t p = 0; p < NPART; p++)
+      hipLaunchKernelGGL((k_split<NPART>), g, dim3(NT), 0, 0, c.keys, c.table, c.T, c.ppf, c.n, c.out, hbuf, p);
+  };
   L(); L();
   CK(hipGetLastError());
   hipEvent_t e0, e1;
@@ -278,6 +351,19 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const int set = getenv("FB_SET") ? atoi(getenv("FB_SET")) : 0;
+  if (set == 2) {  // table-part split: NPART passes, each gathering one part of every table
+    uint32_t* hbuf;
+    CK(hipMalloc(&hbuf, n * 4));
+    P("LW64 quad LDS-DMA (k_probe_floor)", run<64, 0, 1, 0, 0>(c, reps));
+    P("split 1 part (same kernel, no hash buffer)", run_split<1>(c, hbuf, reps));
+    P("split 2 parts", run_split<2>(c, hbuf, reps));
+    P("split 3 parts", run_split<3>(c, hbuf, reps));
+    P("split 4 parts", run_split<4>(c, hbuf, reps));
+    P("LW0  keys LDS-DMA, no line", run<0, 0, 1, 0, 0>(c, reps));
+    P("LW0  hashes in, no line", run<0, 0, 1, 2, 0>(c, reps));
+    CK(hipFree(hbuf));
+    return 0;
+  }
   if (set == 1) {  // round-6 second pass: line width, ILP within the LDS budget, 128-B lines
     P("LW0  keys LDS-DMA, no line", run<0, 0, 1, 0, 0>(c, reps));
     P("LW64 quad LDS-DMA (k_probe_floor)", run<64, 0, 1, 0, 0>(c, reps));

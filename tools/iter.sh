@@ -1,14 +1,11 @@
 #!/bin/bash
-# r06 session 3, call 1: final validation -- full GPU suite (incl. both ring placements), smoke,
-# the default bench
+# r06 session 3, call 2: table-part split of the probe floor (tools/floor_bench.hip FB_SET=2)
+# at C2's and C3's shapes
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r06s3a
+O=gpurun_out/r06s3b
 mkdir -p $O
-timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { echo tests failed; tail -30 $O/tests.log; exit 1; }
-tail -1 $O/tests.log; grep "ring_placements" $O/tests.log
-timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; cat $O/smoke.log; exit 1; }
-cat $O/smoke.log
-timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
-python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['probe_floor'], d['verified'])"
+FB_SET=2 timeout -k 10 120 ./tools/floor_bench $((64<<20)) 8 8388608 "C2 shape" > $O/split.txt 2>&1 || { echo c2 failed; cat $O/split.txt; exit 1; }
+FB_SET=2 timeout -k 10 180 ./tools/floor_bench $((256<<20)) 256 2097152 "C3 shape" >> $O/split.txt 2>&1 || { echo c3 failed; cat $O/split.txt; exit 1; }
+cat $O/split.txt
