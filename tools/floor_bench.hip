@@ -102,7 +102,7 @@ __global__ __launch_bounds__(NT) void k_floor(const uint8_t* __restrict__ keys, 
                                               uint64_t tbytes, uint64_t ppf, uint64_t n,
                                               uint64_t* __restrict__ out) {
   constexpr int G = LW / 16 > 0 ? LW / 16 : 1;  // lanes per line
-  constexpr int KBUF = KM == 0 ? 96 : 0;         // v4u per tile for keys
+  constexpr int KBUF = (KM == 0 || KM == 3) ? 96 : 0;         // v4u per tile for keys
   constexpr int LBUF = (GM == 0 && LW > 0) ? (int)((KSTRIDE * (G - 1) + 1024) / 16 + 1) : 0;
   // the lines land over the keys' staging (read into registers before the lines are requested), as
   // in k_probe's fast path
@@ -117,7 +117,22 @@ __global__ __launch_bounds__(NT) void k_floor(const uint8_t* __restrict__ keys, 
   const uint32_t nlines = (uint32_t)(tbytes / (LW > 0 ? LW : 1));
   uint32_t h[ILP];
   // 1. keys (or hashes) of every tile
-  if constexpr (KM == 0) {
+  if constexpr (KM == 3) {
+    // diagnostic: the same key traffic (LDS-DMA into the tile's buffer), but the line addresses
+    // come from the probe index, so the gathers are issued without waiting for the keys (the
+    // buffer's bytes are garbage; only the traffic and the timing matter)
+#pragma unroll
+    for (int t = 0; t < ILP; t++) {
+      const uint8_t* kb = keys + (wf + t * WAVE) * 24;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + lane * 16),
+                                       (__attribute__((address_space(3))) void*)&s[wv][t][0], 16, 0, 2);
+      if (lane < 32)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void*)&s[wv][t][WAVE], 16, 0, 2);
+      const uint32_t w[6] = {(uint32_t)(wf + t * WAVE + lane), 0x1234567u, 0, 0, 0, 0};
+      h[t] = hash6<0>(w);
+    }
+  } else if constexpr (KM == 0) {
 #pragma unroll
     for (int t = 0; t < ILP; t++) {
       const uint8_t* kb = keys + (wf + t * WAVE) * 24;
@@ -359,6 +374,8 @@ int main(int argc, char** argv) {
     P("split 2 parts", run_split<2>(c, hbuf, reps));
     P("split 3 parts", run_split<3>(c, hbuf, reps));
     P("split 4 parts", run_split<4>(c, hbuf, reps));
+    P("LW64 quad LDS-DMA, gathers not waiting on keys", run<64, 0, 1, 3, 0>(c, reps));
+    P("LW64 quad LDS-DMA, hashes in", run<64, 0, 1, 2, 0>(c, reps));
     P("LW0  keys LDS-DMA, no line", run<0, 0, 1, 0, 0>(c, reps));
     P("LW0  hashes in, no line", run<0, 0, 1, 2, 0>(c, reps));
     CK(hipFree(hbuf));
